@@ -1,0 +1,215 @@
+/* abcd_hip.h -- C ABI of the MI355X (gfx950) ABCD-VAE training path.
+ *
+ * libabcd_hip.so implements the hot path of the reference trainer
+ * (ABCD-VAE/learning.py:147-163: encoder -> sampler -> KL -> decoder -> loss ->
+ * backward -> clip_grad_norm_ -> SGD) as hand-written HIP kernels for CDNA4.
+ * The reference has no native plugin boundary: its hot path sits behind
+ * PyTorch nn.Module methods.  Each entry point below replaces one of those
+ * methods (cited per function); the reference-side ctypes binding a
+ * maintainer would add is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - every pointer is DEVICE memory unless marked HOST;
+ *   - all floating point is IEEE fp32 (the reference trains in fp32);
+ *   - the packed layout is PyTorch's PackedSequence: rows are time-major,
+ *     step t owns rows [off_t, off_t + batch_sizes[t]), batch_sizes is
+ *     non-increasing and lives on the HOST (as in PackedSequence);
+ *   - `stream` is a hipStream_t (void* here to keep this header HIP-free);
+ *     every call is asynchronous and stream-ordered, no host synchronisation;
+ *   - the caller owns all memory; `ws` is a caller-allocated workspace of at
+ *     least *_workspace_bytes(); the SAME workspace must be passed to the
+ *     backward of a module as to its forward (it holds the activation stash);
+ *   - return value: 0 on success, a hipError_t code, or ABCD_EINVAL for
+ *     unsupported shapes/arguments.  Nothing throws across this ABI.
+ *
+ * Shape support: hidden sizes, MLP width, codebook dim, #categories, speaker
+ * embedding dim and the plain feature size must be multiples of 16; the
+ * frequency-bin count F is arbitrary (padded internally); encoder layers <= 4.
+ */
+#ifndef ABCD_HIP_H
+#define ABCD_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ABCD_EINVAL 1000
+#define ABCD_MAX_LAYERS 4
+
+enum abcd_rnn_type { ABCD_LSTM = 0, ABCD_GRU = 1 };
+
+typedef struct abcd_rnn_w { const float *w_ih, *w_hh, *b_ih, *b_hh; } abcd_rnn_w;
+typedef struct abcd_rnn_g { float *w_ih, *w_hh, *b_ih, *b_hh; } abcd_rnn_g;
+typedef struct abcd_mlp_w { const float *w1, *b1, *w2, *b2; } abcd_mlp_w; /* Linear->Tanh->Linear */
+typedef struct abcd_mlp_g { float *w1, *b1, *w2, *b2; } abcd_mlp_g;
+
+/* A packed batch (torch.nn.utils.rnn.PackedSequence): data is L x F. */
+typedef struct abcd_packed {
+  const float* data;          /* L x F, may be NULL for the decoder without ground truth */
+  const int64_t* batch_sizes; /* HOST, T entries */
+  int T, L, B, F;
+} abcd_packed;
+
+/* ------------------------------------------------------------------------
+ * Encoder: RNN_Variational_Encoder (ABCD-VAE/modules/model.py:40-66)
+ * ---------------------------------------------------------------------- */
+typedef struct abcd_encoder_cfg {
+  int input_size, hidden_size, rnn_type, layers, bidirectional;
+} abcd_encoder_cfg;
+typedef struct abcd_encoder_params { abcd_rnn_w w[ABCD_MAX_LAYERS][2]; } abcd_encoder_params;
+typedef struct abcd_encoder_grads { abcd_rnn_g g[ABCD_MAX_LAYERS][2]; } abcd_encoder_grads;
+
+/* hidden_size_total of model.py:54-58 */
+int abcd_encoder_out_size(const abcd_encoder_cfg* cfg);
+size_t abcd_encoder_workspace_bytes(const abcd_encoder_cfg* cfg, int T, int L, int B);
+/* replaces RNN_Variational_Encoder.forward (model.py:60-66): last_hidden is
+ * B x out_size laid out [h_l0f, c_l0f, h_l0b, c_l0b, h_l1f, ...] */
+int abcd_encoder_forward(const abcd_encoder_cfg* cfg, const abcd_encoder_params* p, const abcd_packed* x,
+                         float* last_hidden, void* ws, size_t ws_bytes, void* stream);
+/* autograd backward of the above: writes (overwrites) every weight gradient */
+int abcd_encoder_backward(const abcd_encoder_cfg* cfg, const abcd_encoder_params* p, const abcd_packed* x,
+                          const float* d_last_hidden, const abcd_encoder_grads* g, void* ws, size_t ws_bytes,
+                          void* stream);
+
+/* ------------------------------------------------------------------------
+ * ABCDSampler (model.py:538-639) and the plain Gaussian Sampler
+ * (plain/modules/model.py:538-567, model.py:17-28)
+ * ---------------------------------------------------------------------- */
+typedef struct abcd_sampler_cfg {
+  int input_size, mlp_hidden, num_categories, feature_dim;
+  int plain; /* 1: plain Gaussian feature sampler (feature_dim = output_size) */
+} abcd_sampler_cfg;
+typedef struct abcd_sampler_params {
+  abcd_mlp_w mlp[2];                 /* ABCD: mlp[0] = to_code_like; plain: mlps.0 (mean), mlps.1 (log-var) */
+  const float* codebook;             /* D x K  (ABCD only) */
+  const float* posterior_shape_logits; /* K (ABCD only) */
+  float prior_concentration;
+} abcd_sampler_params;
+typedef struct abcd_sampler_grads {
+  abcd_mlp_g mlp[2];
+  float* codebook;
+  float* posterior_shape_logits;
+} abcd_sampler_grads;
+
+/* sampling modes */
+enum abcd_sample_mode { ABCD_SAMPLE_SOFTMAX = 0, ABCD_SAMPLE_GUMBEL = 1 };
+
+size_t abcd_sampler_workspace_bytes(const abcd_sampler_cfg* cfg, int B);
+/* replaces ABCDSampler.forward (model.py:581-590): logits B x K.
+ * plain: Sampler.forward -> params_out = [mean | log_var] (B x 2f). */
+int abcd_sampler_forward(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
+                         float* logits, void* ws, size_t ws_bytes, void* stream);
+/* replaces ABCDSampler.sample (model.py:592-606) / plain Sampler.sample:
+ * feats B x D.  noise: ABCD gumbel mode: B x K gumbel g = -log(Exp(1));
+ * plain: B x f standard normal.  noise == NULL -> in-kernel Philox(seed, offset). */
+int abcd_sampler_sample(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* logits, int B,
+                        int mode, float temperature, const float* noise, uint64_t seed, uint64_t offset,
+                        float* feats, void* ws, size_t ws_bytes, void* stream);
+/* replaces ABCDSampler.kl_divergence (model.py:608-639) / plain kl: writes a device scalar */
+int abcd_sampler_kl(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* logits, int B,
+                    double entire_data_size, float* kl_out, void* ws, size_t ws_bytes, void* stream);
+/* backward of forward+sample+kl.  d_feats: B x D (may be NULL); d_kl: device
+ * scalar upstream grad of kl (may be NULL); d_h: B x E (may be NULL). */
+int abcd_sampler_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
+                          int mode, float temperature, double entire_data_size, const float* d_feats,
+                          const float* d_kl, float* d_h, const abcd_sampler_grads* g, void* ws, size_t ws_bytes,
+                          void* stream);
+/* The same backward split the way autograd sees the three reference methods:
+ * sample_backward:  d_feats -> d_logits (written), d_codebook (written, may be NULL)
+ *                   (plain: d_feats -> d[mean | log_var])
+ * kl_backward:      d_kl -> d_logits (written, or added when accumulate), d_psl (may be NULL)
+ * forward_backward: d_logits -> MLP grads, codebook grad of the logits product
+ *                   (added to g->codebook when accumulate_codebook), d_h (may be NULL) */
+int abcd_sampler_sample_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, int B, int mode,
+                                 float temperature, const float* d_feats, float* d_logits, float* d_codebook,
+                                 void* ws, size_t ws_bytes, void* stream);
+int abcd_sampler_kl_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, int B,
+                             double entire_data_size, const float* d_kl, int accumulate, float* d_logits,
+                             float* d_psl, void* ws, size_t ws_bytes, void* stream);
+int abcd_sampler_forward_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
+                                  const float* d_logits, float* d_h, const abcd_sampler_grads* g,
+                                  int accumulate_codebook, void* ws, size_t ws_bytes, void* stream);
+/* learning.py:171-178 diagnostics: out[0..2] = posterior clustering /
+ * batch-mean / Dirichlet-shape perplexities (device floats) */
+int abcd_perplexities(const float* logits, int B, int K, const float* posterior_shape_logits, float* out,
+                      void* stream);
+
+/* ------------------------------------------------------------------------
+ * Decoder: RNN_Variational_Decoder (model.py:84-196, unidirectional)
+ * ---------------------------------------------------------------------- */
+typedef struct abcd_decoder_cfg {
+  int output_size, hidden_size, mlp_hidden, feature_size, rnn_type;
+  int feedback;      /* 1: feed the reparameterised sample back (self_feedback, or eval mode) */
+  int num_speakers;  /* 0: no speaker embedding */
+  int speaker_dim;
+} abcd_decoder_cfg;
+typedef struct abcd_decoder_params {
+  const float* embed_speaker;  /* num_speakers x speaker_dim or NULL */
+  const float *f2h_w, *f2h_b;  /* feature2hidden */
+  abcd_mlp_w offset, mu, lv;   /* offset_predictor, emission mlps.0, mlps.1 */
+  abcd_rnn_w cell;             /* rnn_cell.cell */
+} abcd_decoder_params;
+typedef struct abcd_decoder_grads {
+  float* embed_speaker;
+  float *f2h_w, *f2h_b;
+  abcd_mlp_g offset, mu, lv;
+  abcd_rnn_g cell;
+} abcd_decoder_grads;
+
+size_t abcd_decoder_workspace_bytes(const abcd_decoder_cfg* cfg, int T, int L, int B);
+/* replaces RNN_Variational_Decoder.forward (model.py:147-196).
+ * features: B x feature_size; speakers: device int64 B (or NULL);
+ * gt = ground_truth_out (L x F, or NULL); gt_offset (L, or NULL);
+ * eps: L x F standard normals in packed order (or NULL -> Philox(seed,offset));
+ * outputs (each may be NULL): flatten_out, mu, log_var (L x F), offset_logits (L);
+ * losses[0] = emission NLL, losses[1] = offset BCE (device floats). */
+int abcd_decoder_forward(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
+                         const float* features, const int64_t* speakers, const float* gt_offset,
+                         const float* eps, uint64_t seed, uint64_t offset, float* flatten_out, float* mu,
+                         float* log_var, float* offset_logits, float* losses, void* ws, size_t ws_bytes,
+                         void* stream);
+/* backward w.r.t. losses[0] (scaled by *d_em) and losses[1] (scaled by *d_off);
+ * d_em/d_off are device scalars; d_features: B x feature_size (may be NULL). */
+int abcd_decoder_backward(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
+                          const float* features, const int64_t* speakers, const float* gt_offset,
+                          const float* d_em, const float* d_off, float* d_features,
+                          const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Optimiser: torch.nn.utils.clip_grad_norm_ + torch.optim.SGD
+ * (learning.py:161-163, 256) over one flat fp32 parameter/gradient buffer.
+ * ---------------------------------------------------------------------- */
+size_t abcd_optim_workspace_bytes(long n);
+/* total 2-norm of g (device scalar) */
+int abcd_grad_norm(const float* g, long n, float* out_norm, void* ws, size_t ws_bytes, void* stream);
+/* g *= min(1, max_norm / (||g|| + 1e-6)); buf = momentum*buf + g (buf = g if
+ * momentum_init); p -= lr * (momentum ? buf : g).  out_norm (device, may be
+ * NULL) receives the pre-clip norm. */
+int abcd_clip_sgd(float* p, float* g, float* momentum_buf, long n, float max_norm, float lr, float momentum,
+                  int momentum_init, float* out_norm, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Utilities
+ * ---------------------------------------------------------------------- */
+/* loss = (losses[0] + losses[1] + kl[0]) / B  (learning.py:155-157) */
+int abcd_total_loss(const float* losses, const float* kl, int B, float* loss, void* stream);
+/* C = A(MxK) @ B(NxK)^T (+bias[n]); row-major, plain GEMM used by tests */
+int abcd_gemm_nt(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
+                 const float* bias, void* ws, size_t ws_bytes, void* stream);
+/* y = act(x @ W^T + b): nn.Linear (act 0) / Linear->Tanh (act 1); x M x K, W N x K.
+ * Used by the standalone MLP modules (model.py:316-334) outside the training step;
+ * ws >= (M + N) * roundup(K,16) * 4 bytes when K is not a multiple of 16. */
+int abcd_linear(int M, int N, int K, const float* x, long ldx, const float* W, long ldw, const float* b, int act,
+                float* y, long ldy, void* ws, size_t ws_bytes, void* stream);
+/* n standard normals from Philox-4x32-10(seed, offset + i) */
+int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offset, void* stream);
+/* library build identification (gfx target, version) */
+const char* abcd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ABCD_HIP_H */

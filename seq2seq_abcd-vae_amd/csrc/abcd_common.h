@@ -1,0 +1,166 @@
+// abcd_common.h -- shared device building blocks for the ABCD-VAE CDNA4 kernels.
+//
+// Everything here is written for gfx950 (MI355X): 64-lane waves, the f32-input
+// matrix core `v_mfma_f32_16x16x4_f32` (exact f32, 64 FLOP/clk/SIMD), per-CU LDS.
+//
+// GEMM convention used by every kernel in this library
+// ----------------------------------------------------
+//   C[m][n] = sum_k A(m, k) * B(n, k)
+// Both operands are addressed as (row, k).  An operand is either
+//   * KC ("K-contiguous"): element (row, k) at p[row*ld + k]  (row-major A, or
+//     a weight matrix W[n][k] used as x @ W^T) -- loaded as float4 along k;
+//   * KM ("K-major"):      element (row, k) at p[k*ld + row]  (e.g. dG^T when
+//     the reduction runs over the packed-frame axis) -- loaded as 4 dwords,
+//     16 lanes reading 16 consecutive rows (64-B segments).
+// K is walked in chunks of 16.  Inside a chunk lane (r = lane&15, q = lane>>4)
+// supplies k = 16*kc + 4*q + s to MFMA step s (s = 0..3): the float4 of a KC
+// operand therefore feeds four consecutive MFMAs with no shuffles.  The same
+// k assignment is used for A and B, so every k is summed exactly once.
+// Accumulator subtile (16x16): lane holds rows 4*q + {0..3}, column r.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DEV __device__ __forceinline__
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+namespace abcd {
+
+DEV f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+DEV f4 f4zero() { f4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
+
+DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+DEV float tanhf_(float x) { return tanhf(x); }
+
+// ---------------------------------------------------------------------------
+// operand views
+// ---------------------------------------------------------------------------
+struct KC {
+  const float* p; long ld; int nrows;
+  DEV f4 frag(int row, int kc, int q) const {
+    if (row < nrows) return *reinterpret_cast<const f4*>(p + (long)row * ld + kc * 16 + 4 * q);
+    return f4zero();
+  }
+};
+struct KM {
+  const float* p; long ld; int nrows; int nk;
+  DEV f4 frag(int row, int kc, int q) const {
+    f4 v = f4zero();
+    if (row < nrows) {
+      int k0 = kc * 16 + 4 * q;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (k0 + s < nk) v[s] = p[(long)(k0 + s) * ld + row];
+    }
+    return v;
+  }
+};
+
+// One wave accumulates MR x NR 16x16 subtiles over chunks kc0, kc0+step, ... < kc1.
+// ar[i] / br[j]: absolute operand row this lane supplies for subtile i / j.
+template <int MR, int NR, class OA, class OB>
+DEV void wave_mma(f4 (&acc)[MR][NR], const OA& A, const int (&ar)[MR], const OB& B, const int (&br)[NR],
+                  int kc0, int kc1, int step, int q) {
+  if (kc0 >= kc1) return;
+  f4 a[MR], b[NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) a[i] = A.frag(ar[i], kc0, q);
+#pragma unroll
+  for (int j = 0; j < NR; ++j) b[j] = B.frag(br[j], kc0, q);
+  for (int kc = kc0; kc < kc1; kc += step) {
+    f4 an[MR], bn[NR];
+    const int kn = kc + step;
+    const bool more = kn < kc1;
+#pragma unroll
+    for (int i = 0; i < MR; ++i) an[i] = more ? A.frag(ar[i], kn, q) : f4zero();
+#pragma unroll
+    for (int j = 0; j < NR; ++j) bn[j] = more ? B.frag(br[j], kn, q) : f4zero();
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = mfma4(a[i][s], b[j][s], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < MR; ++i) a[i] = an[i];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) b[j] = bn[j];
+  }
+}
+
+template <int MR, int NR>
+DEV void acc_zero(f4 (&acc)[MR][NR]) {
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f4zero();
+}
+
+// Chunks of a K range are dealt round-robin to the 4 waves of a workgroup
+// ("wave split-K"); a segment starting at global chunk g0 gives wave w the
+// chunks kc with (g0 + kc) % 4 == w.
+DEV int first_chunk(int w, int g0) { return ((w - g0) % 4 + 4) % 4; }
+
+// Sum the 4 waves' partial MR x NR tiles in LDS.  After the call, `tile`
+// (TM x (TN+4) floats, TM = 16*MR, TN = 16*NR) holds the reduced tile.
+// `lds` must hold 4 * TM * (TN+4) floats.
+template <int MR, int NR>
+DEV void reduce_waves_to_lds(const f4 (&acc)[MR][NR], float* lds, int wave, int lane) {
+  constexpr int TM = 16 * MR, TN = 16 * NR, LD = TN + 4;
+  const int r = lane & 15, q = lane >> 4;
+  float* mine = lds + wave * TM * LD;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) mine[(16 * i + 4 * q + g) * LD + 16 * j + r] = acc[i][j][g];
+  __syncthreads();
+  for (int e = threadIdx.x; e < TM * TN; e += blockDim.x) {
+    const int row = e / TN, col = e % TN;
+    const int o = row * LD + col;
+    lds[o] = lds[o] + lds[TM * LD + o] + lds[2 * TM * LD + o] + lds[3 * TM * LD + o];
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Philox-4x32-10 (Salmon et al. 2011), counter = (offset lo, offset hi, 0, 0),
+// key = seed.  One call -> 4 uniform 32-bit words.
+// ---------------------------------------------------------------------------
+DEV void philox4x32(uint64_t seed, uint64_t ctr, uint32_t (&out)[4]) {
+  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0, c3 = 0;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1; c3 = (uint32_t)p0; c0 = n0; c2 = n2;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+// uniform in (0, 1]
+DEV float u01(uint32_t x) { return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f); }
+// standard normal for element index i of stream (seed, offset): Box-Muller
+DEV float philox_normal(uint64_t seed, uint64_t idx) {
+  uint32_t o[4];
+  philox4x32(seed, idx, o);
+  const float u1 = u01(o[0]), u2 = u01(o[1]);
+  return sqrtf(-2.0f * __logf(u1)) * __cosf(6.2831853071795864f * u2);
+}
+// Gumbel(0,1) = -log(E), E ~ Exp(1) = -log(U)
+DEV float philox_gumbel(uint64_t seed, uint64_t idx) {
+  uint32_t o[4];
+  philox4x32(seed, idx, o);
+  const float u = u01(o[0]);
+  const float e = -__logf(u);
+  return -__logf(fmaxf(e, 1e-30f));
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+inline int rup16(int x) { return (x + 15) & ~15; }
+
+}  // namespace abcd

@@ -1,0 +1,315 @@
+// abcd_gemm.hip -- fp32 MFMA GEMM and small reduction / layout kernels.
+//
+// Two GEMM shapes share the wave core of abcd_common.h:
+//   gemm_big : 4 waves as 2x2, each wave 64x64 (4x4 subtiles), WG tile 128x128.
+//              For the frame-parallel GEMMs (encoder input projection over all
+//              L packed frames, batched offset MLP, decoder-input GEMMs).
+//   gemm_ks  : 4 waves split K of one 32x64 tile, reduced through LDS.  For
+//              small-M GEMMs (B = 512 rows) and for the weight-gradient GEMMs
+//              whose reduction runs over the packed frames (K = L ~ 65k), where
+//              the grid is also split along K into fp32 slabs that a second
+//              pass reduces deterministically.
+#include "abcd_common.h"
+#include "abcd_internal.h"
+
+namespace abcd {
+
+struct EpiArgs {
+  float* C; long ldc; int M, N; float alpha, beta; const float* bias; int act;
+  float* slab;  // non-null when gridDim.z > 1: raw partials, slab[z][m*N + n]
+};
+
+DEV float apply_epi(const EpiArgs& e, int row, int col, float acc) {
+  float v = e.alpha * acc;
+  if (e.beta != 0.f) v += e.beta * e.C[(long)row * e.ldc + col];
+  if (e.bias) v += e.bias[col];
+  if (e.act == ACT_TANH) v = tanhf(v);
+  return v;
+}
+
+template <int MR, int NR, class OA, class OB>
+__global__ __launch_bounds__(256) void gemm_big_kernel(OA A, OB B, int nch, int cps, EpiArgs e) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * (32 * MR) + wm * 16 * MR;
+  const int n0 = blockIdx.x * (32 * NR) + wn * 16 * NR;
+  int ar[MR], br[NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) ar[i] = m0 + 16 * i + r;
+#pragma unroll
+  for (int j = 0; j < NR; ++j) br[j] = n0 + 16 * j + r;
+  f4 acc[MR][NR];
+  acc_zero(acc);
+  const int c0 = blockIdx.z * cps, c1 = min(nch, c0 + cps);
+  wave_mma<MR, NR>(acc, A, ar, B, br, c0, c1, 1, q);
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int row = m0 + 16 * i + 4 * q + g, col = n0 + 16 * j + r;
+        if (row < e.M && col < e.N) {
+          if (e.slab)
+            e.slab[(long)blockIdx.z * e.M * e.N + (long)row * e.N + col] = acc[i][j][g];
+          else
+            e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, acc[i][j][g]);
+        }
+      }
+}
+
+template <int MR, int NR, class OA, class OB>
+__global__ __launch_bounds__(256) void gemm_ks_kernel(OA A, OB B, int nch, int cps, EpiArgs e) {
+  constexpr int TM = 16 * MR, TN = 16 * NR, LD = TN + 4;
+  __shared__ __attribute__((aligned(16))) float lds[4 * TM * LD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  int ar[MR], br[NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) ar[i] = m0 + 16 * i + r;
+#pragma unroll
+  for (int j = 0; j < NR; ++j) br[j] = n0 + 16 * j + r;
+  f4 acc[MR][NR];
+  acc_zero(acc);
+  const int c0 = blockIdx.z * cps, c1 = min(nch, c0 + cps);
+  wave_mma<MR, NR>(acc, A, ar, B, br, c0 + w, c1, 4, q);
+  reduce_waves_to_lds<MR, NR>(acc, lds, w, lane);
+  for (int t = threadIdx.x; t < TM * TN; t += 256) {
+    const int lr = t / TN, lc = t % TN;
+    const int row = m0 + lr, col = n0 + lc;
+    if (row < e.M && col < e.N) {
+      const float v = lds[lr * LD + lc];
+      if (e.slab)
+        e.slab[(long)blockIdx.z * e.M * e.N + (long)row * e.N + col] = v;
+      else
+        e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, v);
+    }
+  }
+}
+
+__global__ void slab_reduce_kernel(const float* slab, int Z, EpiArgs e) {
+  const long n = (long)e.M * e.N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < Z; ++z) s += slab[(long)z * n + i];
+    const int row = (int)(i / e.N), col = (int)(i % e.N);
+    e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, s);
+  }
+}
+
+template <class OA, class OB>
+static int gemm_launch(hipStream_t s, int M, int N, int K, OA A, OB B, EpiArgs e, float* scratch,
+                       size_t scratch_floats) {
+  const int nch = cdiv(K, 16);
+  const int tiles_big = cdiv(M, 128) * cdiv(N, 128);
+  if (tiles_big >= 240) {
+    dim3 grid(cdiv(N, 128), cdiv(M, 128), 1);
+    gemm_big_kernel<4, 4, OA, OB><<<grid, 256, 0, s>>>(A, B, nch, nch, e);
+    ABCD_CHECK_LAUNCH();
+    return 0;
+  }
+  const int tiles = cdiv(M, 32) * cdiv(N, 64);
+  int Z = 1;
+  if (tiles < 768 && nch >= 16 && scratch) {
+    Z = cdiv(1024, tiles);
+    Z = std::min(Z, std::max(1, nch / 8));
+    const long per = (long)M * N;
+    Z = std::min<long>(Z, (long)(scratch_floats / (size_t)per));
+    if (Z < 2) Z = 1;
+  }
+  const int cps = cdiv(nch, Z);
+  Z = cdiv(nch, cps);
+  dim3 grid(cdiv(N, 64), cdiv(M, 32), Z);
+  EpiArgs ek = e;
+  if (Z > 1) ek.slab = scratch;
+  gemm_ks_kernel<2, 4, OA, OB><<<grid, 256, 0, s>>>(A, B, nch, cps, ek);
+  ABCD_CHECK_LAUNCH();
+  if (Z > 1) {
+    const long n = (long)M * N;
+    slab_reduce_kernel<<<std::min<long>(2048, cdiv(n, 256)), 256, 0, s>>>(scratch, Z, e);
+    ABCD_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, long ldc, float alpha,
+         float beta, const float* bias, int act, float* scratch, size_t scratch_floats) {
+  if (M <= 0 || N <= 0) return 0;
+  EpiArgs e{C, ldc, M, N, alpha, beta, bias, act, nullptr};
+  if (K <= 0) {  // C = beta*C + bias
+    KC za{A.p, 16, 0};
+    KC zb{B.p, 16, 0};
+    return gemm_launch(s, M, N, 16, za, zb, e, nullptr, 0);
+  }
+  if (!A.kmajor) ABCD_REQUIRE(K % 16 == 0 && A.ld % 4 == 0 && ((uintptr_t)A.p % 16) == 0);
+  if (!B.kmajor) ABCD_REQUIRE(K % 16 == 0 && B.ld % 4 == 0 && ((uintptr_t)B.p % 16) == 0);
+  if (!A.kmajor && !B.kmajor)
+    return gemm_launch(s, M, N, K, KC{A.p, A.ld, std::min(A.nrows, M)}, KC{B.p, B.ld, std::min(B.nrows, N)}, e,
+                       scratch, scratch_floats);
+  if (A.kmajor && !B.kmajor)
+    return gemm_launch(s, M, N, K, KM{A.p, A.ld, std::min(A.nrows, M), K}, KC{B.p, B.ld, std::min(B.nrows, N)}, e,
+                       scratch, scratch_floats);
+  if (!A.kmajor && B.kmajor)
+    return gemm_launch(s, M, N, K, KC{A.p, A.ld, std::min(A.nrows, M)}, KM{B.p, B.ld, std::min(B.nrows, N), K}, e,
+                       scratch, scratch_floats);
+  return gemm_launch(s, M, N, K, KM{A.p, A.ld, std::min(A.nrows, M), K}, KM{B.p, B.ld, std::min(B.nrows, N), K},
+                     e, scratch, scratch_floats);
+}
+
+size_t gemm_scratch_floats_hint(int M, int N, int K) { return (size_t)M * N * 16; }
+
+// ---------------------------------------------------------------------------
+// column sums (bias gradients, GEMV-T): out[j] = beta*out[j] + sum_r w[r] Z[r][j]
+// pass 1: blockIdx.y = row slice, 256 threads over columns; pass 2 sums slices.
+// ---------------------------------------------------------------------------
+__global__ void colsum_pass1(const float* Z, long ldz, int nrows, int ncols, const float* w, int rows_per,
+                             float* part) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= ncols) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(nrows, r0 + rows_per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += (w ? w[r] : 1.f) * Z[(long)r * ldz + j];
+  part[(long)blockIdx.y * ncols + j] = s;
+}
+__global__ void colsum_pass2(const float* part, int nslices, int ncols, float* out, float beta) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= ncols) return;
+  float s = 0.f;
+  for (int z = 0; z < nslices; ++z) s += part[(long)z * ncols + j];
+  out[j] = (beta != 0.f ? beta * out[j] : 0.f) + s;
+}
+
+int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const float* w, float* out,
+           float beta, float* scratch, size_t scratch_floats) {
+  if (ncols <= 0) return 0;
+  int slices = std::max(1, std::min(cdiv(nrows, 64), 512));
+  slices = (int)std::max<long>(1, std::min<long>(slices, (long)(scratch_floats / (size_t)ncols)));
+  const int rows_per = cdiv(std::max(nrows, 1), slices);
+  slices = std::max(1, cdiv(std::max(nrows, 1), rows_per));
+  colsum_pass1<<<dim3(cdiv(ncols, 256), slices), 256, 0, s>>>(Z, ldz, nrows, ncols, w, rows_per, scratch);
+  ABCD_CHECK_LAUNCH();
+  colsum_pass2<<<cdiv(ncols, 256), 256, 0, s>>>(scratch, slices, ncols, out, beta);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// layout copies (padding / transposition of weight compute copies)
+// ---------------------------------------------------------------------------
+__global__ void pack2d_kernel(const float* src, long lds, int sr, int sc, int trans, float* dst, long ldd, int dr,
+                              int dc) {
+  const long n = (long)dr * dc;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / dc), c = (int)(i % dc);
+    float v = 0.f;
+    if (r < sr && c < sc) v = trans ? src[(long)c * lds + r] : src[(long)r * lds + c];
+    dst[(long)r * ldd + c] = v;
+  }
+}
+int pack2d(hipStream_t s, const float* src, long lds, int sr, int sc, bool trans, float* dst, long ldd, int dr,
+           int dc) {
+  const long n = (long)dr * dc;
+  if (n <= 0) return 0;
+  pack2d_kernel<<<(int)std::min<long>(4096, cdiv(n, 256)), 256, 0, s>>>(src, lds, sr, sc, trans, dst, ldd, dr, dc);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void add_vec_kernel(const float* a, const float* b, float* y, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = a[i] + b[i];
+}
+int add_vec(hipStream_t s, const float* a, const float* b, float* y, int n) {
+  if (n <= 0) return 0;
+  add_vec_kernel<<<cdiv(n, 256), 256, 0, s>>>(a, b, y, n);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// deterministic sum of a float array -> float (and double) scalar
+// ---------------------------------------------------------------------------
+DEV double block_sum_d(double v, double* sh) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+  __syncthreads();
+  return t;
+}
+__global__ void reduce_pass1(const float* x, long n, double* part) {
+  __shared__ double sh[16];
+  double v = 0.0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) v += x[i];
+  v = block_sum_d(v, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = v;
+}
+__global__ void reduce_pass2(const double* part, int np, float* out, double* out64) {
+  __shared__ double sh[16];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) v += part[i];
+  v = block_sum_d(v, sh);
+  if (threadIdx.x == 0) {
+    if (out) *out = (float)v;
+    if (out64) *out64 = v;
+  }
+}
+int reduce_sum(hipStream_t s, const float* x, long n, double* partials, float* out, double* out64) {
+  const int nb = (int)std::max<long>(1, std::min<long>(1024, cdiv(n, 256)));
+  reduce_pass1<<<nb, 256, 0, s>>>(x, n, partials);
+  ABCD_CHECK_LAUNCH();
+  reduce_pass2<<<1, 256, 0, s>>>(partials, nb, out, out64);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace abcd
+
+// ---------------------------------------------------------------------------
+// C ABI: plain GEMM (used by tests to check the MFMA core against the oracle)
+// ---------------------------------------------------------------------------
+extern "C" int abcd_gemm_nt(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C,
+                            long ldc, const float* bias, void* ws, size_t ws_bytes, void* stream) {
+  using namespace abcd;
+  if (M < 0 || N < 0 || K < 0 || !A || !B || !C) return ABCD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (K % 16 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0)
+    return gemm(s, M, N, K, opKC(A, lda, M), opKC(B, ldb, N), C, ldc, 1.f, 0.f, bias, ACT_NONE, (float*)ws,
+                ws_bytes / 4);
+  // arbitrary K: read both operands K-major-style (transposed view) -> KM path handles tails
+  // (A(m,k) = A[m*lda+k] is a KM operand with ld=1 over rows of stride lda? no: use a padded copy)
+  const int Kp = rup16(K);
+  const size_t need = ((size_t)M + N) * Kp;
+  if (ws_bytes / 4 < need) return ABCD_EINVAL;
+  float* Ap = (float*)ws;
+  float* Bp = Ap + (size_t)M * Kp;
+  ABCD_TRY((hipError_t)pack2d(s, A, lda, M, K, false, Ap, Kp, M, Kp));
+  ABCD_TRY((hipError_t)pack2d(s, B, ldb, N, K, false, Bp, Kp, N, Kp));
+  float* rest = Bp + (size_t)N * Kp;
+  const size_t rest_f = ws_bytes / 4 - need;
+  return gemm(s, M, N, Kp, opKC(Ap, Kp, M), opKC(Bp, Kp, N), C, ldc, 1.f, 0.f, bias, ACT_NONE, rest, rest_f);
+}
+
+// C ABI: y = act(x @ W^T + b), act 0 = none, 1 = tanh (nn.Linear [+ Tanh]); any K
+extern "C" int abcd_linear(int M, int N, int K, const float* x, long ldx, const float* W, long ldw, const float* b,
+                           int act, float* y, long ldy, void* ws, size_t ws_bytes, void* stream) {
+  using namespace abcd;
+  if (M < 0 || N < 0 || K < 0 || !x || !W || !y || (act != ACT_NONE && act != ACT_TANH)) return ABCD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  if (K % 16 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)W % 16) == 0)
+    return gemm(s, M, N, K, opKC(x, ldx, M), opKC(W, ldw, N), y, ldy, 1.f, 0.f, b, act, (float*)ws, ws_bytes / 4);
+  const int Kp = rup16(K);
+  const size_t need = ((size_t)M + N) * Kp;
+  if (ws_bytes / 4 < need) return ABCD_EINVAL;
+  float* xp = (float*)ws;
+  float* wp = xp + (size_t)M * Kp;
+  ABCD_TRY((hipError_t)pack2d(s, x, ldx, M, K, false, xp, Kp, M, Kp));
+  ABCD_TRY((hipError_t)pack2d(s, W, ldw, N, K, false, wp, Kp, N, Kp));
+  return gemm(s, M, N, Kp, opKC(xp, Kp, M), opKC(wp, Kp, N), y, ldy, 1.f, 0.f, b, act, wp + (size_t)N * Kp,
+              ws_bytes / 4 - need);
+}

@@ -1,0 +1,80 @@
+// abcd_internal.h -- host-side helpers shared by the .hip translation units
+// (not part of the C ABI; see include/abcd_hip.h for that).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <algorithm>
+
+#include "abcd_hip.h"
+
+namespace abcd {
+
+#define ABCD_TRY(expr)                                   \
+  do {                                                   \
+    hipError_t e__ = (expr);                             \
+    if (e__ != hipSuccess) return (int)e__;              \
+  } while (0)
+#define ABCD_CHECK_LAUNCH() ABCD_TRY(hipGetLastError())
+#define ABCD_REQUIRE(cond)                               \
+  do {                                                   \
+    if (!(cond)) return ABCD_EINVAL;                     \
+  } while (0)
+
+enum Act { ACT_NONE = 0, ACT_TANH = 1 };
+
+struct Operand {
+  const float* p;
+  long ld;
+  int nrows;    // rows beyond this read as zero
+  bool kmajor;  // false: (row,k) at p[row*ld+k] (K must be a multiple of 16); true: at p[k*ld+row]
+};
+
+inline Operand opKC(const float* p, long ld, int nrows) { return Operand{p, ld, nrows, false}; }
+inline Operand opKM(const float* p, long ld, int nrows) { return Operand{p, ld, nrows, true}; }
+
+// C[m][n] = alpha * sum_k A(m,k) B(n,k) + beta * C[m][n] + bias[n], then act.
+// Stores rows < M, cols < N.  `scratch` (may be null) enables split-K slabs.
+int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, long ldc, float alpha,
+         float beta, const float* bias, int act, float* scratch, size_t scratch_floats);
+
+// out[j] (+)= sum_r w[r] * Z[r*ldz + j]  (w == null -> 1), j < ncols, r < nrows; deterministic.
+int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const float* w, float* out,
+           float beta, float* scratch, size_t scratch_floats);
+
+// dst[r*ldd + c] = (r < sr && c < sc) ? src(r, c) : 0 for r < dr, c < dc;
+// src(r,c) = trans ? src[c*lds + r] : src[r*lds + c]
+int pack2d(hipStream_t s, const float* src, long lds, int sr, int sc, bool trans, float* dst, long ldd,
+           int dr, int dc);
+
+// y = a + b elementwise (n floats)
+int add_vec(hipStream_t s, const float* a, const float* b, float* y, int n);
+
+// Sum of n doubles/floats -> out (device), deterministic two-pass.
+int reduce_sum(hipStream_t s, const float* x, long n, double* partials, float* out, double* out64);
+
+size_t gemm_scratch_floats_hint(int M, int N, int K);
+
+}  // namespace abcd
+
+namespace abcd {
+// Bump allocator used to carve a caller-provided workspace.  The same carve
+// sequence runs with base == nullptr to size the workspace.
+struct Arena {
+  char* base;
+  size_t off, cap;
+  bool ok;
+  explicit Arena(void* b, size_t c) : base((char*)b), off(0), cap(c), ok(true) {}
+  float* f(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    char* p = base ? base + off : nullptr;
+    off += n * sizeof(float);
+    if (base && off > cap) ok = false;
+    return (float*)p;
+  }
+  double* d(size_t n) { return (double*)f(2 * n); }
+};
+
+// checks PackedSequence.batch_sizes (host): non-increasing, sum L, first B
+int validate_batch(const int64_t* bs, int T, int L, int B);
+}  // namespace abcd

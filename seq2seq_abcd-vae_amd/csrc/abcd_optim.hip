@@ -1,0 +1,134 @@
+// abcd_optim.hip -- clip_grad_norm_ + SGD over the flat fp32 parameter buffer
+// (ABCD-VAE/learning.py:161-163,256), the step loss (learning.py:155-157) and
+// the Philox noise generator used when noise is not supplied by the host.
+//
+// The whole model's parameters (1.95 M fp32 at the north-star config) live in
+// ONE flat buffer, gradients in a second one: the global norm is a single
+// deterministic two-pass reduction and the update is one streaming pass
+// (read g, p[, buf]; write g, p[, buf]) -- HBM-bound, ~24-40 B per parameter.
+#include "abcd_common.h"
+#include "abcd_internal.h"
+
+namespace abcd {
+
+__global__ void sq_pass1(const float* g, long n, double* part) {
+  __shared__ double sh[16];
+  double v = 0.0;
+  const long n4 = n / 4;
+  const f4* g4 = reinterpret_cast<const f4*>(g);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const f4 x = g4[i];
+    v += (double)x[0] * x[0] + (double)x[1] * x[1] + (double)x[2] * x[2] + (double)x[3] * x[3];
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    v += (double)g[i] * g[i];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+    part[blockIdx.x] = t;
+  }
+}
+// state[0] = norm, state[1] = clip coefficient
+__global__ void norm_pass2(const double* part, int np, float max_norm, float* state, float* out_norm) {
+  __shared__ double sh[16];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) v += part[i];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+    const float norm = (float)sqrt(t);
+    const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);
+    state[0] = norm;
+    state[1] = coef;
+    if (out_norm) *out_norm = norm;
+  }
+}
+__global__ void sgd_update(float* p, float* g, float* buf, long n, const float* state, float lr, float momentum,
+                           int init) {
+  const float coef = state[1];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i] * coef;
+    g[i] = gi;
+    if (buf) {
+      const float b = init ? gi : momentum * buf[i] + gi;
+      buf[i] = b;
+      gi = b;
+    }
+    p[i] -= lr * gi;
+  }
+}
+
+__global__ void total_loss_kernel(const float* losses, const float* kl, int B, float* loss) {
+  if (threadIdx.x == 0) *loss = (losses[0] + losses[1] + kl[0]) / (float)B;
+}
+
+__global__ void fill_normal_kernel(float* out, long n, uint64_t seed, uint64_t offset) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = philox_normal(seed, offset + (uint64_t)i);
+}
+
+}  // namespace abcd
+
+using namespace abcd;
+
+static const int kNormBlocks = 1024;
+
+extern "C" size_t abcd_optim_workspace_bytes(long n) {
+  (void)n;
+  return kNormBlocks * sizeof(double) + 256;
+}
+
+extern "C" int abcd_grad_norm(const float* g, long n, float* out_norm, void* ws, size_t ws_bytes, void* stream) {
+  if (!g || n <= 0 || !out_norm || !ws || ws_bytes < abcd_optim_workspace_bytes(n)) return ABCD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  double* part = (double*)ws;
+  float* state = (float*)(part + kNormBlocks);
+  sq_pass1<<<kNormBlocks, 256, 0, s>>>(g, n, part);
+  ABCD_CHECK_LAUNCH();
+  norm_pass2<<<1, 256, 0, s>>>(part, kNormBlocks, 1.f, state, out_norm);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int abcd_clip_sgd(float* p, float* g, float* momentum_buf, long n, float max_norm, float lr,
+                             float momentum, int momentum_init, float* out_norm, void* ws, size_t ws_bytes,
+                             void* stream) {
+  if (!p || !g || n <= 0 || !ws || ws_bytes < abcd_optim_workspace_bytes(n)) return ABCD_EINVAL;
+  if (momentum != 0.f && !momentum_buf) return ABCD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  double* part = (double*)ws;
+  float* state = (float*)(part + kNormBlocks);
+  sq_pass1<<<kNormBlocks, 256, 0, s>>>(g, n, part);
+  ABCD_CHECK_LAUNCH();
+  norm_pass2<<<1, 256, 0, s>>>(part, kNormBlocks, max_norm, state, out_norm);
+  ABCD_CHECK_LAUNCH();
+  const int nb = (int)std::min<long>(4096, (n + 255) / 256);
+  sgd_update<<<nb, 256, 0, s>>>(p, g, momentum != 0.f ? momentum_buf : nullptr, n, state, lr, momentum,
+                                momentum_init);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int abcd_total_loss(const float* losses, const float* kl, int B, float* loss, void* stream) {
+  if (!losses || !kl || !loss || B <= 0) return ABCD_EINVAL;
+  total_loss_kernel<<<1, 64, 0, (hipStream_t)stream>>>(losses, kl, B, loss);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offset, void* stream) {
+  if (!out || n < 0) return ABCD_EINVAL;
+  if (n == 0) return 0;
+  fill_normal_kernel<<<(int)std::min<long>(4096, (n + 255) / 256), 256, 0, (hipStream_t)stream>>>(out, n, seed,
+                                                                                                 offset);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" const char* abcd_version(void) { return "abcd_hip 0.1 gfx950 fp32-mfma16x16x4"; }

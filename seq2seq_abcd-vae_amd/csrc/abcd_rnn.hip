@@ -1,0 +1,1011 @@
+// abcd_rnn.hip -- packed-sequence RNN encoder and self-feedback decoder for CDNA4.
+//
+// Hot path of ABCD-VAE/learning.py:149,153 (+ their autograd backward):
+//   encoder  model.py:40-66   torch.nn.LSTM/GRU over a PackedSequence (bi-dir)
+//   decoder  model.py:147-196 LSTMCell/GRUCell loop with Gaussian self-feedback
+//
+// Data layout in HBM (all fp32, row-major, "rows" = packed frames, time-major
+// exactly like PackedSequence.data; step t owns rows [off_t, off_t + bs_t)):
+//   X (L x Fp)   input frames, F padded to Fp = roundup(F, 16) with zeros
+//   GX (L x D*G*H) input projection of all frames, one MFMA GEMM per layer
+//   Hprev/Cprev (L x H)  the recurrent state each row CONSUMES; written by the
+//                predecessor step's epilogue, zeroed by the row's own step when
+//                the sequence has no predecessor.  Because row r's operand is
+//                row r of Hprev, the recurrent GEMM reads a contiguous block and
+//                the weight-gradient GEMM dW_hh = dG^T Hprev is one K=L GEMM.
+//   Gst (L x 4H) activated gates (LSTM i,f,g,o; GRU r,z,n,W_hn h+b_hn)
+// One launch per time step (both encoder directions share it).  A workgroup
+// (4 waves, wave split-K) owns 16 rows x 16 units x G gates, so the LSTM/GRU
+// cell update runs in the GEMM epilogue out of LDS.
+#include <vector>
+
+#include "abcd_common.h"
+#include "abcd_internal.h"
+
+namespace abcd {
+
+int validate_batch(const int64_t* bs, int T, int L, int B) {
+  if (!bs || T <= 0 || L <= 0 || B <= 0) return ABCD_EINVAL;
+  if (bs[0] != B) return ABCD_EINVAL;
+  long s = 0;
+  for (int t = 0; t < T; ++t) {
+    if (bs[t] <= 0 || (t && bs[t] > bs[t - 1])) return ABCD_EINVAL;
+    s += bs[t];
+  }
+  return s == L ? 0 : ABCD_EINVAL;
+}
+
+static std::vector<int> step_offsets(const int64_t* bs, int T) {
+  std::vector<int> off(T + 1, 0);
+  for (int t = 0; t < T; ++t) off[t + 1] = off[t] + (int)bs[t];
+  return off;
+}
+
+// ===========================================================================
+// forward step: gates = [x-part] + Hprev_rows @ W_hh^T, cell update epilogue
+// ===========================================================================
+struct FwdDir {
+  const float* Ah; int prev_valid;            // Hprev + off*H
+  const float* Whh;                           // G*H x H
+  const float* Ax; long ldx; int xrows;       // decoder input rows (Xin + off*ldx)
+  const float* Wih; long ldwih; int nchx;     // decoder W_ih (G*H x Fp)
+  const float* GX; long ldgx;                 // encoder input projection (bias folded in)
+  const float* bih; const float* bhh;         // decoder b_ih(+b_hh for LSTM); GRU b_hh
+  float* Gst; float* Cst; float* Y; long ldy; float* Hprev; float* Cprev;
+  float* out; long ldo; int hcol, ccol;       // encoder final state (last_hidden)
+  int off, bs, next_off, next_bs, tiles;
+};
+struct FwdArgs { FwdDir d[2]; int H; int nd; };
+
+template <int G>
+__global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
+  constexpr int TN = 16 * G, LD = TN + 4, TSZ = 16 * LD;
+  __shared__ __attribute__((aligned(16))) float lds[2 * 4 * TSZ];
+  int blk = blockIdx.x;
+  int sel = 0;
+  if (a.nd == 2 && blk >= a.d[0].tiles) { blk -= a.d[0].tiles; sel = 1; }
+  const FwdDir& D = a.d[sel];
+  const int H = a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
+  const int nut = H / 16;
+  const int ut = blk % nut, rt = blk / nut;
+  f4 accH[1][G], accX[1][G];
+  acc_zero(accH);
+  acc_zero(accX);
+  const int ar[1] = {rt * 16 + r};
+  int br[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) br[j] = j * H + ut * 16 + r;
+  const int nchh = H / 16;
+  wave_mma<1, G>(accH, KC{D.Ah, H, D.prev_valid}, ar, KC{D.Whh, H, G * H}, br, w, nchh, 4, q);
+  if (D.xrows > 0)
+    wave_mma<1, G>(accX, KC{D.Ax, D.ldx, D.xrows}, ar, KC{D.Wih, D.ldwih, G * H}, br, first_chunk(w, nchh),
+                   D.nchx, 4, q);
+  reduce_waves_to_lds<1, G>(accH, lds, w, lane);
+  reduce_waves_to_lds<1, G>(accX, lds + 4 * TSZ, w, lane);
+  const float* tH = lds;
+  const float* tX = lds + 4 * TSZ;
+  const int row = threadIdx.x >> 4, u = threadIdx.x & 15;
+  const int b = rt * 16 + row;
+  if (b >= D.bs) return;
+  const int unit = ut * 16 + u;
+  const long rr = D.off + b;
+  float gx[G], gh[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    gh[j] = tH[row * LD + j * 16 + u];
+    gx[j] = tX[row * LD + j * 16 + u];
+    if (D.GX) gx[j] += D.GX[rr * D.ldgx + j * H + unit];
+    if (D.bih) gx[j] += D.bih[j * H + unit];
+  }
+  const bool haspred = b < D.prev_valid;
+  float* Gr = D.Gst + rr * 4 * H;
+  float h, c = 0.f;
+  if (G == 4) {
+    const float i_ = sigmoidf_(gx[0] + gh[0]);
+    const float f_ = sigmoidf_(gx[1] + gh[1]);
+    const float g_ = tanhf(gx[2] + gh[2]);
+    const float o_ = sigmoidf_(gx[3] + gh[3]);
+    const float cp = haspred ? D.Cprev[rr * H + unit] : 0.f;
+    c = f_ * cp + i_ * g_;
+    h = o_ * tanhf(c);
+    Gr[unit] = i_; Gr[H + unit] = f_; Gr[2 * H + unit] = g_; Gr[3 * H + unit] = o_;
+    D.Cst[rr * H + unit] = c;
+    if (!haspred) { D.Cprev[rr * H + unit] = 0.f; D.Hprev[rr * H + unit] = 0.f; }
+  } else {
+#pragma unroll
+    for (int j = 0; j < G; ++j) gh[j] += D.bhh[j * H + unit];
+    const float r_ = sigmoidf_(gx[0] + gh[0]);
+    const float z_ = sigmoidf_(gx[1] + gh[1]);
+    const float n_ = tanhf(gx[2] + r_ * gh[G - 1]);
+    const float hp = haspred ? D.Hprev[rr * H + unit] : 0.f;
+    h = (1.f - z_) * n_ + z_ * hp;
+    Gr[unit] = r_; Gr[H + unit] = z_; Gr[2 * H + unit] = n_; Gr[3 * H + unit] = gh[G - 1];
+    if (!haspred) D.Hprev[rr * H + unit] = 0.f;
+  }
+  D.Y[rr * D.ldy + unit] = h;
+  if (b < D.next_bs) {
+    D.Hprev[(long)(D.next_off + b) * H + unit] = h;
+    if (G == 4) D.Cprev[(long)(D.next_off + b) * H + unit] = c;
+  } else if (D.out) {
+    D.out[(long)b * D.ldo + D.hcol + unit] = h;
+    if (G == 4) D.out[(long)b * D.ldo + D.ccol + unit] = c;
+  }
+}
+
+// ===========================================================================
+// backward step: dh = dG_succ @ W_hh (+ dZ @ W1cat for the decoder) + extra,
+// then the cell backward in the epilogue -> dG (for the next GEMM and for
+// the weight gradients), carry (dc for LSTM, dh*z for GRU) to the predecessor
+// ===========================================================================
+struct BwdDir {
+  const float* Ag; int succ_valid;            // dGH + succ_off*G*H
+  const float* WhhT;                          // H x G*H
+  const float* Az; int zrows; const float* W1T; long ldz; int nchz;  // decoder: dZ rows, W1cat^T (H x 2Hm)
+  const float* DHX; long lddhx;               // extra dh rows (upper layer / offset head)
+  const float* dlast; long ldl; int hcol, ccol;  // final-state grads (encoder)
+  const float* Gst; const float* Cst; const float* Cprev; const float* Hprev;
+  float* dGX; float* dGH;                     // row-major, ld G*H (LSTM: same buffer)
+  float* DC;                                  // carry rows read at this step
+  float* DCpred; int pred_off;                // carry destination for the predecessor
+  int off, bs, prev_valid, next_bs, tiles;
+};
+struct BwdArgs { BwdDir d[2]; int H; int nd; };
+
+template <int G, int NR>
+__global__ __launch_bounds__(256) void rnn_bwd_step(BwdArgs a) {
+  constexpr int TN = 16 * NR, LD = TN + 4;
+  __shared__ __attribute__((aligned(16))) float lds[4 * 16 * LD];
+  int blk = blockIdx.x;
+  int sel = 0;
+  if (a.nd == 2 && blk >= a.d[0].tiles) { blk -= a.d[0].tiles; sel = 1; }
+  const BwdDir& D = a.d[sel];
+  const int H = a.H, GH = G * H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
+  const int nut = H / TN;
+  const int ut = blk % nut, rt = blk / nut;
+  f4 acc[1][NR];
+  acc_zero(acc);
+  const int ar[1] = {rt * 16 + r};
+  int br[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) br[j] = ut * TN + 16 * j + r;
+  const int nchg = GH / 16;
+  if (D.succ_valid > 0)
+    wave_mma<1, NR>(acc, KC{D.Ag, GH, D.succ_valid}, ar, KC{D.WhhT, GH, H}, br, w, nchg, 4, q);
+  if (D.zrows > 0)
+    wave_mma<1, NR>(acc, KC{D.Az, D.ldz, D.zrows}, ar, KC{D.W1T, D.ldz, H}, br, first_chunk(w, nchg), D.nchz, 4,
+                    q);
+  reduce_waves_to_lds<1, NR>(acc, lds, w, lane);
+  for (int e = threadIdx.x; e < 16 * TN; e += 256) {
+    const int row = e / TN, cu = e % TN;
+    const int b = rt * 16 + row;
+    if (b >= D.bs) continue;
+    const int unit = ut * TN + cu;
+    const long rr = D.off + b;
+    float dh = lds[row * LD + cu];
+    if (D.DHX) dh += D.DHX[rr * D.lddhx + unit];
+    const bool fin = b >= D.next_bs;
+    if (fin && D.dlast) dh += D.dlast[(long)b * D.ldl + D.hcol + unit];
+    const bool haspred = b < D.prev_valid;
+    const float* Gr = D.Gst + rr * 4 * H;
+    if (G == 4) {
+      float dcin = 0.f;
+      if (!fin) dcin = D.DC[rr * H + unit];
+      else if (D.dlast && D.ccol >= 0) dcin = D.dlast[(long)b * D.ldl + D.ccol + unit];
+      const float i_ = Gr[unit], f_ = Gr[H + unit], g_ = Gr[2 * H + unit], o_ = Gr[3 * H + unit];
+      const float c = D.Cst[rr * H + unit];
+      const float cp = haspred ? D.Cprev[rr * H + unit] : 0.f;
+      const float tc = tanhf(c);
+      const float dc = dcin + dh * o_ * (1.f - tc * tc);
+      float* dg = D.dGX + rr * GH;
+      dg[unit] = dc * g_ * i_ * (1.f - i_);
+      dg[H + unit] = dc * cp * f_ * (1.f - f_);
+      dg[2 * H + unit] = dc * i_ * (1.f - g_ * g_);
+      dg[3 * H + unit] = dh * tc * o_ * (1.f - o_);
+      if (haspred) D.DCpred[(long)(D.pred_off + b) * H + unit] = dc * f_;
+    } else {
+      if (!fin) dh += D.DC[rr * H + unit];
+      const float r_ = Gr[unit], z_ = Gr[H + unit], n_ = Gr[2 * H + unit], ghn = Gr[3 * H + unit];
+      const float hp = haspred ? D.Hprev[rr * H + unit] : 0.f;
+      const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
+      const float dzp = dh * (hp - n_) * z_ * (1.f - z_);
+      const float drp = dnp * ghn * r_ * (1.f - r_);
+      float* dx = D.dGX + rr * GH;
+      float* dhh = D.dGH + rr * GH;
+      dx[unit] = drp; dx[H + unit] = dzp; dx[2 * H + unit] = dnp;
+      dhh[unit] = drp; dhh[H + unit] = dzp; dhh[2 * H + unit] = dnp * r_;
+      if (haspred) D.DCpred[(long)(D.pred_off + b) * H + unit] = dh * z_;
+    }
+  }
+}
+
+template <int G>
+static int launch_bwd_step(hipStream_t s, const BwdArgs& a, int grid, int H) {
+  if ((H / 16) % 4 == 0)
+    rnn_bwd_step<G, 4><<<grid, 256, 0, s>>>(a);
+  else if ((H / 16) % 2 == 0)
+    rnn_bwd_step<G, 2><<<grid, 256, 0, s>>>(a);
+  else
+    rnn_bwd_step<G, 1><<<grid, 256, 0, s>>>(a);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+static int bwd_tn(int H) { return (H / 16) % 4 == 0 ? 64 : ((H / 16) % 2 == 0 ? 32 : 16); }
+
+// ===========================================================================
+// ENCODER
+// ===========================================================================
+struct EncWS {
+  float* Xp;
+  float* Wihp[ABCD_MAX_LAYERS];
+  float* bcat[ABCD_MAX_LAYERS];
+  float* WhhT[ABCD_MAX_LAYERS][2];
+  float* WihT[ABCD_MAX_LAYERS][2];
+  float* GX;
+  float* Y[ABCD_MAX_LAYERS];
+  float* Gst[ABCD_MAX_LAYERS][2];
+  float* Cst[ABCD_MAX_LAYERS][2];
+  float* Hprev[ABCD_MAX_LAYERS][2];
+  float* Cprev[ABCD_MAX_LAYERS][2];
+  float* dGX[ABCD_MAX_LAYERS][2];
+  float* dGH[ABCD_MAX_LAYERS][2];
+  float* DC[ABCD_MAX_LAYERS][2];
+  float* DHX[ABCD_MAX_LAYERS];
+  float* scratch;
+  size_t scratch_floats;
+};
+
+static int enc_check(const abcd_encoder_cfg* c) {
+  if (!c || c->hidden_size <= 0 || c->hidden_size % 16 || c->layers < 1 || c->layers > ABCD_MAX_LAYERS ||
+      c->input_size <= 0 || (c->rnn_type != ABCD_LSTM && c->rnn_type != ABCD_GRU))
+    return ABCD_EINVAL;
+  return 0;
+}
+
+static EncWS carve_encoder(Arena& A, const abcd_encoder_cfg* c, int T, int L, int B) {
+  EncWS w{};
+  const int H = c->hidden_size, D = c->bidirectional ? 2 : 1, G = c->rnn_type == ABCD_LSTM ? 4 : 3;
+  const int F = c->input_size, Fp = rup16(F);
+  w.Xp = A.f((size_t)L * Fp);
+  size_t maxMN = 0;
+  for (int l = 0; l < c->layers; ++l) {
+    const int In = l == 0 ? F : D * H, Inp = l == 0 ? Fp : D * H;
+    w.Wihp[l] = A.f((size_t)D * G * H * Inp);
+    w.bcat[l] = A.f((size_t)D * G * H);
+    for (int d = 0; d < D; ++d) {
+      w.WhhT[l][d] = A.f((size_t)H * G * H);
+      w.WihT[l][d] = l > 0 ? A.f((size_t)In * G * H) : nullptr;
+      w.Gst[l][d] = A.f((size_t)L * 4 * H);
+      w.Cst[l][d] = c->rnn_type == ABCD_LSTM ? A.f((size_t)L * H) : nullptr;
+      w.Hprev[l][d] = A.f((size_t)L * H);
+      w.Cprev[l][d] = c->rnn_type == ABCD_LSTM ? A.f((size_t)L * H) : nullptr;
+      w.dGX[l][d] = A.f((size_t)L * G * H);
+      w.dGH[l][d] = c->rnn_type == ABCD_LSTM ? w.dGX[l][d] : A.f((size_t)L * G * H);
+      w.DC[l][d] = A.f((size_t)L * H);
+    }
+    w.Y[l] = A.f((size_t)L * D * H);
+    w.DHX[l] = l + 1 < c->layers ? A.f((size_t)L * D * H) : nullptr;
+    maxMN = std::max(maxMN, (size_t)G * H * std::max(In, H));
+  }
+  w.GX = A.f((size_t)L * D * G * H);
+  w.scratch_floats = std::max(maxMN * 16, (size_t)1 << 20);
+  w.scratch = A.f(w.scratch_floats);
+  (void)T; (void)B;
+  return w;
+}
+
+}  // namespace abcd
+
+using namespace abcd;
+
+extern "C" int abcd_encoder_out_size(const abcd_encoder_cfg* c) {
+  if (enc_check(c)) return -1;
+  int e = c->layers * c->hidden_size * (c->bidirectional ? 2 : 1);
+  return c->rnn_type == ABCD_LSTM ? 2 * e : e;
+}
+
+extern "C" size_t abcd_encoder_workspace_bytes(const abcd_encoder_cfg* c, int T, int L, int B) {
+  if (enc_check(c)) return 0;
+  Arena A(nullptr, 0);
+  carve_encoder(A, c, T, L, B);
+  return A.off + 256;
+}
+
+extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encoder_params* p, const abcd_packed* x,
+                                    float* last_hidden, void* ws, size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(enc_check(c) == 0 && p && x && x->data && last_hidden && ws);
+  ABCD_REQUIRE(x->F == c->input_size);
+  ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
+  hipStream_t s = (hipStream_t)stream;
+  Arena A(ws, ws_bytes);
+  EncWS w = carve_encoder(A, c, x->T, x->L, x->B);
+  ABCD_REQUIRE(A.ok);
+  const int H = c->hidden_size, D = c->bidirectional ? 2 : 1, G = c->rnn_type == ABCD_LSTM ? 4 : 3;
+  const int F = c->input_size, Fp = rup16(F), T = x->T, L = x->L;
+  const int E = abcd_encoder_out_size(c);
+  const std::vector<int> off = step_offsets(x->batch_sizes, T);
+  const int64_t* bs = x->batch_sizes;
+  ABCD_TRY((hipError_t)pack2d(s, x->data, F, L, F, false, w.Xp, Fp, L, Fp));
+  for (int l = 0; l < c->layers; ++l) {
+    const int In = l == 0 ? F : D * H, Inp = l == 0 ? Fp : D * H;
+    for (int d = 0; d < D; ++d) {
+      const abcd_rnn_w& W = p->w[l][d];
+      ABCD_REQUIRE(W.w_ih && W.w_hh && W.b_ih && W.b_hh);
+      ABCD_TRY((hipError_t)pack2d(s, W.w_ih, In, G * H, In, false, w.Wihp[l] + (size_t)d * G * H * Inp, Inp,
+                                  G * H, Inp));
+      if (G == 4)
+        ABCD_TRY((hipError_t)add_vec(s, W.b_ih, W.b_hh, w.bcat[l] + d * G * H, G * H));
+      else
+        ABCD_TRY((hipError_t)pack2d(s, W.b_ih, G * H, 1, G * H, false, w.bcat[l] + d * G * H, G * H, 1, G * H));
+    }
+    const float* X = l == 0 ? w.Xp : w.Y[l - 1];
+    ABCD_TRY((hipError_t)gemm(s, L, D * G * H, Inp, opKC(X, Inp, L), opKC(w.Wihp[l], Inp, D * G * H), w.GX,
+                              (long)D * G * H, 1.f, 0.f, w.bcat[l], ACT_NONE, w.scratch, w.scratch_floats));
+    for (int i = 0; i < T; ++i) {
+      FwdArgs a{};
+      a.H = H;
+      a.nd = D;
+      for (int d = 0; d < D; ++d) {
+        const bool rev = d == 1;
+        const int t = rev ? T - 1 - i : i;
+        FwdDir& f = a.d[d];
+        const abcd_rnn_w& W = p->w[l][d];
+        const int prev_valid = rev ? (t == T - 1 ? 0 : (int)bs[t + 1]) : (t == 0 ? 0 : (int)bs[t]);
+        f.Ah = w.Hprev[l][d] + (size_t)off[t] * H;
+        f.prev_valid = prev_valid;
+        f.Whh = W.w_hh;
+        f.Ax = nullptr; f.ldx = 0; f.xrows = 0; f.Wih = nullptr; f.ldwih = 0; f.nchx = 0;
+        f.GX = w.GX + (size_t)d * G * H;
+        f.ldgx = (long)D * G * H;
+        f.bih = nullptr;
+        f.bhh = G == 3 ? W.b_hh : nullptr;
+        f.Gst = w.Gst[l][d]; f.Cst = w.Cst[l][d];
+        f.Y = w.Y[l] + (size_t)d * H; f.ldy = (long)D * H;
+        f.Hprev = w.Hprev[l][d]; f.Cprev = w.Cprev[l][d];
+        f.out = last_hidden; f.ldo = E;
+        const int base = (l * D + d) * (G == 4 ? 2 * H : H);
+        f.hcol = base; f.ccol = G == 4 ? base + H : -1;
+        f.off = off[t]; f.bs = (int)bs[t];
+        if (rev) { f.next_off = t >= 1 ? off[t - 1] : 0; f.next_bs = t >= 1 ? (int)bs[t] : 0; }
+        else { f.next_off = off[t + 1]; f.next_bs = t + 1 < T ? (int)bs[t + 1] : 0; }
+        f.tiles = cdiv(f.bs, 16) * (H / 16);
+      }
+      const int grid = a.d[0].tiles + (D == 2 ? a.d[1].tiles : 0);
+      if (G == 4) rnn_fwd_step<4><<<grid, 256, 0, s>>>(a);
+      else rnn_fwd_step<3><<<grid, 256, 0, s>>>(a);
+      ABCD_CHECK_LAUNCH();
+    }
+  }
+  return 0;
+}
+
+extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encoder_params* p, const abcd_packed* x,
+                                     const float* d_last_hidden, const abcd_encoder_grads* g, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(enc_check(c) == 0 && p && x && x->data && g && ws && d_last_hidden);
+  ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
+  hipStream_t s = (hipStream_t)stream;
+  Arena A(ws, ws_bytes);
+  EncWS w = carve_encoder(A, c, x->T, x->L, x->B);
+  ABCD_REQUIRE(A.ok);
+  const int H = c->hidden_size, D = c->bidirectional ? 2 : 1, G = c->rnn_type == ABCD_LSTM ? 4 : 3;
+  const int F = c->input_size, T = x->T, L = x->L, GH = G * H;
+  const int E = abcd_encoder_out_size(c);
+  const std::vector<int> off = step_offsets(x->batch_sizes, T);
+  const int64_t* bs = x->batch_sizes;
+  const int TN = bwd_tn(H);
+  for (int l = c->layers - 1; l >= 0; --l) {
+    const int In = l == 0 ? F : D * H;
+    for (int d = 0; d < D; ++d)
+      ABCD_TRY((hipError_t)pack2d(s, p->w[l][d].w_hh, H, H, GH, true, w.WhhT[l][d], GH, H, GH));
+    for (int i = 0; i < T; ++i) {
+      BwdArgs a{};
+      a.H = H;
+      a.nd = D;
+      for (int d = 0; d < D; ++d) {
+        const bool rev = d == 1;
+        const int t = rev ? i : T - 1 - i;
+        BwdDir& b = a.d[d];
+        int succ_off, succ_valid, prev_valid, pred_off;
+        if (!rev) {
+          succ_off = off[t + 1]; succ_valid = t + 1 < T ? (int)bs[t + 1] : 0;
+          prev_valid = t == 0 ? 0 : (int)bs[t]; pred_off = t >= 1 ? off[t - 1] : 0;
+        } else {
+          succ_off = t >= 1 ? off[t - 1] : 0; succ_valid = t >= 1 ? (int)bs[t] : 0;
+          prev_valid = t == T - 1 ? 0 : (int)bs[t + 1]; pred_off = off[t + 1];
+        }
+        b.Ag = w.dGH[l][d] + (size_t)succ_off * GH;
+        b.succ_valid = succ_valid;
+        b.WhhT = w.WhhT[l][d];
+        b.Az = nullptr; b.zrows = 0; b.W1T = nullptr; b.ldz = 0; b.nchz = 0;
+        b.DHX = l + 1 < c->layers ? w.DHX[l] + (size_t)d * H : nullptr;
+        b.lddhx = (long)D * H;
+        b.dlast = d_last_hidden; b.ldl = E;
+        const int base = (l * D + d) * (G == 4 ? 2 * H : H);
+        b.hcol = base; b.ccol = G == 4 ? base + H : -1;
+        b.Gst = w.Gst[l][d]; b.Cst = w.Cst[l][d]; b.Cprev = w.Cprev[l][d]; b.Hprev = w.Hprev[l][d];
+        b.dGX = w.dGX[l][d]; b.dGH = w.dGH[l][d];
+        b.DC = w.DC[l][d]; b.DCpred = w.DC[l][d]; b.pred_off = pred_off;
+        b.off = off[t]; b.bs = (int)bs[t]; b.prev_valid = prev_valid; b.next_bs = succ_valid;
+        b.tiles = cdiv(b.bs, 16) * (H / TN);
+      }
+      const int grid = a.d[0].tiles + (D == 2 ? a.d[1].tiles : 0);
+      if (G == 4) ABCD_TRY((hipError_t)launch_bwd_step<4>(s, a, grid, H));
+      else ABCD_TRY((hipError_t)launch_bwd_step<3>(s, a, grid, H));
+    }
+    // weight gradients: reductions over all L packed frames (K = L, K-major operands)
+    for (int d = 0; d < D; ++d) {
+      const abcd_rnn_g& gr = g->g[l][d];
+      const float* X = l == 0 ? x->data : w.Y[l - 1];
+      const long ldxx = l == 0 ? F : (long)D * H;
+      if (gr.w_ih)
+        ABCD_TRY((hipError_t)gemm(s, GH, In, L, opKM(w.dGX[l][d], GH, GH), opKM(X, ldxx, In), gr.w_ih, In, 1.f, 0.f,
+                                  nullptr, ACT_NONE, w.scratch, w.scratch_floats));
+      if (gr.w_hh)
+        ABCD_TRY((hipError_t)gemm(s, GH, H, L, opKM(w.dGH[l][d], GH, GH), opKM(w.Hprev[l][d], H, H), gr.w_hh, H,
+                                  1.f, 0.f, nullptr, ACT_NONE, w.scratch, w.scratch_floats));
+      if (gr.b_ih)
+        ABCD_TRY((hipError_t)colsum(s, w.dGX[l][d], GH, L, GH, nullptr, gr.b_ih, 0.f, w.scratch, w.scratch_floats));
+      if (gr.b_hh)
+        ABCD_TRY((hipError_t)colsum(s, w.dGH[l][d], GH, L, GH, nullptr, gr.b_hh, 0.f, w.scratch, w.scratch_floats));
+    }
+    if (l > 0) {  // dX of this layer = dh of the layer below (both directions)
+      for (int d = 0; d < D; ++d) {
+        ABCD_TRY((hipError_t)pack2d(s, p->w[l][d].w_ih, In, In, GH, true, w.WihT[l][d], GH, In, GH));
+        ABCD_TRY((hipError_t)gemm(s, L, In, GH, opKC(w.dGX[l][d], GH, L), opKC(w.WihT[l][d], GH, In), w.DHX[l - 1],
+                                  In, 1.f, d == 0 ? 0.f : 1.f, nullptr, ACT_NONE, w.scratch, w.scratch_floats));
+      }
+    }
+  }
+  return 0;
+}
+
+// ===========================================================================
+// DECODER (model.py:147-196): per step t
+//   D1 rnn_fwd_step    gates = Xin_rows @ W_ih^T + Hprev_rows @ W_hh^T (+b), cell
+//   D2 gemm (tanh)     Aact = tanh(h @ [W1_mu; W1_lv]^T + b1)        (bs x 2Hm)
+//   D3 dec_emit_fwd    [mu | lv] = Aact_{mu|lv} @ W2^T + b2, x = mu + e^{lv/2} eps
+//                      -> Xin rows of step t+1 (self-feedback)
+// backward per step (t = T-1 .. 0)
+//   E1 dec_emit_bwd_x  dx_{t+1} = dGX_{t+1} @ W_ih ; dmu, dlv (+ emission NLL grad)
+//   E2 dec_mlp_bwd     dZ = ([dmu|dlv] @ W2) * (1 - Aact^2)
+//   E3 rnn_bwd_step    dh = dZ @ W1cat + dG_{t+1} @ W_hh + dh_offset ; cell bwd
+// ===========================================================================
+namespace abcd {
+
+struct EmitFwd {
+  const float* Aact; long lda; int Hm, nch;
+  const float *W2m, *W2l, *b2m, *b2l;  // padded Fp x Hm, Fp
+  const float* eps; uint64_t seed, offset;
+  float *MU, *LV, *OUT, *Xin; int F, Fp;
+  int off, bs, next_off, next_bs, feedback;
+};
+
+__global__ __launch_bounds__(256) void dec_emit_fwd(EmitFwd a) {
+  constexpr int LD = 20;
+  __shared__ __attribute__((aligned(16))) float lds[2 * 4 * 16 * LD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
+  const int nct = a.Fp / 16;
+  const int ct = blockIdx.x % nct, rt = blockIdx.x / nct;
+  f4 am[1][1], al[1][1];
+  acc_zero(am);
+  acc_zero(al);
+  const int ar[1] = {rt * 16 + r};
+  const int br[1] = {ct * 16 + r};
+  const float* Arows = a.Aact + (long)a.off * a.lda;
+  wave_mma<1, 1>(am, KC{Arows, a.lda, a.bs}, ar, KC{a.W2m, a.Hm, a.Fp}, br, w, a.nch, 4, q);
+  wave_mma<1, 1>(al, KC{Arows + a.Hm, a.lda, a.bs}, ar, KC{a.W2l, a.Hm, a.Fp}, br, w, a.nch, 4, q);
+  reduce_waves_to_lds<1, 1>(am, lds, w, lane);
+  reduce_waves_to_lds<1, 1>(al, lds + 4 * 16 * LD, w, lane);
+  const int row = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  const int b = rt * 16 + row;
+  if (b >= a.bs) return;
+  const int j = ct * 16 + cc;
+  const long rr = a.off + b;
+  float mu = 0.f, lv = 0.f, x = 0.f;
+  if (j < a.F) {
+    mu = lds[row * LD + cc] + a.b2m[j];
+    lv = lds[4 * 16 * LD + row * LD + cc] + a.b2l[j];
+    const float e = a.eps ? a.eps[rr * a.F + j] : philox_normal(a.seed, a.offset + (uint64_t)rr * a.F + j);
+    x = mu + __expf(0.5f * lv) * e;
+  }
+  a.MU[rr * a.Fp + j] = mu;
+  a.LV[rr * a.Fp + j] = lv;
+  a.OUT[rr * a.Fp + j] = x;
+  if (a.feedback && b < a.next_bs) a.Xin[(long)(a.next_off + b) * a.Fp + j] = x;
+}
+
+struct EmitBwdX {
+  const float* Ag; long ldg; int succ_valid; int nch;  // dGX rows of step t+1
+  const float* WihT;                                  // Fp x G*H
+  const float *MU, *LV, *OUT, *Y;                     // stash (ld Fp), gt (ld F)
+  const float* s_em;                                  // device scalar
+  float *dMU, *dLV; int F, Fp; int off, bs;
+};
+
+__global__ __launch_bounds__(256) void dec_emit_bwd_x(EmitBwdX a) {
+  constexpr int LD = 20;
+  __shared__ __attribute__((aligned(16))) float lds[4 * 16 * LD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
+  const int nct = a.Fp / 16;
+  const int ct = blockIdx.x % nct, rt = blockIdx.x / nct;
+  f4 acc[1][1];
+  acc_zero(acc);
+  const int ar[1] = {rt * 16 + r};
+  const int br[1] = {ct * 16 + r};
+  if (a.succ_valid > 0) wave_mma<1, 1>(acc, KC{a.Ag, a.ldg, a.succ_valid}, ar, KC{a.WihT, a.ldg, a.Fp}, br, w, a.nch, 4, q);
+  reduce_waves_to_lds<1, 1>(acc, lds, w, lane);
+  const int row = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  const int b = rt * 16 + row;
+  if (b >= a.bs) return;
+  const int j = ct * 16 + cc;
+  const long rr = a.off + b;
+  float dmu = 0.f, dlv = 0.f;
+  if (j < a.F) {
+    const float dx = lds[row * LD + cc];
+    const float mu = a.MU[rr * a.Fp + j], lv = a.LV[rr * a.Fp + j], o = a.OUT[rr * a.Fp + j];
+    const float y = a.Y[rr * a.F + j];
+    const float s = *a.s_em;
+    const float iv = __expf(-lv), d = y - mu;
+    dmu = dx + s * (-d) * iv;
+    dlv = dx * 0.5f * (o - mu) + s * 0.5f * (1.f - d * d * iv);
+  }
+  a.dMU[rr * a.Fp + j] = dmu;
+  a.dLV[rr * a.Fp + j] = dlv;
+}
+
+struct MlpBwd {
+  const float *dMU, *dLV; int Fp, nch;   // rows (ld Fp)
+  const float *W2mT, *W2lT;              // Hm x Fp
+  const float* Aact; float* dZ; int Hm;  // ld 2Hm
+  int off, bs;
+};
+
+template <int NR>
+__global__ __launch_bounds__(256) void dec_mlp_bwd(MlpBwd a) {
+  constexpr int TN = 16 * NR, LD = TN + 4;
+  __shared__ __attribute__((aligned(16))) float lds[2 * 4 * 16 * LD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
+  const int nct = a.Hm / TN;
+  const int ct = blockIdx.x % nct, rt = blockIdx.x / nct;
+  f4 am[1][NR], al[1][NR];
+  acc_zero(am);
+  acc_zero(al);
+  const int ar[1] = {rt * 16 + r};
+  int br[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) br[j] = ct * TN + 16 * j + r;
+  const long o = (long)a.off * a.Fp;
+  wave_mma<1, NR>(am, KC{a.dMU + o, a.Fp, a.bs}, ar, KC{a.W2mT, a.Fp, a.Hm}, br, w, a.nch, 4, q);
+  wave_mma<1, NR>(al, KC{a.dLV + o, a.Fp, a.bs}, ar, KC{a.W2lT, a.Fp, a.Hm}, br, w, a.nch, 4, q);
+  reduce_waves_to_lds<1, NR>(am, lds, w, lane);
+  reduce_waves_to_lds<1, NR>(al, lds + 4 * 16 * LD, w, lane);
+  const int H2 = 2 * a.Hm;
+  for (int e = threadIdx.x; e < 16 * TN; e += 256) {
+    const int row = e / TN, cc = e % TN;
+    const int b = rt * 16 + row;
+    if (b >= a.bs) continue;
+    const int j = ct * TN + cc;
+    const long rr = a.off + b;
+    const float xm = a.Aact[rr * H2 + j], xl = a.Aact[rr * H2 + a.Hm + j];
+    a.dZ[rr * H2 + j] = lds[row * LD + cc] * (1.f - xm * xm);
+    a.dZ[rr * H2 + a.Hm + j] = lds[4 * 16 * LD + row * LD + cc] * (1.f - xl * xl);
+  }
+}
+
+// ---- small decoder helpers ------------------------------------------------
+// FS = [features | embed_speaker[speaker]]
+__global__ void dec_feats(const float* feats, int D, const float* emb, const int64_t* spk, int S, int B, float* FS) {
+  const int DS = D + S;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < B * DS; i += gridDim.x * 256) {
+    const int b = i / DS, c = i % DS;
+    FS[i] = c < D ? feats[(long)b * D + c] : emb[spk[b] * S + (c - D)];
+  }
+}
+// rows [0,B) of Hprev/Cprev from feature2hidden (LSTM: interleaved h/c, model.py:100,262-263); Xin rows [0,B) = 0
+__global__ void dec_init(const float* Hinit, int B, int H, int lstm, float* Hprev, float* Cprev, float* Xin, int Fp) {
+  const int n = B * H;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int b = i / H, u = i % H;
+    if (lstm) {
+      Hprev[i] = Hinit[(long)b * 2 * H + 2 * u];
+      Cprev[i] = Hinit[(long)b * 2 * H + 2 * u + 1];
+    } else {
+      Hprev[i] = Hinit[(long)b * H + u];
+    }
+  }
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < B * Fp; i += gridDim.x * 256) Xin[i] = 0.f;
+}
+// offset head (model.py:121-122,191,195): logit = Zo . w2 + b2 ; BCE-with-logits (sum)
+__global__ void dec_offset_head(const float* Zo, int L, int Hm, const float* w2, const float* b2, const float* tgt,
+                                float* logit, float* dlog_raw, float* bce) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= L) return;
+  float s = 0.f;
+  for (int j = lane; j < Hm; j += 64) s += Zo[(long)row * Hm + j] * w2[j];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if (lane == 0) {
+    const float x = s + b2[0];
+    logit[row] = x;
+    if (tgt) {
+      const float y = tgt[row];
+      bce[row] = fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
+      dlog_raw[row] = 1.f / (1.f + __expf(-x)) - y;
+    }
+  }
+}
+// emission NLL partial sums: 0.5*(log 2pi + lv + (y-mu)^2 e^{-lv}) over L x F
+__global__ void dec_emission_nll(const float* MU, const float* LV, int Fp, const float* Y, int F, long L,
+                                 double* part) {
+  __shared__ double sh[16];
+  double acc = 0.0;
+  const long n = L * F;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / F;
+    const int j = (int)(i % F);
+    const float mu = MU[r * Fp + j], lv = LV[r * Fp + j], d = Y[i] - mu;
+    acc += 0.5f * (1.8378770664093453f + lv + d * d * __expf(-lv));
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) sh[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += sh[k];
+    part[blockIdx.x] = t;
+  }
+}
+__global__ void sum_partials(const double* part, int np, float* out) {
+  __shared__ double sh[4];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) v += part[i];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += sh[k];
+    *out = (float)t;
+  }
+}
+// offset-head backward: dlog = s_off * (sigmoid(x) - y); dZo = dlog * w2 * (1 - Zo^2)
+__global__ void dec_offset_bwd(const float* Zo, int L, int Hm, const float* w2, const float* dlog_raw,
+                               const float* s_off, float* dZo, float* dlog_s) {
+  const long n = (long)L * Hm;
+  const float s = *s_off;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / Hm;
+    const int j = (int)(i % Hm);
+    const float z = Zo[i];
+    const float dl = s * dlog_raw[r];
+    dZo[i] = dl * w2[j] * (1.f - z * z);
+    if (j == 0) dlog_s[r] = dl;
+  }
+}
+// gradient of feature2hidden output from the t=0 carries
+__global__ void dec_hidden_init_bwd(const float* dH0, const float* DC0, int B, int H, int lstm, float* dhid) {
+  const int n = B * H;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int b = i / H, u = i % H;
+    if (lstm) {
+      dhid[(long)b * 2 * H + 2 * u] = dH0[i];
+      dhid[(long)b * 2 * H + 2 * u + 1] = DC0[i];
+    } else {
+      dhid[i] = dH0[i] + DC0[i];
+    }
+  }
+}
+// d_features = dFS[:, :D]; embedding grad rows (deterministic: one thread per (speaker, col))
+__global__ void dec_feats_bwd(const float* dFS, int D, int S, int B, const int64_t* spk, int nspk, float* dfeat,
+                              float* demb) {
+  const int DS = D + S;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < B * D; i += gridDim.x * 256) {
+    const int b = i / D, c = i % D;
+    if (dfeat) dfeat[i] = dFS[(long)b * DS + c];
+  }
+  if (!demb) return;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nspk * S; i += gridDim.x * 256) {
+    const int sp = i / S, c = i % S;
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b)
+      if (spk[b] == sp) acc += dFS[(long)b * DS + D + c];
+    demb[i] = acc;
+  }
+}
+// copy a padded (rows x Fp) stash into a user (rows x F) buffer
+__global__ void unpad_rows(const float* src, int Fp, float* dst, int F, long rows) {
+  const long n = rows * F;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = src[(i / F) * Fp + (i % F)];
+}
+
+struct DecWS {
+  // derived weights
+  float *Wihp, *bcomb, *W1cat, *b1cat, *W2mp, *W2lp, *b2mp, *b2lp;
+  float *WihTp, *WhhT, *W2mT, *W2lT, *W1catT, *W1oT, *Wf2hT;
+  // forward stash
+  float *FS, *Hinit, *Xin, *Hprev, *Cprev, *Gst, *Cst, *Hs, *Aact, *MU, *LV, *OUT, *Zo, *offlog, *dlog_raw, *bce;
+  double* part;
+  // backward
+  float *dGX, *dGH, *DC, *DC0, *dH0, *dhid, *dFS, *DHO, *dMU, *dLV, *dZ, *dZo, *dlog_s;
+  float* scratch;
+  size_t scratch_floats;
+};
+
+static int dec_check(const abcd_decoder_cfg* c) {
+  if (!c || c->hidden_size <= 0 || c->hidden_size % 16 || c->mlp_hidden <= 0 || c->mlp_hidden % 16 ||
+      c->feature_size <= 0 || c->feature_size % 16 || c->output_size <= 0 ||
+      (c->rnn_type != ABCD_LSTM && c->rnn_type != ABCD_GRU))
+    return ABCD_EINVAL;
+  if (c->num_speakers > 0 && (c->speaker_dim <= 0 || c->speaker_dim % 16)) return ABCD_EINVAL;
+  return 0;
+}
+
+static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, int B) {
+  DecWS w{};
+  const int H = c->hidden_size, Hm = c->mlp_hidden, F = c->output_size, Fp = rup16(F);
+  const int G = c->rnn_type == ABCD_LSTM ? 4 : 3, GH = G * H;
+  const int Htot = c->rnn_type == ABCD_LSTM ? 2 * H : H;
+  const int DS = c->feature_size + (c->num_speakers > 0 ? c->speaker_dim : 0);
+  w.Wihp = A.f((size_t)GH * Fp); w.bcomb = A.f(GH);
+  w.W1cat = A.f((size_t)2 * Hm * H); w.b1cat = A.f(2 * Hm);
+  w.W2mp = A.f((size_t)Fp * Hm); w.W2lp = A.f((size_t)Fp * Hm); w.b2mp = A.f(Fp); w.b2lp = A.f(Fp);
+  w.WihTp = A.f((size_t)Fp * GH); w.WhhT = A.f((size_t)H * GH);
+  w.W2mT = A.f((size_t)Hm * Fp); w.W2lT = A.f((size_t)Hm * Fp);
+  w.W1catT = A.f((size_t)H * 2 * Hm); w.W1oT = A.f((size_t)H * Hm); w.Wf2hT = A.f((size_t)DS * Htot);
+  w.FS = A.f((size_t)B * DS); w.Hinit = A.f((size_t)B * Htot);
+  w.Xin = A.f((size_t)L * Fp); w.Hprev = A.f((size_t)L * H);
+  w.Cprev = G == 4 ? A.f((size_t)L * H) : nullptr;
+  w.Gst = A.f((size_t)L * 4 * H);
+  w.Cst = G == 4 ? A.f((size_t)L * H) : nullptr;
+  w.Hs = A.f((size_t)L * H); w.Aact = A.f((size_t)L * 2 * Hm);
+  w.MU = A.f((size_t)L * Fp); w.LV = A.f((size_t)L * Fp); w.OUT = A.f((size_t)L * Fp);
+  w.Zo = A.f((size_t)L * Hm); w.offlog = A.f(L); w.dlog_raw = A.f(L); w.bce = A.f(L);
+  w.part = A.d(2048);
+  w.dGX = A.f((size_t)L * GH);
+  w.dGH = G == 4 ? w.dGX : A.f((size_t)L * GH);
+  w.DC = A.f((size_t)L * H); w.DC0 = A.f((size_t)B * H); w.dH0 = A.f((size_t)B * H);
+  w.dhid = A.f((size_t)B * Htot); w.dFS = A.f((size_t)B * DS); w.DHO = A.f((size_t)L * H);
+  w.dMU = A.f((size_t)L * Fp); w.dLV = A.f((size_t)L * Fp); w.dZ = A.f((size_t)L * 2 * Hm);
+  w.dZo = A.f((size_t)L * Hm); w.dlog_s = A.f(L);
+  size_t maxMN = std::max<size_t>({(size_t)GH * std::max(Fp, H), (size_t)Fp * Hm, (size_t)Hm * H,
+                                   (size_t)Htot * DS, (size_t)L});
+  w.scratch_floats = std::max(maxMN * 16, (size_t)1 << 20);
+  w.scratch = A.f(w.scratch_floats);
+  (void)T;
+  return w;
+}
+
+static int launch_grid(long n) { return (int)std::max<long>(1, std::min<long>(4096, cdiv(n, 256))); }
+
+}  // namespace abcd
+
+extern "C" size_t abcd_decoder_workspace_bytes(const abcd_decoder_cfg* c, int T, int L, int B) {
+  if (dec_check(c)) return 0;
+  Arena A(nullptr, 0);
+  carve_decoder(A, c, T, L, B);
+  return A.off + 256;
+}
+
+extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decoder_params* p, const abcd_packed* x,
+                                    const float* features, const int64_t* speakers, const float* gt_offset,
+                                    const float* eps, uint64_t seed, uint64_t offset, float* flatten_out,
+                                    float* mu_out, float* lv_out, float* offset_logits, float* losses, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(dec_check(c) == 0 && p && x && features && ws);
+  ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
+  ABCD_REQUIRE(c->num_speakers == 0 || (speakers && p->embed_speaker));
+  hipStream_t s = (hipStream_t)stream;
+  Arena A(ws, ws_bytes);
+  DecWS w = carve_decoder(A, c, x->T, x->L, x->B);
+  ABCD_REQUIRE(A.ok);
+  const int H = c->hidden_size, Hm = c->mlp_hidden, F = c->output_size, Fp = rup16(F);
+  const int G = c->rnn_type == ABCD_LSTM ? 4 : 3, GH = G * H;
+  const int Htot = G == 4 ? 2 * H : H;
+  const int D = c->feature_size, S = c->num_speakers > 0 ? c->speaker_dim : 0, DS = D + S;
+  const int T = x->T, L = x->L, B = x->B;
+  const int64_t* bs = x->batch_sizes;
+  const std::vector<int> off = step_offsets(bs, T);
+  const abcd_rnn_w& cw = p->cell;
+  // ---- derived (compute-layout) weights ----
+  ABCD_TRY((hipError_t)pack2d(s, cw.w_ih, F, GH, F, false, w.Wihp, Fp, GH, Fp));
+  if (G == 4) ABCD_TRY((hipError_t)add_vec(s, cw.b_ih, cw.b_hh, w.bcomb, GH));
+  else ABCD_TRY((hipError_t)pack2d(s, cw.b_ih, GH, 1, GH, false, w.bcomb, GH, 1, GH));
+  ABCD_TRY((hipError_t)pack2d(s, p->mu.w1, H, Hm, H, false, w.W1cat, H, Hm, H));
+  ABCD_TRY((hipError_t)pack2d(s, p->lv.w1, H, Hm, H, false, w.W1cat + (size_t)Hm * H, H, Hm, H));
+  ABCD_TRY((hipError_t)pack2d(s, p->mu.b1, Hm, 1, Hm, false, w.b1cat, Hm, 1, Hm));
+  ABCD_TRY((hipError_t)pack2d(s, p->lv.b1, Hm, 1, Hm, false, w.b1cat + Hm, Hm, 1, Hm));
+  ABCD_TRY((hipError_t)pack2d(s, p->mu.w2, Hm, F, Hm, false, w.W2mp, Hm, Fp, Hm));
+  ABCD_TRY((hipError_t)pack2d(s, p->lv.w2, Hm, F, Hm, false, w.W2lp, Hm, Fp, Hm));
+  ABCD_TRY((hipError_t)pack2d(s, p->mu.b2, F, 1, F, false, w.b2mp, Fp, 1, Fp));
+  ABCD_TRY((hipError_t)pack2d(s, p->lv.b2, F, 1, F, false, w.b2lp, Fp, 1, Fp));
+  // ---- feature2hidden -> initial state ----
+  const float* FS = features;
+  if (S > 0) {
+    dec_feats<<<launch_grid((long)B * DS), 256, 0, s>>>(features, D, p->embed_speaker, speakers, S, B, w.FS);
+    ABCD_CHECK_LAUNCH();
+    FS = w.FS;
+  }
+  ABCD_TRY((hipError_t)gemm(s, B, Htot, DS, opKC(FS, DS, B), opKC(p->f2h_w, DS, Htot), w.Hinit, Htot, 1.f, 0.f,
+                            p->f2h_b, ACT_NONE, nullptr, 0));
+  dec_init<<<launch_grid((long)B * std::max(H, Fp)), 256, 0, s>>>(w.Hinit, B, H, G == 4, w.Hprev, w.Cprev, w.Xin, Fp);
+  ABCD_CHECK_LAUNCH();
+  // ---- time loop ----
+  for (int t = 0; t < T; ++t) {
+    const int b_t = (int)bs[t];
+    const int nb = t + 1 < T ? (int)bs[t + 1] : 0;
+    FwdArgs a{};
+    a.H = H;
+    a.nd = 1;
+    FwdDir& f = a.d[0];
+    f.Ah = w.Hprev + (size_t)off[t] * H; f.prev_valid = b_t; f.Whh = cw.w_hh;
+    f.Ax = w.Xin + (size_t)off[t] * Fp; f.ldx = Fp; f.xrows = (c->feedback && t > 0) ? b_t : 0;
+    f.Wih = w.Wihp; f.ldwih = Fp; f.nchx = Fp / 16;
+    f.GX = nullptr; f.ldgx = 0; f.bih = w.bcomb; f.bhh = G == 3 ? cw.b_hh : nullptr;
+    f.Gst = w.Gst; f.Cst = w.Cst; f.Y = w.Hs; f.ldy = H; f.Hprev = w.Hprev; f.Cprev = w.Cprev;
+    f.out = nullptr; f.ldo = 0; f.hcol = 0; f.ccol = 0;
+    f.off = off[t]; f.bs = b_t; f.next_off = off[t + 1]; f.next_bs = nb;
+    f.tiles = cdiv(b_t, 16) * (H / 16);
+    if (G == 4) rnn_fwd_step<4><<<f.tiles, 256, 0, s>>>(a);
+    else rnn_fwd_step<3><<<f.tiles, 256, 0, s>>>(a);
+    ABCD_CHECK_LAUNCH();
+    ABCD_TRY((hipError_t)gemm(s, b_t, 2 * Hm, H, opKC(w.Hs + (size_t)off[t] * H, H, b_t), opKC(w.W1cat, H, 2 * Hm),
+                              w.Aact + (size_t)off[t] * 2 * Hm, 2 * Hm, 1.f, 0.f, w.b1cat, ACT_TANH, nullptr, 0));
+    EmitFwd e{};
+    e.Aact = w.Aact; e.lda = 2 * Hm; e.Hm = Hm; e.nch = Hm / 16;
+    e.W2m = w.W2mp; e.W2l = w.W2lp; e.b2m = w.b2mp; e.b2l = w.b2lp;
+    e.eps = eps; e.seed = seed; e.offset = offset;
+    e.MU = w.MU; e.LV = w.LV; e.OUT = w.OUT; e.Xin = w.Xin; e.F = F; e.Fp = Fp;
+    e.off = off[t]; e.bs = b_t; e.next_off = off[t + 1]; e.next_bs = nb; e.feedback = c->feedback;
+    dec_emit_fwd<<<cdiv(b_t, 16) * (Fp / 16), 256, 0, s>>>(e);
+    ABCD_CHECK_LAUNCH();
+  }
+  // ---- offset head over all frames (off the recurrent critical path) ----
+  ABCD_TRY((hipError_t)gemm(s, L, Hm, H, opKC(w.Hs, H, L), opKC(p->offset.w1, H, Hm), w.Zo, Hm, 1.f, 0.f,
+                            p->offset.b1, ACT_TANH, w.scratch, w.scratch_floats));
+  dec_offset_head<<<cdiv(L, 4), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, p->offset.b2, gt_offset, w.offlog,
+                                             w.dlog_raw, w.bce);
+  ABCD_CHECK_LAUNCH();
+  if (losses) {
+    if (x->data) {
+      const int nbk = 1024;
+      dec_emission_nll<<<nbk, 256, 0, s>>>(w.MU, w.LV, Fp, x->data, F, L, w.part);
+      ABCD_CHECK_LAUNCH();
+      sum_partials<<<1, 256, 0, s>>>(w.part, nbk, losses);
+      ABCD_CHECK_LAUNCH();
+    }
+    if (gt_offset) ABCD_TRY((hipError_t)reduce_sum(s, w.bce, L, w.part + 1024, losses + 1, nullptr));
+  }
+  if (flatten_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.OUT, Fp, flatten_out, F, L); ABCD_CHECK_LAUNCH(); }
+  if (mu_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.MU, Fp, mu_out, F, L); ABCD_CHECK_LAUNCH(); }
+  if (lv_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.LV, Fp, lv_out, F, L); ABCD_CHECK_LAUNCH(); }
+  if (offset_logits) ABCD_TRY(hipMemcpyAsync(offset_logits, w.offlog, (size_t)L * 4, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+extern "C" int abcd_decoder_backward(const abcd_decoder_cfg* c, const abcd_decoder_params* p, const abcd_packed* x,
+                                     const float* features, const int64_t* speakers, const float* gt_offset,
+                                     const float* d_em, const float* d_off, float* d_features,
+                                     const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(dec_check(c) == 0 && p && x && x->data && features && g && ws && d_em && d_off && gt_offset);
+  ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
+  hipStream_t s = (hipStream_t)stream;
+  Arena A(ws, ws_bytes);
+  DecWS w = carve_decoder(A, c, x->T, x->L, x->B);
+  ABCD_REQUIRE(A.ok);
+  const int H = c->hidden_size, Hm = c->mlp_hidden, F = c->output_size, Fp = rup16(F);
+  const int G = c->rnn_type == ABCD_LSTM ? 4 : 3, GH = G * H;
+  const int Htot = G == 4 ? 2 * H : H;
+  const int D = c->feature_size, S = c->num_speakers > 0 ? c->speaker_dim : 0, DS = D + S;
+  const int T = x->T, L = x->L, B = x->B;
+  const int64_t* bs = x->batch_sizes;
+  const std::vector<int> off = step_offsets(bs, T);
+  const abcd_rnn_w& cw = p->cell;
+  float* sc = w.scratch;
+  const size_t scf = w.scratch_floats;
+  // ---- derived transposed weights for the backward GEMMs ----
+  ABCD_TRY((hipError_t)pack2d(s, cw.w_ih, F, F, GH, true, w.WihTp, GH, Fp, GH));  // rows >= F zero
+  ABCD_TRY((hipError_t)pack2d(s, cw.w_hh, H, H, GH, true, w.WhhT, GH, H, GH));
+  ABCD_TRY((hipError_t)pack2d(s, p->mu.w2, Hm, Hm, F, true, w.W2mT, Fp, Hm, Fp));
+  ABCD_TRY((hipError_t)pack2d(s, p->lv.w2, Hm, Hm, F, true, w.W2lT, Fp, Hm, Fp));
+  ABCD_TRY((hipError_t)pack2d(s, p->mu.w1, H, H, Hm, true, w.W1catT, 2 * Hm, H, Hm));
+  ABCD_TRY((hipError_t)pack2d(s, p->lv.w1, H, H, Hm, true, w.W1catT + Hm, 2 * Hm, H, Hm));
+  ABCD_TRY((hipError_t)pack2d(s, p->offset.w1, H, H, Hm, true, w.W1oT, Hm, H, Hm));
+  ABCD_TRY((hipError_t)pack2d(s, p->f2h_w, DS, DS, Htot, true, w.Wf2hT, Htot, DS, Htot));
+  // ---- offset head backward (batched over all frames) ----
+  dec_offset_bwd<<<launch_grid((long)L * Hm), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, w.dlog_raw, d_off, w.dZo,
+                                                           w.dlog_s);
+  ABCD_CHECK_LAUNCH();
+  ABCD_TRY((hipError_t)gemm(s, L, H, Hm, opKC(w.dZo, Hm, L), opKC(w.W1oT, Hm, H), w.DHO, H, 1.f, 0.f, nullptr,
+                            ACT_NONE, sc, scf));
+  // ---- BPTT ----
+  const int TN = bwd_tn(H);
+  for (int t = T - 1; t >= 0; --t) {
+    const int b_t = (int)bs[t];
+    const int nb = t + 1 < T ? (int)bs[t + 1] : 0;
+    EmitBwdX e{};
+    e.Ag = w.dGX + (size_t)off[t + 1] * GH; e.ldg = GH; e.succ_valid = c->feedback ? nb : 0; e.nch = GH / 16;
+    e.WihT = w.WihTp; e.MU = w.MU; e.LV = w.LV; e.OUT = w.OUT; e.Y = x->data; e.s_em = d_em;
+    e.dMU = w.dMU; e.dLV = w.dLV; e.F = F; e.Fp = Fp; e.off = off[t]; e.bs = b_t;
+    dec_emit_bwd_x<<<cdiv(b_t, 16) * (Fp / 16), 256, 0, s>>>(e);
+    ABCD_CHECK_LAUNCH();
+    MlpBwd m{};
+    m.dMU = w.dMU; m.dLV = w.dLV; m.Fp = Fp; m.nch = Fp / 16; m.W2mT = w.W2mT; m.W2lT = w.W2lT;
+    m.Aact = w.Aact; m.dZ = w.dZ; m.Hm = Hm; m.off = off[t]; m.bs = b_t;
+    const int nr = (Hm / 16) % 4 == 0 ? 4 : ((Hm / 16) % 2 == 0 ? 2 : 1);
+    const int mgrid = cdiv(b_t, 16) * (Hm / (16 * nr));
+    if (nr == 4) dec_mlp_bwd<4><<<mgrid, 256, 0, s>>>(m);
+    else if (nr == 2) dec_mlp_bwd<2><<<mgrid, 256, 0, s>>>(m);
+    else dec_mlp_bwd<1><<<mgrid, 256, 0, s>>>(m);
+    ABCD_CHECK_LAUNCH();
+    BwdArgs a{};
+    a.H = H;
+    a.nd = 1;
+    BwdDir& bd = a.d[0];
+    bd.Ag = w.dGH + (size_t)off[t + 1] * GH; bd.succ_valid = nb; bd.WhhT = w.WhhT;
+    bd.Az = w.dZ + (size_t)off[t] * 2 * Hm; bd.zrows = b_t; bd.W1T = w.W1catT; bd.ldz = 2 * Hm; bd.nchz = 2 * Hm / 16;
+    bd.DHX = w.DHO; bd.lddhx = H;
+    bd.dlast = nullptr; bd.ldl = 0; bd.hcol = 0; bd.ccol = -1;
+    bd.Gst = w.Gst; bd.Cst = w.Cst; bd.Cprev = w.Cprev; bd.Hprev = w.Hprev;
+    bd.dGX = w.dGX; bd.dGH = w.dGH; bd.DC = w.DC;
+    bd.DCpred = t > 0 ? w.DC : w.DC0; bd.pred_off = t > 0 ? off[t - 1] : 0;
+    bd.off = off[t]; bd.bs = b_t; bd.prev_valid = b_t; bd.next_bs = nb;
+    bd.tiles = cdiv(b_t, 16) * (H / TN);
+    if (G == 4) ABCD_TRY((hipError_t)launch_bwd_step<4>(s, a, bd.tiles, H));
+    else ABCD_TRY((hipError_t)launch_bwd_step<3>(s, a, bd.tiles, H));
+  }
+  // ---- initial state gradient -> feature2hidden -> features / speaker embedding ----
+  ABCD_TRY((hipError_t)gemm(s, B, H, GH, opKC(w.dGH, GH, B), opKC(w.WhhT, GH, H), w.dH0, H, 1.f, 0.f, nullptr,
+                            ACT_NONE, sc, scf));
+  dec_hidden_init_bwd<<<launch_grid((long)B * H), 256, 0, s>>>(w.dH0, w.DC0, B, H, G == 4, w.dhid);
+  ABCD_CHECK_LAUNCH();
+  const float* FS = S > 0 ? w.FS : features;
+  ABCD_TRY((hipError_t)gemm(s, B, DS, Htot, opKC(w.dhid, Htot, B), opKC(w.Wf2hT, Htot, DS), w.dFS, DS, 1.f, 0.f,
+                            nullptr, ACT_NONE, sc, scf));
+  dec_feats_bwd<<<launch_grid((long)B * std::max(D, 1)), 256, 0, s>>>(w.dFS, D, S, B, speakers, c->num_speakers,
+                                                                     d_features, S > 0 ? g->embed_speaker : nullptr);
+  ABCD_CHECK_LAUNCH();
+  if (g->f2h_w)
+    ABCD_TRY((hipError_t)gemm(s, Htot, DS, B, opKM(w.dhid, Htot, Htot), opKM(FS, DS, DS), g->f2h_w, DS, 1.f, 0.f,
+                              nullptr, ACT_NONE, sc, scf));
+  if (g->f2h_b) ABCD_TRY((hipError_t)colsum(s, w.dhid, Htot, B, Htot, nullptr, g->f2h_b, 0.f, sc, scf));
+  // ---- weight gradients, K = L frames ----
+  const abcd_rnn_g& cg = g->cell;
+  if (cg.w_ih) {
+    if (c->feedback)
+      ABCD_TRY((hipError_t)gemm(s, GH, F, L, opKM(w.dGX, GH, GH), opKM(w.Xin, Fp, F), cg.w_ih, F, 1.f, 0.f, nullptr,
+                                ACT_NONE, sc, scf));
+    else
+      ABCD_TRY(hipMemsetAsync(cg.w_ih, 0, (size_t)GH * F * 4, s));
+  }
+  if (cg.w_hh)
+    ABCD_TRY((hipError_t)gemm(s, GH, H, L, opKM(w.dGH, GH, GH), opKM(w.Hprev, H, H), cg.w_hh, H, 1.f, 0.f, nullptr,
+                              ACT_NONE, sc, scf));
+  if (cg.b_ih) ABCD_TRY((hipError_t)colsum(s, w.dGX, GH, L, GH, nullptr, cg.b_ih, 0.f, sc, scf));
+  if (cg.b_hh) ABCD_TRY((hipError_t)colsum(s, w.dGH, GH, L, GH, nullptr, cg.b_hh, 0.f, sc, scf));
+  const abcd_mlp_g* em[2] = {&g->mu, &g->lv};
+  const float* dout[2] = {w.dMU, w.dLV};
+  for (int k = 0; k < 2; ++k) {
+    const abcd_mlp_g& mg = *em[k];
+    if (mg.w2)
+      ABCD_TRY((hipError_t)gemm(s, F, Hm, L, opKM(dout[k], Fp, F), opKM(w.Aact + k * Hm, 2 * Hm, Hm), mg.w2, Hm, 1.f,
+                                0.f, nullptr, ACT_NONE, sc, scf));
+    if (mg.b2) ABCD_TRY((hipError_t)colsum(s, dout[k], Fp, L, F, nullptr, mg.b2, 0.f, sc, scf));
+    if (mg.w1)
+      ABCD_TRY((hipError_t)gemm(s, Hm, H, L, opKM(w.dZ + k * Hm, 2 * Hm, Hm), opKM(w.Hs, H, H), mg.w1, H, 1.f, 0.f,
+                                nullptr, ACT_NONE, sc, scf));
+    if (mg.b1) ABCD_TRY((hipError_t)colsum(s, w.dZ + k * Hm, 2 * Hm, L, Hm, nullptr, mg.b1, 0.f, sc, scf));
+  }
+  const abcd_mlp_g& og = g->offset;
+  if (og.w1)
+    ABCD_TRY((hipError_t)gemm(s, Hm, H, L, opKM(w.dZo, Hm, Hm), opKM(w.Hs, H, H), og.w1, H, 1.f, 0.f, nullptr,
+                              ACT_NONE, sc, scf));
+  if (og.b1) ABCD_TRY((hipError_t)colsum(s, w.dZo, Hm, L, Hm, nullptr, og.b1, 0.f, sc, scf));
+  if (og.w2) ABCD_TRY((hipError_t)colsum(s, w.Zo, Hm, L, Hm, w.dlog_s, og.w2, 0.f, sc, scf));
+  if (og.b2) ABCD_TRY((hipError_t)colsum(s, w.dlog_s, 1, L, 1, nullptr, og.b2, 0.f, sc, scf));
+  return 0;
+}

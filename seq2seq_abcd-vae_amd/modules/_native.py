@@ -1,0 +1,167 @@
+"""ctypes binding of the C ABI in ``include/abcd_hip.h`` (``libabcd_hip.so``).
+
+The library is built in-tree (``seq2seq_abcd-vae_amd/libabcd_hip.so``) by
+``__graft_entry__.build()`` / ``make -C seq2seq_abcd-vae_amd/csrc``.  There is
+no fallback: if the library (or a GPU) is missing, every compute call raises.
+
+torch is imported first on purpose: libabcd_hip.so needs libamdhip64.so.7 and
+must bind to the HIP runtime torch already loaded, so that torch's streams and
+device pointers are valid for our kernels.
+"""
+import ctypes
+import os
+
+import torch
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("ABCD_HIP_LIB", os.path.join(PKG_DIR, "libabcd_hip.so"))
+
+c_int, c_long, c_float, c_double, c_void_p, c_size_t, c_uint64 = (
+    ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t,
+    ctypes.c_uint64)
+
+ABCD_EINVAL = 1000
+ABCD_MAX_LAYERS = 4
+LSTM, GRU = 0, 1
+SAMPLE_SOFTMAX, SAMPLE_GUMBEL = 0, 1
+
+
+class RnnW(ctypes.Structure):
+    _fields_ = [("w_ih", c_void_p), ("w_hh", c_void_p), ("b_ih", c_void_p), ("b_hh", c_void_p)]
+
+
+class MlpW(ctypes.Structure):
+    _fields_ = [("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p), ("b2", c_void_p)]
+
+
+class Packed(ctypes.Structure):
+    _fields_ = [("data", c_void_p), ("batch_sizes", c_void_p), ("T", c_int), ("L", c_int), ("B", c_int),
+                ("F", c_int)]
+
+
+class EncoderCfg(ctypes.Structure):
+    _fields_ = [("input_size", c_int), ("hidden_size", c_int), ("rnn_type", c_int), ("layers", c_int),
+                ("bidirectional", c_int)]
+
+
+class EncoderParams(ctypes.Structure):
+    _fields_ = [("w", (RnnW * 2) * ABCD_MAX_LAYERS)]
+
+
+class SamplerCfg(ctypes.Structure):
+    _fields_ = [("input_size", c_int), ("mlp_hidden", c_int), ("num_categories", c_int),
+                ("feature_dim", c_int), ("plain", c_int)]
+
+
+class SamplerParams(ctypes.Structure):
+    _fields_ = [("mlp", MlpW * 2), ("codebook", c_void_p), ("posterior_shape_logits", c_void_p),
+                ("prior_concentration", c_float)]
+
+
+class SamplerGrads(ctypes.Structure):
+    _fields_ = [("mlp", MlpW * 2), ("codebook", c_void_p), ("posterior_shape_logits", c_void_p)]
+
+
+class DecoderCfg(ctypes.Structure):
+    _fields_ = [("output_size", c_int), ("hidden_size", c_int), ("mlp_hidden", c_int), ("feature_size", c_int),
+                ("rnn_type", c_int), ("feedback", c_int), ("num_speakers", c_int), ("speaker_dim", c_int)]
+
+
+class DecoderParams(ctypes.Structure):
+    _fields_ = [("embed_speaker", c_void_p), ("f2h_w", c_void_p), ("f2h_b", c_void_p), ("offset", MlpW),
+                ("mu", MlpW), ("lv", MlpW), ("cell", RnnW)]
+
+
+EncoderGrads = EncoderParams
+DecoderGrads = DecoderParams
+
+_P = ctypes.POINTER
+_SIGS = {
+    "abcd_version": (ctypes.c_char_p, []),
+    "abcd_encoder_out_size": (c_int, [_P(EncoderCfg)]),
+    "abcd_encoder_workspace_bytes": (c_size_t, [_P(EncoderCfg), c_int, c_int, c_int]),
+    "abcd_encoder_forward": (c_int, [_P(EncoderCfg), _P(EncoderParams), _P(Packed), c_void_p, c_void_p, c_size_t,
+                                     c_void_p]),
+    "abcd_encoder_backward": (c_int, [_P(EncoderCfg), _P(EncoderParams), _P(Packed), c_void_p, _P(EncoderGrads),
+                                      c_void_p, c_size_t, c_void_p]),
+    "abcd_sampler_workspace_bytes": (c_size_t, [_P(SamplerCfg), c_int]),
+    "abcd_sampler_forward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_void_p, c_void_p,
+                                     c_size_t, c_void_p]),
+    "abcd_sampler_sample": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float, c_void_p,
+                                    c_uint64, c_uint64, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "abcd_sampler_kl": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_double, c_void_p, c_void_p,
+                                c_size_t, c_void_p]),
+    "abcd_sampler_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float, c_double,
+                                      c_void_p, c_void_p, c_void_p, _P(SamplerGrads), c_void_p, c_size_t, c_void_p]),
+    "abcd_sampler_sample_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_int, c_float, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "abcd_sampler_kl_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_double, c_void_p, c_int,
+                                         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "abcd_sampler_forward_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_void_p,
+                                              c_void_p, _P(SamplerGrads), c_int, c_void_p, c_size_t, c_void_p]),
+    "abcd_perplexities": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "abcd_decoder_workspace_bytes": (c_size_t, [_P(DecoderCfg), c_int, c_int, c_int]),
+    "abcd_decoder_forward": (c_int, [_P(DecoderCfg), _P(DecoderParams), _P(Packed), c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_size_t, c_void_p]),
+    "abcd_decoder_backward": (c_int, [_P(DecoderCfg), _P(DecoderParams), _P(Packed), c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, _P(DecoderGrads), c_void_p, c_size_t, c_void_p]),
+    "abcd_optim_workspace_bytes": (c_size_t, [c_long]),
+    "abcd_grad_norm": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "abcd_clip_sgd": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_float, c_float, c_float, c_int, c_void_p,
+                              c_void_p, c_size_t, c_void_p]),
+    "abcd_total_loss": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "abcd_gemm_nt": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p,
+                             c_void_p, c_size_t, c_void_p]),
+    "abcd_linear": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_void_p,
+                            c_long, c_void_p, c_size_t, c_void_p]),
+    "abcd_fill_normal": (c_int, [c_void_p, c_long, c_uint64, c_uint64, c_void_p]),
+}
+EXPORTED = sorted(_SIGS)
+
+_lib = None
+
+
+def lib():
+    """The loaded libabcd_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.isfile(LIB_PATH):
+            raise RuntimeError(f"libabcd_hip.so not found at {LIB_PATH}: run __graft_entry__.build() "
+                               "(make -C seq2seq_abcd-vae_amd/csrc). There is no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def check(rc, what):
+    if rc != 0:
+        if rc == ABCD_EINVAL:
+            raise HipError(f"{what}: invalid or unsupported arguments (ABCD_EINVAL)")
+        raise HipError(f"{what}: HIP error {rc}")
+
+
+def require_gpu(t):
+    if not (torch.is_tensor(t) and t.is_cuda):
+        raise RuntimeError("the ABCD-VAE HIP path runs on an MI355X GPU only; got a tensor on "
+                           f"{getattr(t, 'device', None)} (no CPU fallback)")
+
+
+def ptr(t):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def stream():
+    return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

@@ -1,0 +1,224 @@
+"""Fused training step: the body of ``Learner.train`` (ABCD-VAE/learning.py:147-163)
+run as a fixed sequence of C-ABI calls, with no autograd graph.
+
+    zero_grad -> encoder -> sampler.forward -> sample -> kl -> decoder
+      -> loss = (em + off + kl) / batch_sizes[0] -> backward -> clip_grad_norm_ -> SGD
+
+All parameters live in ONE flat fp32 device buffer (the modules' Parameters are
+views into it, so ``state_dict``/checkpoints are unchanged) and all gradients
+in a second one: the backward kernels write gradients in place, the global
+clip + SGD is one pass over the flat buffers, and data parallelism is a single
+all-reduce of the flat gradient buffer (``parallel.py``).  The step never
+synchronises with the host; loss terms and diagnostics stay on the device in
+``FusedStep.scalars`` until the caller reads them.
+"""
+import itertools
+
+import torch
+
+from . import _native as N
+from . import noise as _noise
+from .model import ABCDSampler
+
+# layout of the device scalar vector returned by FusedStep.step
+EM, OFF, KL, LOSS, NORM, PPL_CLUSTER, PPL_BATCH, PPL_SHAPE = range(8)
+N_SCALARS = 8
+
+
+class FlatParams:
+    """Re-home a list of Parameters into one flat buffer (params) + one flat
+    buffer (grads); each Parameter's ``.data``/``.grad`` become views."""
+
+    def __init__(self, params, device):
+        self.params = list(params)
+        sizes = [p.numel() for p in self.params]
+        self.offsets = list(itertools.accumulate([0] + sizes))[:-1]
+        self.n = sum(sizes)
+        self.flat = torch.empty(self.n, device=device)
+        self.grad = torch.zeros(self.n, device=device)
+        self.index = {}
+        for p, o, s in zip(self.params, self.offsets, sizes):
+            self.flat[o:o + s].copy_(p.detach().reshape(-1).to(device))
+            p.data = self.flat[o:o + s].view_as(p)
+            p.grad = self.grad[o:o + s].view_as(p)
+            self.index[id(p)] = (o, s)
+
+    def grad_of(self, p):
+        o, s = self.index[id(p)]
+        return self.grad[o:o + s].view_as(p)
+
+    def rebind(self):
+        """Re-attach .data/.grad views (e.g. after something replaced them)."""
+        for p, o in zip(self.params, self.offsets):
+            s = p.numel()
+            if p.data.data_ptr() != self.flat[o:o + s].data_ptr():
+                self.flat[o:o + s].copy_(p.data.reshape(-1))
+                p.data = self.flat[o:o + s].view_as(p)
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + s].data_ptr():
+                p.grad = self.grad[o:o + s].view_as(p)
+
+
+class FusedStep:
+    def __init__(self, encoder, sampler, decoder, device=None):
+        self.encoder, self.sampler, self.decoder = encoder, sampler, decoder
+        self.plain = not isinstance(sampler, ABCDSampler)
+        device = torch.device(device) if device is not None else next(encoder.parameters()).device
+        self.device = device
+        params = itertools.chain(encoder.parameters(), sampler.parameters(), decoder.parameters())
+        self.flat = FlatParams(params, device)
+        self.momentum_buf = None
+        self.momentum_init = True
+        self._ws = {}
+        self.optim_ws = N.workspace(N.lib().abcd_optim_workspace_bytes(self.flat.n), device)
+        self.scalars = torch.zeros(N_SCALARS, device=device)
+        self._inv = {}
+        self._build_structs()
+        self.allreduce = None  # set by parallel.DataParallel
+
+    # ------------------------------------------------------------------ setup
+    def _build_structs(self):
+        enc, samp, dec, fp = self.encoder, self.sampler, self.decoder, self.flat
+        self.enc_cfg = enc._cfg()
+        self.enc_p = enc._params()
+        dirs = 2 if enc.rnn.bidirectional else 1
+        eg = {(l, d): [fp.grad_of(t) for t in enc.rnn.layer_weights(l, d)]
+              for l in range(enc.rnn.num_layers) for d in range(dirs)}
+        self.enc_g = enc._params(eg)
+        self.samp_cfg = samp._scfg()
+        self.samp_p = samp._sparams()
+        views = {}
+        for k, m in enumerate(samp._mlps()):
+            for f, t in zip(("w1", "b1", "w2", "b2"), m.weights()):
+                views[f"mlp{k}.{f}"] = fp.grad_of(t)
+        if not self.plain:
+            views["codebook"] = fp.grad_of(samp.codebook)
+            views["posterior_shape_logits"] = fp.grad_of(samp.posterior_shape_logits)
+        self.samp_g = samp._sgrads(views)
+        self.dec_p = dec._dparams()
+        self.dec_g = dec._dparams([fp.grad_of(t) for t in dec._param_list()])
+        self.E = enc.hidden_size_total
+        self.Dfeat = samp._feat_dim()
+
+    def refresh(self):
+        """Call after load_state_dict / .to(): re-bind views and pointer tables."""
+        self.flat.rebind()
+        self._build_structs()
+
+    def _workspace(self, name, nbytes):
+        ws = self._ws.get(name)
+        if ws is None or ws.numel() < nbytes:
+            ws = N.workspace(int(nbytes * 1.1) + 4096, self.device)
+            self._ws[name] = ws
+        return ws
+
+    def _inv_b(self, B):
+        t = self._inv.get(B)
+        if t is None:
+            t = torch.full((), 1.0 / B, device=self.device)
+            self._inv[B] = t
+        return t
+
+    # --------------------------------------------------------------- the step
+    def forward_backward(self, data, batch_sizes, is_offset, speakers, entire_data_size, is_pretraining=False,
+                         train=True):
+        """Forward + backward of learning.py:149-158; gradients land in flat.grad."""
+        L_ = N.lib()
+        st = N.stream()
+        data = data.contiguous()
+        N.require_gpu(data)
+        pk, bs_keep = _packed(data, batch_sizes, self.enc_cfg.input_size)
+        T, L, B = pk.T, pk.L, pk.B
+        dev = self.device
+        sc = self.scalars
+        ws_e = self._workspace("enc", L_.abcd_encoder_workspace_bytes(self.enc_cfg, T, L, B))
+        ws_s = self._workspace("samp", L_.abcd_sampler_workspace_bytes(self.samp_cfg, B))
+        dcfg = self.decoder._dcfg(None if train else 1)
+        ws_d = self._workspace("dec", L_.abcd_decoder_workspace_bytes(dcfg, T, L, B))
+        h = torch.empty(B, self.E, device=dev)
+        N.check(L_.abcd_encoder_forward(self.enc_cfg, self.enc_p, pk, N.ptr(h), N.ptr(ws_e), ws_e.numel(), st),
+                "encoder forward")
+        W = self.sampler._logit_width()
+        logits = torch.empty(B, W, device=dev)
+        N.check(L_.abcd_sampler_forward(self.samp_cfg, self.samp_p, N.ptr(h), B, N.ptr(logits), N.ptr(ws_s),
+                                        ws_s.numel(), st), "sampler forward")
+        feats = torch.empty(B, self.Dfeat, device=dev)
+        if self.plain:
+            mode, tau = 0, 1.0
+            nt, seed, off = _noise.normal(B, self.Dfeat, dev)
+        elif is_pretraining:
+            mode, tau, nt, seed, off = N.SAMPLE_SOFTMAX, 1.0, None, 0, 0
+        else:
+            mode, tau = N.SAMPLE_GUMBEL, float(self.sampler.temperature)
+            nt, seed, off = _noise.gumbel(B, W, dev)
+        N.check(L_.abcd_sampler_sample(self.samp_cfg, self.samp_p, N.ptr(logits), B, mode, tau, N.ptr(nt), seed, off,
+                                       N.ptr(feats), N.ptr(ws_s), ws_s.numel(), st), "sampler sample")
+        N.check(L_.abcd_sampler_kl(self.samp_cfg, self.samp_p, N.ptr(logits), B, float(entire_data_size),
+                                   N.ptr(sc[KL:KL + 1]), N.ptr(ws_s), ws_s.numel(), st), "sampler kl")
+        F = self.decoder.rnn_cell.cell.input_size
+        eps, eseed, eoff = _noise.decoder_eps(bs_keep, F, dev)
+        spk = None
+        if self.decoder.embed_speaker is not None:
+            spk = speakers.to(dev, torch.int64).contiguous()
+        gt_off = is_offset.contiguous()
+        N.check(L_.abcd_decoder_forward(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off), N.ptr(eps),
+                                        eseed, eoff, None, None, None, None, N.ptr(sc[EM:EM + 2]), N.ptr(ws_d),
+                                        ws_d.numel(), st), "decoder forward")
+        N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), B, N.ptr(sc[LOSS:LOSS + 1]), st),
+                "total loss")
+        if not train:
+            return sc, logits
+        inv = self._inv_b(B)
+        d_feats = torch.empty(B, self.Dfeat, device=dev)
+        N.check(L_.abcd_decoder_backward(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off), N.ptr(inv),
+                                         N.ptr(inv), N.ptr(d_feats), self.dec_g, N.ptr(ws_d), ws_d.numel(), st),
+                "decoder backward")
+        d_h = torch.empty(B, self.E, device=dev)
+        N.check(L_.abcd_sampler_backward(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, float(entire_data_size),
+                                         N.ptr(d_feats), N.ptr(inv), N.ptr(d_h), self.samp_g, N.ptr(ws_s),
+                                         ws_s.numel(), st), "sampler backward")
+        N.check(L_.abcd_encoder_backward(self.enc_cfg, self.enc_p, pk, N.ptr(d_h), self.enc_g, N.ptr(ws_e),
+                                         ws_e.numel(), st), "encoder backward")
+        return sc, logits
+
+    def optimizer_step(self, lr, momentum=0.0, clip=1.0):
+        """clip_grad_norm_(all params, clip) + SGD(lr, momentum) on the flat buffers."""
+        if self.allreduce is not None:
+            self.allreduce(self.flat.grad)
+        buf = None
+        if momentum != 0.0:
+            if self.momentum_buf is None:
+                self.momentum_buf = torch.zeros_like(self.flat.flat)
+                self.momentum_init = True
+            buf = self.momentum_buf
+        N.check(N.lib().abcd_clip_sgd(N.ptr(self.flat.flat), N.ptr(self.flat.grad), N.ptr(buf), self.flat.n,
+                                      float(clip), float(lr), float(momentum), int(self.momentum_init),
+                                      N.ptr(self.scalars[NORM:NORM + 1]), N.ptr(self.optim_ws),
+                                      self.optim_ws.numel(), N.stream()), "clip+sgd")
+        if buf is not None:
+            self.momentum_init = False
+
+    def step(self, data, batch_sizes, is_offset, speakers, entire_data_size, is_pretraining=False, lr=1.0,
+             momentum=0.0, clip=1.0):
+        sc, logits = self.forward_backward(data, batch_sizes, is_offset, speakers, entire_data_size,
+                                           is_pretraining)
+        self.optimizer_step(lr, momentum, clip)
+        if not self.plain:  # learning.py:171-178 reads posterior_shape_logits AFTER the SGD step
+            N.check(N.lib().abcd_perplexities(N.ptr(logits), logits.shape[0], logits.shape[1],
+                                              N.ptr(self.sampler.posterior_shape_logits),
+                                              N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 3]), N.stream()), "perplexities")
+        return sc
+
+
+def _packed(data, batch_sizes, F):
+    bs = batch_sizes
+    if bs.dtype != torch.int64 or bs.device.type != "cpu":
+        bs = bs.to("cpu", torch.int64)
+    bs = bs.contiguous()
+    st = N.Packed()
+    st.data = data.data_ptr()
+    st.batch_sizes = bs.data_ptr()
+    st.T = int(bs.numel())
+    st.L = int(data.shape[0])
+    st.B = int(bs[0])
+    st.F = int(F)
+    return st, bs

@@ -1,0 +1,834 @@
+# coding: utf-8
+"""nn.Module surface of the reference model (ABCD-VAE/modules/model.py), backed
+by the MI355X kernels of libabcd_hip.so.
+
+Class names, constructor signatures, ``forward``/``sample``/``kl_divergence``
+signatures, attribute names, ``state_dict`` keys and ``pack_init_parameters``
+dicts follow the reference (file:line cited per class) so that ``learning.py``,
+``encode*.py`` and reference checkpoints work unchanged.  Parameters are
+created with the same torch init calls in the same order as the reference, so
+``torch.manual_seed(seed)`` gives bit-identical initial weights.
+
+Every forward/backward runs on the GPU through the C ABI (``_native``); there is
+no CPU fallback -- a CPU tensor raises.
+"""
+import math
+
+import torch
+
+from . import _native as N
+from . import noise as _noise
+
+
+# ----------------------------------------------------------------------------
+# reference helper functions (model.py:6-37), torch-level, used only on
+# tensors the caller already holds (e.g. Sampler.log_pdf in user code)
+# ----------------------------------------------------------------------------
+def choose_distribution(distribution_name):
+    distributions = {"isotropic_gaussian": (sample_from_isotropic_gaussian, log_pdf_isotropic_gaussian,
+                                            kl_isotropic_to_standard_gaussian, 2)}
+    return distributions[distribution_name]
+
+
+def sample_from_isotropic_gaussian(mean, log_variance):
+    return mean + (0.5 * log_variance).exp() * torch.randn_like(mean)
+
+
+def kl_isotropic_to_standard_gaussian(mean, log_variance):
+    return -0.5 * (1 + log_variance - mean.pow(2) - log_variance.exp()).sum()
+
+
+def log_pdf_isotropic_gaussian(value, mean, log_variance):
+    d = value - mean
+    return -0.5 * (math.log(2 * math.pi) + log_variance + d * (-log_variance).exp() * d).sum()
+
+
+def _packed_struct(data, batch_sizes, F):
+    bs = batch_sizes
+    if bs.dtype != torch.int64 or bs.device.type != "cpu":
+        bs = bs.to("cpu", torch.int64)
+    bs = bs.contiguous()
+    st = N.Packed()
+    st.data = data.data_ptr() if data is not None else None
+    st.batch_sizes = bs.data_ptr()
+    st.T = int(bs.numel())
+    st.L = int(data.shape[0]) if data is not None else int(bs.sum())
+    st.B = int(bs[0])
+    st.F = int(F)
+    return st, bs  # keep bs alive while the struct is used
+
+
+def _f32c(t):
+    if t.dtype != torch.float32:
+        raise TypeError(f"fp32 tensors only (got {t.dtype})")
+    return t.contiguous()
+
+
+# ----------------------------------------------------------------------------
+# parameter containers with the reference's names / init
+# ----------------------------------------------------------------------------
+class PackedRNN(torch.nn.Module):
+    """Parameter holder standing in for ``torch.nn.LSTM/GRU`` inside the
+    encoder (``model.py:53``): same attribute names (mode, input_size,
+    hidden_size, num_layers, dropout, bidirectional, batch_first), same
+    parameter names/order and the same ``reset_parameters`` (every weight
+    U(-1/sqrt(H), 1/sqrt(H)) in ``_flat_weights`` order)."""
+
+    def __init__(self, mode, input_size, hidden_size, num_layers=1, dropout=0.0, bidirectional=False,
+                 batch_first=True):
+        super().__init__()
+        if mode not in ("LSTM", "GRU"):
+            raise NotImplementedError(f"rnn_type {mode!r}: only LSTM and GRU run on the HIP path "
+                                      "(ESN is broken in the reference on torch>=1.9: torch.eig)")
+        self.mode = mode
+        self.input_size = input_size
+        self.hidden_size = hidden_size
+        self.num_layers = num_layers
+        self.dropout = float(dropout)
+        self.bidirectional = bidirectional
+        self.batch_first = batch_first
+        G = 4 if mode == "LSTM" else 3
+        dirs = 2 if bidirectional else 1
+        for l in range(num_layers):
+            In = input_size if l == 0 else hidden_size * dirs
+            for d in range(dirs):
+                sfx = "_reverse" if d == 1 else ""
+                self.register_parameter(f"weight_ih_l{l}{sfx}", torch.nn.Parameter(torch.empty(G * hidden_size, In)))
+                self.register_parameter(f"weight_hh_l{l}{sfx}",
+                                        torch.nn.Parameter(torch.empty(G * hidden_size, hidden_size)))
+                self.register_parameter(f"bias_ih_l{l}{sfx}", torch.nn.Parameter(torch.empty(G * hidden_size)))
+                self.register_parameter(f"bias_hh_l{l}{sfx}", torch.nn.Parameter(torch.empty(G * hidden_size)))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        stdv = 1.0 / math.sqrt(self.hidden_size)
+        for w in self.parameters():
+            torch.nn.init.uniform_(w, -stdv, stdv)
+
+    def layer_weights(self, l, d):
+        sfx = "_reverse" if d == 1 else ""
+        return [getattr(self, f"{n}_l{l}{sfx}") for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+
+
+class MLP(torch.nn.Module):
+    """``model.py:316-334``: Linear -> Tanh -> Linear (``whole_network``)."""
+
+    def __init__(self, input_size, hidden_size, output_size):
+        super().__init__()
+        self.input_size = input_size
+        self.hidden_size = hidden_size
+        self.output_size = output_size
+        self.whole_network = torch.nn.Sequential(torch.nn.Linear(input_size, hidden_size), torch.nn.Tanh(),
+                                                 torch.nn.Linear(hidden_size, output_size))
+
+    def weights(self):
+        return (self.whole_network[0].weight, self.whole_network[0].bias, self.whole_network[2].weight,
+                self.whole_network[2].bias)
+
+    def forward(self, batched_input):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("standalone MLP forward is inference-only on the HIP path; its training "
+                                      "backward is fused into the sampler/decoder kernels")
+        x = _f32c(batched_input)
+        N.require_gpu(x)
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        M = x2.shape[0]
+        w1, b1, w2, b2 = [t.detach() for t in self.weights()]
+        hid = torch.empty(M, self.hidden_size, device=x.device)
+        out = torch.empty(M, self.output_size, device=x.device)
+        Kp = (max(self.input_size, self.hidden_size) + 15) // 16 * 16
+        ws = N.workspace((M + max(self.hidden_size, self.output_size)) * Kp * 4 + (1 << 22), x.device)
+        L = N.lib()
+        N.check(L.abcd_linear(M, self.hidden_size, self.input_size, N.ptr(x2), x2.shape[1], N.ptr(w1), w1.shape[1],
+                              N.ptr(b1), 1, N.ptr(hid), self.hidden_size, N.ptr(ws), ws.numel(), N.stream()),
+                "MLP layer 1")
+        N.check(L.abcd_linear(M, self.output_size, self.hidden_size, N.ptr(hid), self.hidden_size, N.ptr(w2),
+                              w2.shape[1], N.ptr(b2), 0, N.ptr(out), self.output_size, N.ptr(ws), ws.numel(),
+                              N.stream()), "MLP layer 2")
+        return out.reshape(*shp[:-1], self.output_size)
+
+
+class MLP_To_k_Vecs(torch.nn.Module):
+    """``model.py:303-314``"""
+
+    def __init__(self, input_size, hidden_size, output_size, k):
+        super().__init__()
+        self.input_size = input_size
+        self.hidden_size = hidden_size
+        self.output_size = output_size
+        self.k = k
+        self.mlps = torch.nn.ModuleList([MLP(input_size, hidden_size, output_size) for _ in range(k)])
+
+    def forward(self, batched_input):
+        return [mlp(batched_input) for mlp in self.mlps]
+
+
+class RNN_Cell(torch.nn.Module):
+    """``model.py:287-300``: input dropout + LSTMCell/GRUCell (parameter holder)."""
+
+    def __init__(self, input_size, hidden_size, model_type="LSTM", input_dropout=0.0, esn_leak=1.0):
+        super().__init__()
+        if model_type not in ("LSTM", "GRU"):
+            raise NotImplementedError(f"decoder rnn_type {model_type!r}: only LSTM and GRU are supported")
+        self.drop = torch.nn.Dropout(input_dropout)
+        self.mode = model_type
+        self.cell = getattr(torch.nn, model_type + "Cell")(input_size, hidden_size)
+
+    def forward(self, batched_input, init_hidden=None):
+        raise NotImplementedError("RNN_Cell is stepped inside the fused decoder kernels "
+                                  "(RNN_Variational_Decoder.forward)")
+
+
+# ----------------------------------------------------------------------------
+# Encoder (model.py:40-79)
+# ----------------------------------------------------------------------------
+class _EncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, enc, data, batch_sizes, *params):
+        out, ws, keep = enc._run_forward(data, batch_sizes)
+        ctx.enc, ctx.ws, ctx.keep = enc, ws, keep
+        ctx.data, ctx.batch_sizes = data, batch_sizes
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_out):
+        grads = ctx.enc._run_backward(ctx.data, ctx.batch_sizes, d_out.contiguous(), ctx.ws)
+        return (None, None, None) + tuple(grads)
+
+
+class RNN_Variational_Encoder(torch.nn.Module):
+    """Bi-directional LSTM/GRU over a PackedSequence; returns the last (h, c)
+    of every layer/direction flattened to (B, hidden_size_total)."""
+
+    def __init__(self, input_size, rnn_hidden_size, rnn_type="LSTM", rnn_layers=1, hidden_dropout=0.0,
+                 bidirectional=True, esn_leak=1.0):
+        super().__init__()
+        self.rnn = PackedRNN(rnn_type, input_size, rnn_hidden_size, rnn_layers, dropout=hidden_dropout,
+                             bidirectional=bidirectional, batch_first=True)
+        self.hidden_size_total = rnn_layers * rnn_hidden_size
+        if bidirectional:
+            self.hidden_size_total *= 2
+        if rnn_type == "LSTM":
+            self.hidden_size_total *= 2
+
+    def _cfg(self):
+        c = N.EncoderCfg()
+        c.input_size, c.hidden_size = self.rnn.input_size, self.rnn.hidden_size
+        c.rnn_type = N.LSTM if self.rnn.mode == "LSTM" else N.GRU
+        c.layers, c.bidirectional = self.rnn.num_layers, int(self.rnn.bidirectional)
+        return c
+
+    def _params(self, grads=None):
+        st = N.EncoderParams()
+        dirs = 2 if self.rnn.bidirectional else 1
+        for l in range(self.rnn.num_layers):
+            for d in range(dirs):
+                ws = self.rnn.layer_weights(l, d) if grads is None else grads[(l, d)]
+                st.w[l][d].w_ih, st.w[l][d].w_hh, st.w[l][d].b_ih, st.w[l][d].b_hh = [
+                    None if t is None else t.data_ptr() for t in ws]
+        return st
+
+    def _check_dropout(self):
+        if self.training and self.rnn.dropout > 0 and self.rnn.num_layers > 1:
+            raise NotImplementedError("inter-layer encoder dropout > 0 in training is not on the HIP path yet")
+
+    def _run_forward(self, data, batch_sizes, ws=None):
+        data = _f32c(data)
+        N.require_gpu(data)
+        cfg = self._cfg()
+        pk, bs = _packed_struct(data, batch_sizes, cfg.input_size)
+        L = N.lib()
+        nbytes = L.abcd_encoder_workspace_bytes(cfg, pk.T, pk.L, pk.B)
+        if nbytes == 0:
+            raise N.HipError("encoder: unsupported configuration (hidden size must be a multiple of 16)")
+        if ws is None or ws.numel() < nbytes:
+            ws = N.workspace(nbytes, data.device)
+        out = torch.empty(pk.B, self.hidden_size_total, device=data.device)
+        N.check(L.abcd_encoder_forward(cfg, self._params(), pk, N.ptr(out), N.ptr(ws), ws.numel(), N.stream()),
+                "encoder forward")
+        return out, ws, (bs, data)
+
+    def _run_backward(self, data, batch_sizes, d_out, ws, grad_views=None):
+        cfg = self._cfg()
+        pk, bs = _packed_struct(data, batch_sizes, cfg.input_size)
+        dirs = 2 if self.rnn.bidirectional else 1
+        if grad_views is None:
+            grad_views = {}
+            for l in range(self.rnn.num_layers):
+                for d in range(dirs):
+                    grad_views[(l, d)] = [torch.empty_like(p) for p in self.rnn.layer_weights(l, d)]
+        N.check(N.lib().abcd_encoder_backward(cfg, self._params(), pk, N.ptr(d_out), self._params(grad_views),
+                                              N.ptr(ws), ws.numel(), N.stream()), "encoder backward")
+        out = []
+        for l in range(self.rnn.num_layers):
+            for d in range(dirs):
+                out.extend(grad_views[(l, d)])
+        return out
+
+    def forward(self, packed_input):
+        self._check_dropout()
+        data, bsz = packed_input.data, packed_input.batch_sizes
+        params = list(self.rnn.parameters())
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _EncoderFn.apply(self, data, bsz, *params)
+        return self._run_forward(data, bsz)[0]
+
+    def pack_init_parameters(self):
+        return {"input_size": self.rnn.input_size, "rnn_hidden_size": self.rnn.hidden_size,
+                "rnn_type": self.rnn.mode.split("_")[0], "rnn_layers": self.rnn.num_layers,
+                "hidden_dropout": self.rnn.dropout, "bidirectional": self.rnn.bidirectional}
+
+
+# ----------------------------------------------------------------------------
+# Samplers (model.py:538-705, plain/modules/model.py:538-567)
+# ----------------------------------------------------------------------------
+class _SamplerBase(torch.nn.Module):
+    """Shared native plumbing of ABCDSampler and the plain feature Sampler."""
+
+    def _mlps(self):
+        raise NotImplementedError
+
+    def _scfg(self):
+        raise NotImplementedError
+
+    def _sparams(self):
+        st = N.SamplerParams()
+        for k, m in enumerate(self._mlps()):
+            w1, b1, w2, b2 = m.weights()
+            st.mlp[k].w1, st.mlp[k].b1, st.mlp[k].w2, st.mlp[k].b2 = (w1.data_ptr(), b1.data_ptr(),
+                                                                      w2.data_ptr(), b2.data_ptr())
+        if isinstance(self, ABCDSampler):
+            st.codebook = self.codebook.data_ptr()
+            st.posterior_shape_logits = self.posterior_shape_logits.data_ptr()
+            st.prior_concentration = self._prior_value()
+        return st
+
+    def _sgrads(self, views):
+        """views: dict name -> tensor (mlp{k}.w1 ..., codebook, posterior_shape_logits)."""
+        st = N.SamplerGrads()
+        for k in range(len(self._mlps())):
+            for f in ("w1", "b1", "w2", "b2"):
+                t = views.get(f"mlp{k}.{f}")
+                setattr(st.mlp[k], f, None if t is None else t.data_ptr())
+        for f in ("codebook", "posterior_shape_logits"):
+            t = views.get(f)
+            setattr(st, f, None if t is None else t.data_ptr())
+        return st
+
+    def _ws_for(self, B, device, ws=None):
+        nbytes = N.lib().abcd_sampler_workspace_bytes(self._scfg(), B)
+        if nbytes == 0:
+            raise N.HipError("sampler: unsupported configuration (sizes must be multiples of 16)")
+        if ws is None or ws.numel() < nbytes:
+            ws = N.workspace(nbytes, device)
+        return ws
+
+    def _run_forward(self, h, ws=None):
+        h = _f32c(h)
+        N.require_gpu(h)
+        B = h.shape[0]
+        ws = self._ws_for(B, h.device, ws)
+        out = torch.empty(B, self._logit_width(), device=h.device)
+        N.check(N.lib().abcd_sampler_forward(self._scfg(), self._sparams(), N.ptr(h), B, N.ptr(out), N.ptr(ws),
+                                             ws.numel(), N.stream()), "sampler forward")
+        return out, ws
+
+
+class _SamplerForwardFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, samp, h, *params):
+        out, ws = samp._run_forward(h)
+        ctx.samp, ctx.ws, ctx.h = samp, ws, h
+        out._abcd_ws = ws
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_logits):
+        samp = ctx.samp
+        views = samp._grad_views_forward()
+        d_h = torch.empty_like(ctx.h) if ctx.needs_input_grad[1] else None
+        N.check(N.lib().abcd_sampler_forward_backward(
+            samp._scfg(), samp._sparams(), N.ptr(ctx.h), ctx.h.shape[0], N.ptr(d_logits.contiguous()), N.ptr(d_h),
+            samp._sgrads(views), 0, N.ptr(ctx.ws), ctx.ws.numel(), N.stream()), "sampler forward backward")
+        return (None, d_h) + samp._order_grads(views)
+
+
+class _SampleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, samp, logits, mode, tau, ws, noise_t, seed, offset, *params):
+        B = logits.shape[0]
+        feats = torch.empty(B, samp._feat_dim(), device=logits.device)
+        N.check(N.lib().abcd_sampler_sample(samp._scfg(), samp._sparams(), N.ptr(logits), B, mode, tau,
+                                            N.ptr(noise_t), seed, offset, N.ptr(feats), N.ptr(ws), ws.numel(),
+                                            N.stream()), "sampler sample")
+        ctx.samp, ctx.ws, ctx.mode, ctx.tau, ctx.B = samp, ws, mode, tau, B
+        return feats
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_feats):
+        samp = ctx.samp
+        d_logits = torch.empty(ctx.B, samp._logit_width(), device=d_feats.device)
+        d_cb = torch.empty_like(samp.codebook) if isinstance(samp, ABCDSampler) else None
+        N.check(N.lib().abcd_sampler_sample_backward(samp._scfg(), samp._sparams(), ctx.B, ctx.mode, ctx.tau,
+                                                     N.ptr(d_feats.contiguous()), N.ptr(d_logits), N.ptr(d_cb),
+                                                     N.ptr(ctx.ws), ctx.ws.numel(), N.stream()),
+                "sampler sample backward")
+        grads = [None] * len(samp._sample_params())
+        if d_cb is not None:
+            grads[0] = d_cb
+        return (None, d_logits, None, None, None, None, None, None) + tuple(grads)
+
+
+class _KLFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, samp, logits, Ntot, ws, *params):
+        B = logits.shape[0]
+        kl = torch.empty((), device=logits.device)
+        N.check(N.lib().abcd_sampler_kl(samp._scfg(), samp._sparams(), N.ptr(logits), B, float(Ntot), N.ptr(kl),
+                                        N.ptr(ws), ws.numel(), N.stream()), "sampler kl")
+        ctx.samp, ctx.ws, ctx.B, ctx.N = samp, ws, B, float(Ntot)
+        return kl
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_kl):
+        samp = ctx.samp
+        d_logits = torch.empty(ctx.B, samp._logit_width(), device=d_kl.device)
+        d_psl = torch.empty_like(samp.posterior_shape_logits) if isinstance(samp, ABCDSampler) else None
+        N.check(N.lib().abcd_sampler_kl_backward(samp._scfg(), samp._sparams(), ctx.B, ctx.N,
+                                                 N.ptr(d_kl.contiguous()), 0, N.ptr(d_logits), N.ptr(d_psl),
+                                                 N.ptr(ctx.ws), ctx.ws.numel(), N.stream()), "sampler kl backward")
+        grads = [None] * len(samp._kl_params())
+        if d_psl is not None:
+            grads[0] = d_psl
+        return (None, d_logits, None, None) + tuple(grads)
+
+
+def _ws_of(samp, logits):
+    ws = getattr(logits, "_abcd_ws", None)
+    if ws is None:
+        ws = samp._ws_for(logits.shape[0], logits.device)
+        try:
+            logits._abcd_ws = ws
+        except Exception:
+            pass
+    return ws
+
+
+class ABCDSampler(_SamplerBase):
+    """"A"ttention-"B"ased "C"ategorical sampler with a "D"irichlet prior (model.py:538-673)."""
+
+    def __init__(self, input_size, mlp_hidden_size, num_categories, feature_dim, prior_concentration=1.0,
+                 min_temperature=1.0, epoch_init_iter_counts=0, temperature_update_freq=1000,
+                 temperature_anneal_rate=1e-5):
+        super().__init__()
+        self.num_categories = num_categories
+        self.to_code_like = MLP(input_size, mlp_hidden_size, feature_dim)
+        self.min_temperature = min_temperature
+        self.epoch_init_iter_counts = epoch_init_iter_counts
+        self.iter_counts = epoch_init_iter_counts
+        self.temperature_update_freq = temperature_update_freq
+        self.temperature_anneal_rate = temperature_anneal_rate
+        self.update_temperature((self.iter_counts // self.temperature_update_freq) * self.temperature_update_freq)
+        self.register_buffer("prior_concentration", torch.tensor(prior_concentration))
+        self.register_parameter("posterior_shape_logits",
+                                torch.nn.Parameter(torch.randn(num_categories), requires_grad=True))
+        self.register_parameter("codebook", torch.nn.Parameter(torch.randn((feature_dim, num_categories)),
+                                                               requires_grad=True))
+        self._prior_cache = (None, float(prior_concentration))
+
+    # -- native plumbing --
+    def _prior_value(self):
+        key = (self.prior_concentration.data_ptr(), self.prior_concentration._version)
+        if self._prior_cache[0] != key:
+            self._prior_cache = (key, float(self.prior_concentration.detach().cpu()))
+        return self._prior_cache[1]
+
+    def _mlps(self):
+        return [self.to_code_like]
+
+    def _scfg(self):
+        c = N.SamplerCfg()
+        c.input_size, c.mlp_hidden = self.to_code_like.input_size, self.to_code_like.hidden_size
+        c.num_categories, c.feature_dim, c.plain = self.num_categories, self.to_code_like.output_size, 0
+        return c
+
+    def _logit_width(self):
+        return self.num_categories
+
+    def _feat_dim(self):
+        return self.to_code_like.output_size
+
+    def _sample_params(self):
+        return [self.codebook]
+
+    def _kl_params(self):
+        return [self.posterior_shape_logits]
+
+    def _grad_views_forward(self):
+        w1, b1, w2, b2 = self.to_code_like.weights()
+        return {"mlp0.w1": torch.empty_like(w1), "mlp0.b1": torch.empty_like(b1), "mlp0.w2": torch.empty_like(w2),
+                "mlp0.b2": torch.empty_like(b2), "codebook": torch.empty_like(self.codebook)}
+
+    def _order_grads(self, views):
+        # parameter order of the Function call: to_code_like (w1,b1,w2,b2), codebook
+        return (views["mlp0.w1"], views["mlp0.b1"], views["mlp0.w2"], views["mlp0.b2"], views["codebook"])
+
+    # -- reference API --
+    def forward(self, x):
+        params = list(self.to_code_like.weights()) + [self.codebook]
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
+            return _SamplerForwardFn.apply(self, x, *params)
+        out, ws = self._run_forward(x)
+        out._abcd_ws = ws
+        return out
+
+    def sample(self, logits, no_sample=False):
+        logits = _f32c(logits)
+        N.require_gpu(logits)
+        ws = _ws_of(self, logits)
+        B, K = logits.shape
+        if no_sample:
+            mode, tau, nt, seed, off = N.SAMPLE_SOFTMAX, 1.0, None, 0, 0
+        else:
+            mode, tau = N.SAMPLE_GUMBEL, float(self.temperature)
+            nt, seed, off = _noise.gumbel(B, K, logits.device)
+        if torch.is_grad_enabled() and (logits.requires_grad or self.codebook.requires_grad):
+            return _SampleFn.apply(self, logits, mode, tau, ws, nt, seed, off, self.codebook)
+        feats = torch.empty(B, self._feat_dim(), device=logits.device)
+        N.check(N.lib().abcd_sampler_sample(self._scfg(), self._sparams(), N.ptr(logits), B, mode, tau, N.ptr(nt),
+                                            seed, off, N.ptr(feats), N.ptr(ws), ws.numel(), N.stream()),
+                "sampler sample")
+        return feats
+
+    def kl_divergence(self, logits, entire_data_size):
+        logits = _f32c(logits)
+        N.require_gpu(logits)
+        ws = _ws_of(self, logits)
+        if torch.is_grad_enabled() and (logits.requires_grad or self.posterior_shape_logits.requires_grad):
+            return _KLFn.apply(self, logits, entire_data_size, ws, self.posterior_shape_logits)
+        kl = torch.empty((), device=logits.device)
+        N.check(N.lib().abcd_sampler_kl(self._scfg(), self._sparams(), N.ptr(logits), logits.shape[0],
+                                        float(entire_data_size), N.ptr(kl), N.ptr(ws), ws.numel(), N.stream()),
+                "sampler kl")
+        return kl
+
+    def log_pmf(self, targets, logits):
+        return torch.nn.functional.cross_entropy(logits, targets, reduction="sum")
+
+    def increment_iter_counts(self):
+        self.iter_counts += 1
+        if self.iter_counts % self.temperature_update_freq == 0:
+            self.update_temperature()
+
+    def update_epoch_init_iter_counts(self):
+        self.epoch_init_iter_counts = self.iter_counts
+
+    def update_temperature(self, steps=None):
+        if steps is None:
+            steps = self.iter_counts
+        self.temperature = min(self.min_temperature, math.exp(-self.temperature_anneal_rate * steps))
+
+    def pack_init_parameters(self):
+        return {"input_size": self.to_code_like.input_size, "mlp_hidden_size": self.to_code_like.hidden_size,
+                "num_categories": self.num_categories, "feature_dim": self.to_code_like.output_size,
+                "prior_concentration": self._prior_value(), "min_temperature": self.min_temperature,
+                "epoch_init_iter_counts": self.epoch_init_iter_counts,
+                "temperature_update_freq": self.temperature_update_freq,
+                "temperature_anneal_rate": self.temperature_anneal_rate}
+
+
+class Sampler(_SamplerBase):
+    """``model.py:676-705``.  As the decoder's emission sampler it is a
+    parameter holder (the emission MLPs run inside the fused decoder kernels);
+    as the plain VAE's feature sampler (``plain/learning.py:90``) forward /
+    sample / kl_divergence run on the HIP path."""
+
+    def __init__(self, input_size, mlp_hidden_size, output_size, distribution_name="isotropic_gaussian"):
+        super().__init__()
+        self.distribution_name = distribution_name
+        self._sampler, self._log_pdf, self._kl_divergence, num_parameters = choose_distribution(distribution_name)
+        self.to_parameters = MLP_To_k_Vecs(input_size, mlp_hidden_size, output_size, num_parameters)
+
+    def _mlps(self):
+        return list(self.to_parameters.mlps)
+
+    def _scfg(self):
+        c = N.SamplerCfg()
+        c.input_size, c.mlp_hidden = self.to_parameters.input_size, self.to_parameters.hidden_size
+        c.num_categories, c.feature_dim, c.plain = 16, self.to_parameters.output_size, 1
+        return c
+
+    def _logit_width(self):
+        return 2 * self.to_parameters.output_size
+
+    def _feat_dim(self):
+        return self.to_parameters.output_size
+
+    def _sample_params(self):
+        return []
+
+    def _kl_params(self):
+        return []
+
+    def _grad_views_forward(self):
+        v = {}
+        for k, m in enumerate(self._mlps()):
+            for f, t in zip(("w1", "b1", "w2", "b2"), m.weights()):
+                v[f"mlp{k}.{f}"] = torch.empty_like(t)
+        return v
+
+    def _order_grads(self, views):
+        return tuple(views[f"mlp{k}.{f}"] for k in range(2) for f in ("w1", "b1", "w2", "b2"))
+
+    def forward(self, parameter_seed):
+        params = [t for m in self._mlps() for t in m.weights()]
+        f = self.to_parameters.output_size
+        if torch.is_grad_enabled() and (parameter_seed.requires_grad or any(p.requires_grad for p in params)):
+            mv = _SamplerForwardFn.apply(self, parameter_seed, *params)
+        else:
+            mv, ws = self._run_forward(parameter_seed)
+            mv._abcd_ws = ws
+        mu, lv = mv[:, :f], mv[:, f:]
+        mu._abcd_mv = mv
+        return [mu, lv]
+
+    def sample(self, parameters):
+        mu, lv = parameters
+        mv = getattr(mu, "_abcd_mv", None)
+        if mv is None:  # parameters not produced by this module's forward: reference torch formula
+            return self._sampler(*parameters)
+        ws = _ws_of(self, mv)
+        B, f = mu.shape
+        nt, seed, off = _noise.normal(B, f, mu.device)
+        if torch.is_grad_enabled() and mv.requires_grad:
+            return _SampleFn.apply(self, mv, 0, 1.0, ws, nt, seed, off)
+        feats = torch.empty(B, f, device=mu.device)
+        N.check(N.lib().abcd_sampler_sample(self._scfg(), self._sparams(), N.ptr(mv), B, 0, 1.0, N.ptr(nt), seed,
+                                            off, N.ptr(feats), N.ptr(ws), ws.numel(), N.stream()), "plain sample")
+        return feats
+
+    def kl_divergence(self, parameters):
+        mu, lv = parameters
+        mv = getattr(mu, "_abcd_mv", None)
+        if mv is None:
+            return self._kl_divergence(*parameters)
+        ws = _ws_of(self, mv)
+        if torch.is_grad_enabled() and mv.requires_grad:
+            return _KLFn.apply(self, mv, 1.0, ws)
+        kl = torch.empty((), device=mu.device)
+        N.check(N.lib().abcd_sampler_kl(self._scfg(), self._sparams(), N.ptr(mv), mu.shape[0], 1.0, N.ptr(kl),
+                                        N.ptr(ws), ws.numel(), N.stream()), "plain kl")
+        return kl
+
+    def log_pdf(self, samples, parameters):
+        return self._log_pdf(samples, *parameters)
+
+    def pack_init_parameters(self):
+        return {"input_size": self.to_parameters.input_size, "mlp_hidden_size": self.to_parameters.hidden_size,
+                "output_size": self.to_parameters.output_size, "distribution_name": self.distribution_name}
+
+
+# ----------------------------------------------------------------------------
+# Decoder (model.py:84-285)
+# ----------------------------------------------------------------------------
+class _DecoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dec, features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, *params):
+        res = dec._run_forward(features, batch_sizes, speaker, gt, gt_off, eps, seed, offset)
+        em, off, flat, mu, lv, offl, ws = res
+        ctx.dec, ctx.ws = dec, ws
+        ctx.saved = (features, batch_sizes, speaker, gt, gt_off)
+        ctx.feedback = dec._feedback()
+        ctx.mark_non_differentiable(flat, mu, lv, offl)
+        ctx.set_materialize_grads(False)
+        return em, off, flat, mu, lv, offl
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, d_em, d_off, d_flat, d_mu, d_lv, d_offl):
+        if any(g is not None for g in (d_flat, d_mu, d_lv, d_offl)):
+            raise NotImplementedError("decoder backward supports gradients of the emission and offset losses only")
+        features, batch_sizes, speaker, gt, gt_off = ctx.saved
+        dev = features.device
+        z = torch.zeros((), device=dev)
+        d_em = z if d_em is None else d_em.reshape(()).contiguous()
+        d_off = z if d_off is None else d_off.reshape(()).contiguous()
+        d_feat, grads = ctx.dec._run_backward(features, batch_sizes, speaker, gt, gt_off, d_em, d_off, ctx.ws,
+                                              feedback=ctx.feedback)
+        return (None, d_feat, None, None, None, None, None, None, None) + tuple(grads)
+
+
+class RNN_Variational_Decoder(torch.nn.Module):
+    """Self-feedback LSTM/GRU decoder with isotropic-Gaussian emission and an
+    end-of-segment (offset) predictor, unidirectional (model.py:84-196)."""
+
+    def __init__(self, output_size, rnn_hidden_size, mlp_hidden_size, feature_size,
+                 emission_distr_name="isotropic_gaussian", rnn_type="LSTM", rnn_layers=1, input_dropout=0.0,
+                 self_feedback=True, bidirectional=False, right2left_weight=0.5, esn_leak=1.0, num_speakers=None,
+                 speaker_embed_dim=None):
+        super().__init__()
+        assert rnn_layers == 1, "Only rnn_layers=1 is currently supported."
+        if bidirectional:
+            raise NotImplementedError("bidirectional decoder: broken in the reference (model.py:224,258); "
+                                      "not on the HIP path")
+        if emission_distr_name != "isotropic_gaussian":
+            raise NotImplementedError(emission_distr_name)
+        if not self_feedback:
+            input_dropout = 1.0
+        self.bidirectional = False
+        self.rnn_type = rnn_type
+        self.feature_size = feature_size
+        if num_speakers is None or speaker_embed_dim is None:
+            self.embed_speaker = None
+        else:
+            self.embed_speaker = torch.nn.Embedding(num_speakers, speaker_embed_dim, sparse=True)
+            feature_size += speaker_embed_dim
+        hidden_size_total = rnn_hidden_size * (2 if rnn_type == "LSTM" else 1)
+        self.feature2hidden = torch.nn.Linear(feature_size, hidden_size_total)
+        self.offset_predictor = MLP(rnn_hidden_size, mlp_hidden_size, 1)
+        self.bce_with_logits_loss = torch.nn.BCEWithLogitsLoss(reduction="sum")
+        self.emission_sampler = Sampler(rnn_hidden_size, mlp_hidden_size, output_size,
+                                        distribution_name=emission_distr_name)
+        self.rnn_cell = RNN_Cell(output_size, rnn_hidden_size, model_type=rnn_type, input_dropout=input_dropout,
+                                 esn_leak=esn_leak)
+
+    # -- native plumbing --
+    def _feedback(self):
+        p = self.rnn_cell.drop.p
+        if not self.training or p == 0.0:
+            return 1
+        if p == 1.0:
+            return 0
+        raise NotImplementedError("decoder input dropout with 0 < p < 1 in training is not on the HIP path yet")
+
+    def _dcfg(self, feedback=None):
+        c = N.DecoderCfg()
+        cell = self.rnn_cell.cell
+        c.output_size, c.hidden_size = cell.input_size, cell.hidden_size
+        c.mlp_hidden, c.feature_size = self.offset_predictor.hidden_size, self.feature_size
+        c.rnn_type = N.LSTM if self.rnn_cell.mode == "LSTM" else N.GRU
+        c.feedback = self._feedback() if feedback is None else feedback
+        if self.embed_speaker is not None:
+            c.num_speakers, c.speaker_dim = self.embed_speaker.num_embeddings, self.embed_speaker.embedding_dim
+        return c
+
+    def _param_list(self):
+        out = []
+        if self.embed_speaker is not None:
+            out.append(self.embed_speaker.weight)
+        out += [self.feature2hidden.weight, self.feature2hidden.bias]
+        out += list(self.offset_predictor.weights())
+        for m in self.emission_sampler.to_parameters.mlps:
+            out += list(m.weights())
+        cell = self.rnn_cell.cell
+        out += [cell.weight_ih, cell.weight_hh, cell.bias_ih, cell.bias_hh]
+        return out
+
+    def _dparams(self, tensors=None):
+        t = self._param_list() if tensors is None else tensors
+        st = N.DecoderParams()
+        i = 0
+        if self.embed_speaker is not None:
+            st.embed_speaker = None if t[0] is None else t[0].data_ptr()
+            i = 1
+        p = [None if x is None else x.data_ptr() for x in t[i:]]
+        st.f2h_w, st.f2h_b = p[0], p[1]
+        for name, k in (("offset", 2), ("mu", 6), ("lv", 10)):
+            m = getattr(st, name)
+            m.w1, m.b1, m.w2, m.b2 = p[k:k + 4]
+        st.cell.w_ih, st.cell.w_hh, st.cell.b_ih, st.cell.b_hh = p[14:18]
+        return st
+
+    def workspace_bytes(self, T, L, B):
+        return N.lib().abcd_decoder_workspace_bytes(self._dcfg(1), T, L, B)
+
+    def _run_forward(self, features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, ws=None,
+                     want_outputs=True):
+        features = _f32c(features)
+        N.require_gpu(features)
+        cfg = self._dcfg()
+        pk, bs = _packed_struct(gt, batch_sizes, cfg.output_size)
+        L = N.lib()
+        nbytes = L.abcd_decoder_workspace_bytes(cfg, pk.T, pk.L, pk.B)
+        if nbytes == 0:
+            raise N.HipError("decoder: unsupported configuration (sizes must be multiples of 16)")
+        if ws is None or ws.numel() < nbytes:
+            ws = N.workspace(nbytes, features.device)
+        dev = features.device
+        F = cfg.output_size
+        spk = None
+        if self.embed_speaker is not None:
+            spk = speaker.to(dev, torch.int64).contiguous()
+        flat = mu = lv = None
+        if want_outputs:
+            flat = torch.empty(pk.L, F, device=dev)
+            mu = torch.empty(pk.L, F, device=dev)
+            lv = torch.empty(pk.L, F, device=dev)
+        offl = torch.empty(pk.L, device=dev)
+        losses = torch.zeros(2, device=dev)
+        N.check(L.abcd_decoder_forward(cfg, self._dparams(), pk, N.ptr(features), N.ptr(spk),
+                                       N.ptr(None if gt_off is None else _f32c(gt_off)), N.ptr(eps), seed, offset,
+                                       N.ptr(flat), N.ptr(mu), N.ptr(lv), N.ptr(offl), N.ptr(losses), N.ptr(ws),
+                                       ws.numel(), N.stream()), "decoder forward")
+        em = losses[0] if gt is not None else None
+        off = losses[1] if gt_off is not None else None
+        return em, off, flat, mu, lv, offl, ws
+
+    def _run_backward(self, features, batch_sizes, speaker, gt, gt_off, d_em, d_off, ws, grad_tensors=None,
+                      feedback=None, d_features=None):
+        cfg = self._dcfg(feedback)
+        pk, bs = _packed_struct(gt, batch_sizes, cfg.output_size)
+        dev = features.device
+        spk = speaker.to(dev, torch.int64).contiguous() if self.embed_speaker is not None else None
+        if grad_tensors is None:
+            grad_tensors = [torch.empty_like(p) for p in self._param_list()]
+        if d_features is None:
+            d_features = torch.empty_like(features)
+        N.check(N.lib().abcd_decoder_backward(cfg, self._dparams(), pk, N.ptr(features), N.ptr(spk),
+                                              N.ptr(_f32c(gt_off)), N.ptr(d_em), N.ptr(d_off), N.ptr(d_features),
+                                              self._dparams(grad_tensors), N.ptr(ws), ws.numel(), N.stream()),
+                "decoder backward")
+        return d_features, grad_tensors
+
+    # -- reference API --
+    def forward(self, features, lengths=None, batch_sizes=None, speaker=None, ground_truth_out=None,
+                ground_truth_offset=None):
+        assert (lengths is not None) or (batch_sizes is not None), "Either lengths or batch_sizes must be given."
+        if lengths is not None:
+            batch_sizes = self._length_to_batch_sizes(lengths)
+        if not torch.is_tensor(batch_sizes):
+            batch_sizes = torch.tensor([int(b) for b in batch_sizes], dtype=torch.int64)
+        F = self.rnn_cell.cell.input_size
+        eps, seed, offset = _noise.decoder_eps(batch_sizes, F, features.device)
+        params = self._param_list()
+        gt = ground_truth_out
+        gt_off = ground_truth_offset
+        if (gt is not None and gt_off is not None and torch.is_grad_enabled()
+                and (features.requires_grad or any(p.requires_grad for p in params))):
+            em, off, flat, mu, lv, offl = _DecoderFn.apply(self, features, batch_sizes, speaker, _f32c(gt),
+                                                           gt_off, eps, seed, offset, *params)
+        else:
+            em, off, flat, mu, lv, offl, _ = self._run_forward(features, batch_sizes, speaker,
+                                                               None if gt is None else _f32c(gt), gt_off, eps,
+                                                               seed, offset)
+        return em, off, flat, (mu, lv), offl
+
+    def _length_to_batch_sizes(self, lengths):
+        lengths = torch.as_tensor(lengths).cpu()
+        return torch.tensor([int((lengths > t).sum()) for t in range(int(lengths.max()))], dtype=torch.int64)
+
+    def pack_init_parameters(self):
+        parameters = {"output_size": self.rnn_cell.cell.input_size, "rnn_hidden_size": self.rnn_cell.cell.hidden_size,
+                      "mlp_hidden_size": self.offset_predictor.hidden_size, "feature_size": self.feature_size,
+                      "emission_distr_name": self.emission_sampler.distribution_name,
+                      "rnn_type": self.rnn_cell.mode, "rnn_layers": 1, "input_dropout": self.rnn_cell.drop.p,
+                      "bidirectional": self.bidirectional}
+        if self.embed_speaker is not None:
+            parameters["num_speakers"] = self.embed_speaker.num_embeddings
+            parameters["speaker_embed_dim"] = self.embed_speaker.embedding_dim
+        return parameters

@@ -1,0 +1,110 @@
+"""Noise sources for the stochastic parts of the step (Gumbel, Gaussian).
+
+Two modes:
+
+* ``"philox"`` (default, production): the kernels draw Philox-4x32-10
+  counter-based noise in place (``abcd_common.h``), keyed by ``(seed, offset)``;
+  nothing is drawn or copied on the host.  The stream is advanced like torch's
+  own CUDA Philox generator: one offset block per draw.
+* ``"reference"``: the noise is drawn on the HOST from torch's global CPU
+  generator, with exactly the calls, shapes and order the reference makes
+  (``F.gumbel_softmax``'s ``-empty_like(logits).exponential_().log()``,
+  ``model.py:604``; ``randn_like(mean)`` per decoder step, ``model.py:19``;
+  the plain sampler's ``randn_like(mean)``), then uploaded.  This reproduces a
+  reference CPU run's random numbers bit-for-bit and is what
+  the parity tests and the toy-trajectory check use.
+"""
+import torch
+
+_state = {"mode": "philox", "seed": 0x5EED1111, "offset": 0}
+_replay = []  # FIFO of host tensors consumed before any other source (tests / replays)
+
+
+def replay(*tensors):
+    """Queue exact noise tensors (e.g. recorded from a reference run); each
+    draw pops one, in call order, and checks its shape."""
+    _replay.extend(tensors)
+
+
+def _pop(shape, device):
+    t = _replay.pop(0)
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"replayed noise has shape {tuple(t.shape)}, draw wants {tuple(shape)}")
+    return t.to(device=device, dtype=torch.float32).contiguous(), 0, 0
+
+
+def set_mode(mode):
+    if mode not in ("philox", "reference"):
+        raise ValueError(f"noise mode must be 'philox' or 'reference', not {mode!r}")
+    _state["mode"] = mode
+
+
+def get_mode():
+    return _state["mode"]
+
+
+def manual_seed(seed):
+    _state["seed"] = int(seed) & 0xFFFFFFFFFFFFFFFF
+    _state["offset"] = 0
+
+
+def get_state():
+    return dict(_state)
+
+
+def set_state(st):
+    _state.update({k: st[k] for k in ("mode", "seed", "offset") if k in st})
+
+
+class mode:
+    """Context manager: ``with noise.mode("reference"): ...``"""
+
+    def __init__(self, m):
+        self.m = m
+
+    def __enter__(self):
+        self.prev = get_mode()
+        set_mode(self.m)
+
+    def __exit__(self, *exc):
+        set_mode(self.prev)
+
+
+def philox(n):
+    """Reserve n counters of the Philox stream: returns (seed, offset)."""
+    off = _state["offset"]
+    _state["offset"] = off + ((int(n) + 3) // 4) * 4
+    return _state["seed"], off
+
+
+def gumbel(B, K, device):
+    """(noise tensor or None, seed, offset) for a B x K Gumbel draw."""
+    if _replay:
+        return _pop((B, K), device)
+    if _state["mode"] == "reference":
+        g = -torch.empty(B, K).exponential_().log()
+        return g.to(device, non_blocking=True), 0, 0
+    s, o = philox(B * K)
+    return None, s, o
+
+
+def normal(B, f, device):
+    """(noise tensor or None, seed, offset) for a B x f standard normal draw."""
+    if _replay:
+        return _pop((B, f), device)
+    if _state["mode"] == "reference":
+        return torch.randn(B, f).to(device, non_blocking=True), 0, 0
+    s, o = philox(B * f)
+    return None, s, o
+
+
+def decoder_eps(batch_sizes, F, device):
+    """Per-step ``randn(bs_t, F)`` in packed order (reference) or a Philox block."""
+    L = int(sum(int(b) for b in batch_sizes))
+    if _replay:
+        return _pop((L, F), device)
+    if _state["mode"] == "reference":
+        eps = torch.cat([torch.randn(int(bs), F) for bs in batch_sizes], 0)
+        return eps.to(device, non_blocking=True), 0, 0
+    s, o = philox(L * F)
+    return None, s, o

@@ -111,7 +111,7 @@ def import_reference(variant_dir):
 # small one-step fixtures
 # --------------------------------------------------------------------------
 SMALL_LENGTHS = [12, 10, 10, 7, 4, 2]
-SMALL_DIMS = dict(F=33, H=32, Hm=32, D=32, K=16, S=16, NSPK=3, FPLAIN=8)
+SMALL_DIMS = dict(F=33, H=32, Hm=32, D=32, K=16, S=16, NSPK=3, FPLAIN=16)
 
 SMALL_VARIANTS = {
     "lstm_gumbel": dict(rnn="LSTM"),

@@ -1,0 +1,55 @@
+"""Helpers shared by the GPU parity tests: build the HIP-backed modules with a
+fixture's configuration and weights."""
+import torch
+
+from golden_io import params_from
+
+
+def modules_api():
+    from modules import model as M  # seq2seq_abcd-vae_amd/modules (product)
+    return M
+
+
+def build_from_meta(meta, arr=None, device="cuda", cfg_override=None):
+    M = modules_api()
+    d = meta["dims"]
+    F, H, Hm, D, K = d["F"], d["H"], d["Hm"], d["D"], d["K"]
+    rnn = meta["rnn"]
+    speaker = meta.get("speaker", False)
+    torch.manual_seed(1111)
+    enc = M.RNN_Variational_Encoder(F, H, rnn_type=rnn, rnn_layers=meta.get("layers", 1),
+                                    bidirectional=meta.get("bidirectional", True))
+    if meta.get("plain"):
+        samp = M.Sampler(enc.hidden_size_total, Hm, d["FPLAIN"])
+        fdim = d["FPLAIN"]
+    else:
+        samp = M.ABCDSampler(enc.hidden_size_total, Hm, K, D)
+        fdim = D
+        if meta.get("temperature"):
+            samp.temperature = meta["temperature"]
+    dec = M.RNN_Variational_Decoder(F, H, Hm, fdim, rnn_type=rnn, self_feedback=not meta.get("greedy", False),
+                                    num_speakers=d["NSPK"] if speaker else None,
+                                    speaker_embed_dim=d["S"] if speaker else None)
+    if arr is not None:
+        P = params_from(arr)
+        for name, mod in (("encoder", enc), ("feature_sampler", samp), ("decoder", dec)):
+            sd = {k[len(name) + 1:]: v for k, v in P.items() if k.startswith(name + "/")}
+            mod.load_state_dict(sd)
+    for m in (enc, samp, dec):
+        m.to(device)
+        m.train()
+    return enc, samp, dec
+
+
+def named_params(enc, samp, dec):
+    out = {}
+    for name, mod in (("encoder", enc), ("feature_sampler", samp), ("decoder", dec)):
+        for k, v in mod.named_parameters():
+            out[f"{name}/{k}"] = v
+    return out
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)

@@ -1,0 +1,111 @@
+"""CPU-side tests of the product package: the C-ABI library loads and exports
+every symbol include/abcd_hip.h declares (no compute without a GPU), the
+nn.Module surface has the reference's names / init / state_dict, and compute
+refuses CPU tensors (no silent fallback)."""
+import hashlib
+import os
+import re
+
+import pytest
+import torch
+
+from golden_io import SMALL, load_small, params_from, load_toy
+from gpu_helpers import build_from_meta
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "abcd_hip.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(abcd_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    from modules import _native as N
+    lib = N.lib()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(N.EXPORTED) == set(syms), set(N.EXPORTED) ^ set(syms)
+    assert b"gfx950" in lib.abcd_version()
+
+
+def test_workspace_queries_without_gpu():
+    from modules import _native as N
+    c = N.EncoderCfg(129, 256, N.LSTM, 1, 1)
+    assert N.lib().abcd_encoder_out_size(c) == 1024
+    assert N.lib().abcd_encoder_workspace_bytes(c, 200, 65583, 512) > 65583 * 256 * 4
+    bad = N.EncoderCfg(129, 250, N.LSTM, 1, 1)
+    assert N.lib().abcd_encoder_workspace_bytes(bad, 200, 65583, 512) == 0
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_init_and_state_dict_match_reference(name):
+    meta, arr = load_small(name)
+    enc, samp, dec = build_from_meta(meta, None, device="cpu")
+    ref = params_from(arr)
+    ours = {}
+    for pfx, m in (("encoder", enc), ("feature_sampler", samp), ("decoder", dec)):
+        ours.update({f"{pfx}/{k}": v for k, v in m.state_dict().items()})
+    assert list(ours) == list(ref)
+    for k in ref:
+        assert torch.equal(ours[k], ref[k]), k
+
+
+def test_toy_init_checksums():
+    from modules import model as M
+    cks, toy = load_toy()
+    torch.manual_seed(1111)
+    enc = M.RNN_Variational_Encoder(65, 256, rnn_type="LSTM")
+    samp = M.ABCDSampler(enc.hidden_size_total, 256, 16, 256)
+    dec = M.RNN_Variational_Decoder(65, 256, 256, 256, rnn_type="LSTM")
+    for name, m in (("encoder", enc), ("feature_sampler", samp), ("decoder", dec)):
+        h = hashlib.sha256()
+        for v in m.state_dict().values():
+            h.update(v.detach().contiguous().numpy().tobytes())
+        assert h.hexdigest()[:16] == cks[name][1], name
+
+
+def test_pack_init_parameters_roundtrip():
+    from modules import model as M
+    enc = M.RNN_Variational_Encoder(65, 32, rnn_type="GRU", rnn_layers=2)
+    p = enc.pack_init_parameters()
+    assert p == {"input_size": 65, "rnn_hidden_size": 32, "rnn_type": "GRU", "rnn_layers": 2,
+                 "hidden_dropout": 0.0, "bidirectional": True}
+    enc2 = M.RNN_Variational_Encoder(**p)
+    enc2.load_state_dict(enc.state_dict())
+    samp = M.ABCDSampler(enc.hidden_size_total, 32, 16, 32)
+    s2 = M.ABCDSampler(**samp.pack_init_parameters())
+    s2.load_state_dict(samp.state_dict())
+    dec = M.RNN_Variational_Decoder(65, 32, 32, 32, num_speakers=3, speaker_embed_dim=16)
+    d2 = M.RNN_Variational_Decoder(**dec.pack_init_parameters())
+    d2.load_state_dict(dec.state_dict())
+
+
+def test_temperature_schedule():
+    """tau = min(min_temperature, exp(-rate * steps)), refreshed every 1000
+    iterations: min_temperature acts as a cap (model.py:644-658)."""
+    import math
+    from modules import model as M
+    s = M.ABCDSampler(32, 32, 16, 32)
+    assert s.temperature == 1.0
+    for _ in range(999):
+        s.increment_iter_counts()
+    assert s.temperature == 1.0
+    s.increment_iter_counts()
+    assert s.temperature == math.exp(-1e-5 * 1000)
+    s2 = M.ABCDSampler(32, 32, 16, 32, min_temperature=0.5)
+    assert s2.temperature == 0.5
+    s3 = M.ABCDSampler(32, 32, 16, 32, epoch_init_iter_counts=2500)
+    assert s3.temperature == math.exp(-1e-5 * 2000)
+
+
+def test_compute_refuses_cpu_tensors():
+    from modules import model as M
+    enc = M.RNN_Variational_Encoder(33, 32)
+    x = torch.nn.utils.rnn.pack_sequence([torch.randn(5, 33), torch.randn(3, 33)])
+    with pytest.raises(RuntimeError):
+        enc(x)
