@@ -1,0 +1,259 @@
+#!/usr/bin/env python3
+"""Throughput of the ABCD-VAE training step (ABCD-VAE/learning.py:147-163) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5]
+
+Metric (BASELINE.json): segments/sec/node for a full training step
+(encoder -> sampler -> KL -> decoder -> loss -> backward -> all-reduce ->
+clip -> SGD), weak scaling: b = 512 segments per GPU per step.  Workload
+`c2` (default) is BASELINE.json configs[1]: synthetic segments, lengths
+U{50..200} with the longest of each batch forced to 200 frames, 129 FFT bins,
+K = 128, hidden 256, bi-LSTM encoder, self-feedback LSTM decoder, Gumbel
+sampling on, N = 10,000.  Inputs are resident in HBM before the timed region;
+noise is drawn in-kernel (Philox).
+
+Besides the one JSON line the driver reads, it reports
+  roofline     -- FP32-MFMA roofline of the dominant kernel family, timed live
+                  with HIP events;
+  cpu_baseline -- the CPU oracle (oracle/abcd_oracle.py, a torch-CPU
+                  restatement of the reference step) timed on a bounded sample
+                  on this host (rank 0, N = 1 only).
+For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "seq2seq_abcd-vae_amd"))
+
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (dense, spec)
+
+CONFIGS = {
+    "c2": dict(workload="abcd-lstm synthetic 10k segments, T_max=200, F=129, K=128, h=256, b=512/GPU",
+               F=129, H=256, Hm=256, D=256, K=128, rnn="LSTM", plain=False, tmin=50, tmax=200, B=512, N=10000,
+               spk=0, sdim=None),
+    "c4": dict(workload="plain gaussian-vae lstm, T_max=200, F=129, f=16, h=256, b=512/GPU",
+               F=129, H=256, Hm=256, D=16, K=0, rnn="LSTM", plain=True, tmin=50, tmax=200, B=512, N=10000,
+               spk=0, sdim=None),
+    "c5": dict(workload="abcd-lstm stress K=1024, speaker_dim=256 (16 spk), T_max=512, F=129, h=256, b=512/GPU",
+               F=129, H=256, Hm=256, D=256, K=1024, rnn="LSTM", plain=False, tmin=128, tmax=512, B=512,
+               N=10000, spk=16, sdim=256),
+    "c5gru": dict(workload="abcd-gru stress K=1024, speaker_dim=256 (16 spk), T_max=512, F=129, h=256, b=512/GPU",
+                  F=129, H=256, Hm=256, D=256, K=1024, rnn="GRU", plain=False, tmin=128, tmax=512, B=512,
+                  N=10000, spk=16, sdim=256),
+}
+
+
+def flops_per_step(cfg, L, B):
+    """Algorithmic GEMM FLOPs of one training step: 3 x forward."""
+    F, H, Hm, D, K = cfg["F"], cfg["H"], cfg["Hm"], cfg["D"], cfg["K"]
+    G = 4 if cfg["rnn"] == "LSTM" else 3
+    enc = 2 * 2 * (F + H) * G * H
+    dec = 2 * (F + H) * G * H + 2 * (2 * H * Hm + 2 * Hm * F) + (2 * H * Hm + 2 * Hm)
+    E = 4 * H if cfg["rnn"] == "LSTM" else 2 * H
+    Hdec = 2 * H if cfg["rnn"] == "LSTM" else H
+    S = cfg["sdim"] or 0
+    if cfg["plain"]:
+        seg = 2 * (2 * E * Hm + 2 * Hm * D) + 2 * (D + S) * Hdec
+    else:
+        seg = 2 * E * Hm + 2 * Hm * D + 2 * D * K + 2 * K * D + 2 * (D + S) * Hdec
+    return 3 * ((enc + dec) * L + seg * B)
+
+
+def recurrent_flops(cfg, L):
+    """FLOPs of the recurrent-step kernel family (encoder + decoder cell GEMMs,
+    forward and backward), per step of training."""
+    F, H, Hm = cfg["F"], cfg["H"], cfg["Hm"]
+    G = 4 if cfg["rnn"] == "LSTM" else 3
+    enc_rec = 2 * 2 * H * G * H  # both directions, h @ W_hh^T (fwd) / dG @ W_hh (bwd)
+    dec_cell = 2 * (F + H) * G * H  # [x | h] @ [W_ih | W_hh]^T
+    dec_bwd = 2 * (G * H + 2 * Hm) * H  # dG @ W_hh + dZ @ [W1_mu; W1_lv]
+    return (enc_rec + dec_cell + enc_rec + dec_bwd) * L
+
+
+def make_batch(cfg, seed, device):
+    g = torch.Generator().manual_seed(seed)
+    B, tmin, tmax = cfg["B"], cfg["tmin"], cfg["tmax"]
+    lens = torch.randint(tmin, tmax + 1, (B,), generator=g)
+    lens[0] = tmax
+    lens, _ = torch.sort(lens, descending=True)
+    T = int(lens[0])
+    bs = torch.tensor([int((lens > t).sum()) for t in range(T)], dtype=torch.int64)
+    L = int(bs.sum())
+    data = torch.randn(L, cfg["F"], generator=g)
+    is_off = torch.zeros(L)
+    off = 0
+    for t in range(T):
+        n = int(bs[t])
+        ends = (lens[:n] == t + 1).nonzero().flatten()
+        is_off[off + ends] = 1.0
+        off += n
+    spk = torch.randint(0, max(cfg["spk"], 1), (B,), generator=g)
+    return dict(data=data.to(device), batch_sizes=bs, is_offset=is_off.to(device), speakers=spk.to(device),
+                lengths=lens, L=L, T=T)
+
+
+def build(cfg, device):
+    from modules import model as M, engine
+    torch.manual_seed(1111)
+    enc = M.RNN_Variational_Encoder(cfg["F"], cfg["H"], rnn_type=cfg["rnn"])
+    if cfg["plain"]:
+        samp = M.Sampler(enc.hidden_size_total, cfg["Hm"], cfg["D"])
+    else:
+        samp = M.ABCDSampler(enc.hidden_size_total, cfg["Hm"], cfg["K"], cfg["D"])
+    dec = M.RNN_Variational_Decoder(cfg["F"], cfg["H"], cfg["Hm"], cfg["D"], rnn_type=cfg["rnn"],
+                                    num_speakers=cfg["spk"] or None, speaker_embed_dim=cfg["sdim"])
+    for m in (enc, samp, dec):
+        m.to(device).train()
+    return engine.FusedStep(enc, samp, dec, device)
+
+
+def cpu_baseline(cfg, budget_s=25.0):
+    """Time the CPU oracle on a bounded sample of the same workload."""
+    from oracle import abcd_oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    ocfg = O.default_cfg(F=cfg["F"], H=cfg["H"], Hdec=cfg["H"], Hm=cfg["Hm"], D=cfg["D"], K=cfg["K"] or 16,
+                         rnn=cfg["rnn"], plain=cfg["plain"], fplain=cfg["D"])
+    P = O.init_params(ocfg, 1111)
+    b = 64
+    sub = dict(cfg, B=b)
+    batch = make_batch(sub, 4321, "cpu")
+    bsz = batch["batch_sizes"]
+    feat = torch.randn(b, cfg["D"]) if cfg["plain"] else -torch.empty(b, cfg["K"]).exponential_().log()
+    eps = torch.randn(batch["L"], cfg["F"])
+    noise = dict(feat=feat, eps=eps)
+    steps, t_total = 0, 0.0
+    while steps < 3:
+        t0 = time.perf_counter()
+        O.train_step(P, dict(data=batch["data"], batch_sizes=bsz, is_offset=batch["is_offset"]), ocfg, noise,
+                     cfg["N"])
+        t_total += time.perf_counter() - t0
+        steps += 1
+        if t_total > budget_s:
+            break
+    return {"value": round(steps * b / t_total, 3), "unit": "segments/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} oracle train steps of b={b} segments (T_max={cfg['tmax']}, L={batch['L']} frames) "
+                      f"of the {cfg['workload']} workload, torch-CPU fp32, {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batches", type=int, default=4, help="distinct synthetic batches cycled per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from modules import noise, parallel, engine as E
+    noise.set_mode("philox")
+    noise.manual_seed(1234 + rank)
+    step = build(cfg, device)
+    if world > 1:
+        parallel.broadcast_parameters(step)
+        parallel.attach(step)
+    batches = [make_batch(cfg, 1000 * rank + i, device) for i in range(args.batches)]
+    lr, clip = 1.0, 1.0
+
+    def run(i):
+        b = batches[i % len(batches)]
+        step.step(b["data"], b["batch_sizes"], b["is_offset"], b["speakers"], cfg["N"], is_pretraining=False,
+                  lr=lr, momentum=0.0, clip=clip)
+
+    for i in range(args.warmup):
+        run(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    segs = world * cfg["B"] * args.steps
+    value = segs / elapsed
+    ms = elapsed / args.steps * 1e3
+    Ls = [b["L"] for b in batches]
+    L_avg = sum(Ls[i % len(Ls)] for i in range(args.steps)) / args.steps
+    fl = flops_per_step(cfg, L_avg, cfg["B"])
+    loss = float(step.scalars[E.LOSS])
+    out = {
+        "metric": "segments/sec/node (fwd+bwd), batch=512 K=128 h=256; recon-loss delta vs ref",
+        "value": round(value, 2), "unit": "segments/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random STFT-shaped segments, random-init weights)",
+        "config": {"workload": cfg["workload"], "global_batch": world * cfg["B"], "seq_len": cfg["tmax"],
+                   "n_fft_bins": cfg["F"], "K": cfg["K"], "hidden": cfg["H"], "frames_per_batch_avg": L_avg,
+                   "parallelism": f"dp{world}", "noise": "philox in-kernel", "final_loss": round(loss, 4)},
+        "step_tflops": round(fl / (elapsed / args.steps) / 1e12, 3),
+    }
+    if not args.no_kernel_timing:
+        out["roofline"] = kernel_roofline(step, batches, cfg, run)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def kernel_roofline(step, batches, cfg, run):
+    """Dominant kernel family = the per-time-step recurrent kernels.  Their
+    device time is measured live with HIP events recorded by the library
+    around every launch of the family (abcd_timing_*), over the same steps."""
+    from modules import _native as N
+    lib = N.lib()
+    if not hasattr(lib, "abcd_timing_enable"):
+        return None
+    nsteps = 3
+    lib.abcd_timing_reset()
+    lib.abcd_timing_enable(1)
+    for i in range(nsteps):
+        run(i)
+    torch.cuda.synchronize()
+    lib.abcd_timing_enable(0)
+    res = (N.c_double * 4)()
+    lib.abcd_timing_read(res)
+    total_ms, launches = res[0], res[1]
+    Ls = sum(batches[i % len(batches)]["L"] for i in range(nsteps))
+    fl = recurrent_flops(cfg, Ls)
+    per_launch_flops = fl / max(launches, 1)
+    avg_s = total_ms / 1e3 / max(launches, 1)
+    achieved = per_launch_flops / avg_s / 1e12
+    return {"bound": "mfma", "kernel": "rnn_fwd_step/rnn_bwd_step (recurrent cell GEMM + fused cell)",
+            "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+            "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(launches),
+            "flops_per_launch": round(per_launch_flops)}
+
+
+if __name__ == "__main__":
+    main()

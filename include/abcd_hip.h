@@ -206,6 +206,12 @@ int abcd_linear(int M, int N, int K, const float* x, long ldx, const float* W, l
                 float* y, long ldy, void* ws, size_t ws_bytes, void* stream);
 /* n standard normals from Philox-4x32-10(seed, offset + i) */
 int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offset, void* stream);
+/* live device timing of the recurrent-step kernel family (encoder and decoder
+ * rnn_fwd_step / rnn_bwd_step): HIP events around every launch while enabled;
+ * read: out[0] = summed device ms, out[1] = number of launches */
+void abcd_timing_enable(int on);
+void abcd_timing_reset(void);
+int abcd_timing_read(double* out);
 /* library build identification (gfx target, version) */
 const char* abcd_version(void);
 

@@ -162,33 +162,53 @@ size_t gemm_scratch_floats_hint(int M, int N, int K) { return (size_t)M * N * 16
 
 // ---------------------------------------------------------------------------
 // column sums (bias gradients, GEMV-T): out[j] = beta*out[j] + sum_r w[r] Z[r][j]
-// pass 1: blockIdx.y = row slice, 256 threads over columns; pass 2 sums slices.
+// pass 1: block = 64 columns x 4 row groups over one row slice (coalesced
+// 256-B rows, 4 independent accumulators per thread); pass 2 sums the slices.
 // ---------------------------------------------------------------------------
-__global__ void colsum_pass1(const float* Z, long ldz, int nrows, int ncols, const float* w, int rows_per,
-                             float* part) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= ncols) return;
+__global__ __launch_bounds__(256) void colsum_pass1(const float* Z, long ldz, int nrows, int ncols, const float* w,
+                                                    int rows_per, float* part) {
+  __shared__ float sh[4][64];
+  const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cg;
   const int r0 = blockIdx.y * rows_per, r1 = min(nrows, r0 + rows_per);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += (w ? w[r] : 1.f) * Z[(long)r * ldz + j];
-  part[(long)blockIdx.y * ncols + j] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < ncols) {
+    int r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      s0 += (w ? w[r] : 1.f) * Z[(long)r * ldz + j];
+      s1 += (w ? w[r + 4] : 1.f) * Z[(long)(r + 4) * ldz + j];
+      s2 += (w ? w[r + 8] : 1.f) * Z[(long)(r + 8) * ldz + j];
+      s3 += (w ? w[r + 12] : 1.f) * Z[(long)(r + 12) * ldz + j];
+    }
+    for (; r < r1; r += 4) s0 += (w ? w[r] : 1.f) * Z[(long)r * ldz + j];
+  }
+  sh[rg][cg] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (rg == 0 && j < ncols) part[(long)blockIdx.y * ncols + j] = (sh[0][cg] + sh[1][cg]) + (sh[2][cg] + sh[3][cg]);
 }
 __global__ void colsum_pass2(const float* part, int nslices, int ncols, float* out, float beta) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= ncols) return;
-  float s = 0.f;
-  for (int z = 0; z < nslices; ++z) s += part[(long)z * ncols + j];
-  out[j] = (beta != 0.f ? beta * out[j] : 0.f) + s;
+  float s0 = 0.f, s1 = 0.f;
+  int z = 0;
+  for (; z + 1 < nslices; z += 2) {
+    s0 += part[(long)z * ncols + j];
+    s1 += part[(long)(z + 1) * ncols + j];
+  }
+  if (z < nslices) s0 += part[(long)z * ncols + j];
+  out[j] = (beta != 0.f ? beta * out[j] : 0.f) + (s0 + s1);
 }
 
 int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const float* w, float* out,
            float beta, float* scratch, size_t scratch_floats) {
   if (ncols <= 0) return 0;
-  int slices = std::max(1, std::min(cdiv(nrows, 64), 512));
+  const int cblocks = cdiv(ncols, 64);
+  int slices = std::max(1, std::min(cdiv(std::max(nrows, 1), 256), std::max(1, 1024 / cblocks)));
+  slices = std::min(slices, 256);
   slices = (int)std::max<long>(1, std::min<long>(slices, (long)(scratch_floats / (size_t)ncols)));
   const int rows_per = cdiv(std::max(nrows, 1), slices);
   slices = std::max(1, cdiv(std::max(nrows, 1), rows_per));
-  colsum_pass1<<<dim3(cdiv(ncols, 256), slices), 256, 0, s>>>(Z, ldz, nrows, ncols, w, rows_per, scratch);
+  colsum_pass1<<<dim3(cblocks, slices), 256, 0, s>>>(Z, ldz, nrows, ncols, w, rows_per, scratch);
   ABCD_CHECK_LAUNCH();
   colsum_pass2<<<cdiv(ncols, 256), 256, 0, s>>>(scratch, slices, ncols, out, beta);
   ABCD_CHECK_LAUNCH();

@@ -78,3 +78,16 @@ struct Arena {
 // checks PackedSequence.batch_sizes (host): non-increasing, sum L, first B
 int validate_batch(const int64_t* bs, int T, int L, int B);
 }  // namespace abcd
+
+namespace abcd {
+// Optional live timing of the recurrent-step kernel family (bench.py roofline):
+// when enabled, a HIP event pair brackets every launch inside TimedScope.
+bool timing_on();
+void timing_mark(hipStream_t s, bool begin);
+struct TimedScope {
+  hipStream_t s;
+  bool on;
+  explicit TimedScope(hipStream_t st) : s(st), on(timing_on()) { if (on) timing_mark(s, true); }
+  ~TimedScope() { if (on) timing_mark(s, false); }
+};
+}  // namespace abcd

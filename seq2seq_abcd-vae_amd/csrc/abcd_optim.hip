@@ -132,3 +132,45 @@ extern "C" int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offs
 }
 
 extern "C" const char* abcd_version(void) { return "abcd_hip 0.1 gfx950 fp32-mfma16x16x4"; }
+
+// ---------------------------------------------------------------------------
+// live kernel timing (bench.py): event pairs around recurrent-step launches
+// ---------------------------------------------------------------------------
+#include <vector>
+namespace abcd {
+struct TimingState {
+  bool on = false;
+  std::vector<hipEvent_t> ev;  // begin, end, begin, end, ...
+  size_t used = 0;
+};
+static TimingState g_timing;
+bool timing_on() { return g_timing.on; }
+void timing_mark(hipStream_t s, bool begin) {
+  (void)begin;
+  if (g_timing.used == g_timing.ev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) { g_timing.on = false; return; }
+    g_timing.ev.push_back(e);
+  }
+  (void)hipEventRecord(g_timing.ev[g_timing.used++], s);
+}
+}  // namespace abcd
+
+extern "C" void abcd_timing_enable(int on) { abcd::g_timing.on = on != 0; }
+extern "C" void abcd_timing_reset(void) { abcd::g_timing.used = 0; }
+/* out[0] = total device ms inside the timed launches, out[1] = launches */
+extern "C" int abcd_timing_read(double* out) {
+  using namespace abcd;
+  double tot = 0.0;
+  const size_t n = g_timing.used / 2;
+  if (n) ABCD_TRY(hipEventSynchronize(g_timing.ev[2 * n - 1]));
+  for (size_t i = 0; i < n; ++i) {
+    float ms = 0.f;
+    ABCD_TRY(hipEventElapsedTime(&ms, g_timing.ev[2 * i], g_timing.ev[2 * i + 1]));
+    tot += ms;
+  }
+  out[0] = tot;
+  out[1] = (double)n;
+  out[2] = out[3] = 0.0;
+  return 0;
+}

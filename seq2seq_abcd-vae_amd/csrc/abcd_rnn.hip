@@ -18,6 +18,7 @@
 // (4 waves, wave split-K) owns 16 rows x 16 units x G gates, so the LSTM/GRU
 // cell update runs in the GEMM epilogue out of LDS.
 #include <vector>
+#include <cstdlib>
 
 #include "abcd_common.h"
 #include "abcd_internal.h"
@@ -33,6 +34,18 @@ int validate_batch(const int64_t* bs, int T, int L, int B) {
     s += bs[t];
   }
   return s == L ? 0 : ABCD_EINVAL;
+}
+
+// diagnostic ablation mask for the recurrent step kernels (ABCD_DIAG env var,
+// timing experiments only; 0 in normal runs): 1 skip GEMM, 2 skip LDS reduce,
+// 4 skip epilogue
+static int diag_mask() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("ABCD_DIAG");
+    m = e ? atoi(e) : 0;
+  }
+  return m;
 }
 
 static std::vector<int> step_offsets(const int64_t* bs, int T) {
@@ -55,7 +68,7 @@ struct FwdDir {
   float* out; long ldo; int hcol, ccol;       // encoder final state (last_hidden)
   int off, bs, next_off, next_bs, tiles;
 };
-struct FwdArgs { FwdDir d[2]; int H; int nd; };
+struct FwdArgs { FwdDir d[2]; int H; int nd; int diag; };
 
 template <int G>
 __global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
@@ -69,6 +82,23 @@ __global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
   const int nut = H / 16;
   const int ut = blk % nut, rt = blk / nut;
+  // epilogue operands of this thread's (row, unit), fetched before the GEMM so
+  // their HBM latency overlaps the K loop
+  const int row = threadIdx.x >> 4, u = threadIdx.x & 15;
+  const int b = rt * 16 + row;
+  const bool live = b < D.bs;
+  const int unit = ut * 16 + u;
+  const long rr = D.off + (live ? b : 0);
+  const bool haspred = live && b < D.prev_valid;
+  float gxp[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    gxp[j] = 0.f;
+    if (live && D.GX) gxp[j] = D.GX[rr * D.ldgx + j * H + unit];
+    if (live && D.bih) gxp[j] += D.bih[j * H + unit];
+  }
+  const float cprev = (G == 4 && haspred) ? D.Cprev[rr * H + unit] : 0.f;
+  const float hprev = (G == 3 && haspred) ? D.Hprev[rr * H + unit] : 0.f;
   f4 accH[1][G], accX[1][G];
   acc_zero(accH);
   acc_zero(accX);
@@ -77,28 +107,23 @@ __global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
 #pragma unroll
   for (int j = 0; j < G; ++j) br[j] = j * H + ut * 16 + r;
   const int nchh = H / 16;
-  wave_mma<1, G>(accH, KC{D.Ah, H, D.prev_valid}, ar, KC{D.Whh, H, G * H}, br, w, nchh, 4, q);
-  if (D.xrows > 0)
+  if (!(a.diag & 1)) wave_mma<1, G>(accH, KC{D.Ah, H, D.prev_valid}, ar, KC{D.Whh, H, G * H}, br, w, nchh, 4, q);
+  if (D.xrows > 0 && !(a.diag & 1))
     wave_mma<1, G>(accX, KC{D.Ax, D.ldx, D.xrows}, ar, KC{D.Wih, D.ldwih, G * H}, br, first_chunk(w, nchh),
                    D.nchx, 4, q);
-  reduce_waves_to_lds<1, G>(accH, lds, w, lane);
-  reduce_waves_to_lds<1, G>(accX, lds + 4 * TSZ, w, lane);
+  if (!(a.diag & 2)) {
+    reduce_waves_to_lds<1, G>(accH, lds, w, lane);
+    reduce_waves_to_lds<1, G>(accX, lds + 4 * TSZ, w, lane);
+  }
   const float* tH = lds;
   const float* tX = lds + 4 * TSZ;
-  const int row = threadIdx.x >> 4, u = threadIdx.x & 15;
-  const int b = rt * 16 + row;
-  if (b >= D.bs) return;
-  const int unit = ut * 16 + u;
-  const long rr = D.off + b;
+  if (!live || (a.diag & 4)) return;
   float gx[G], gh[G];
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     gh[j] = tH[row * LD + j * 16 + u];
-    gx[j] = tX[row * LD + j * 16 + u];
-    if (D.GX) gx[j] += D.GX[rr * D.ldgx + j * H + unit];
-    if (D.bih) gx[j] += D.bih[j * H + unit];
+    gx[j] = tX[row * LD + j * 16 + u] + gxp[j];
   }
-  const bool haspred = b < D.prev_valid;
   float* Gr = D.Gst + rr * 4 * H;
   float h, c = 0.f;
   if (G == 4) {
@@ -106,8 +131,7 @@ __global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
     const float f_ = sigmoidf_(gx[1] + gh[1]);
     const float g_ = tanhf(gx[2] + gh[2]);
     const float o_ = sigmoidf_(gx[3] + gh[3]);
-    const float cp = haspred ? D.Cprev[rr * H + unit] : 0.f;
-    c = f_ * cp + i_ * g_;
+    c = f_ * cprev + i_ * g_;
     h = o_ * tanhf(c);
     Gr[unit] = i_; Gr[H + unit] = f_; Gr[2 * H + unit] = g_; Gr[3 * H + unit] = o_;
     D.Cst[rr * H + unit] = c;
@@ -118,8 +142,7 @@ __global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
     const float r_ = sigmoidf_(gx[0] + gh[0]);
     const float z_ = sigmoidf_(gx[1] + gh[1]);
     const float n_ = tanhf(gx[2] + r_ * gh[G - 1]);
-    const float hp = haspred ? D.Hprev[rr * H + unit] : 0.f;
-    h = (1.f - z_) * n_ + z_ * hp;
+    h = (1.f - z_) * n_ + z_ * hprev;
     Gr[unit] = r_; Gr[H + unit] = z_; Gr[2 * H + unit] = n_; Gr[3 * H + unit] = gh[G - 1];
     if (!haspred) D.Hprev[rr * H + unit] = 0.f;
   }
@@ -164,6 +187,41 @@ __global__ __launch_bounds__(256) void rnn_bwd_step(BwdArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
   const int nut = H / TN;
   const int ut = blk % nut, rt = blk / nut;
+  // epilogue operands (NR elements per thread), fetched before the GEMM
+  constexpr int EPT = (16 * TN) / 256;  // elements per thread
+  float pg[EPT][4], pc[EPT], pcp[EPT], pdc[EPT], pdh[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + 256 * k;
+    const int row = e / TN, cu = e % TN;
+    const int b = rt * 16 + row;
+    const bool live = b < D.bs;
+    const int unit = ut * TN + cu;
+    const long rr = D.off + (live ? b : 0);
+    const bool fin = b >= D.next_bs;
+    const bool haspred = live && b < D.prev_valid;
+    const float* Gr = D.Gst + rr * 4 * H;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pg[k][j] = live ? Gr[j * H + unit] : 0.f;
+    pc[k] = (live && G == 4) ? D.Cst[rr * H + unit] : 0.f;
+    pcp[k] = 0.f;
+    if (haspred) pcp[k] = G == 4 ? D.Cprev[rr * H + unit] : D.Hprev[rr * H + unit];
+    float dh = 0.f, dc = 0.f;
+    if (live) {
+      if (D.DHX) dh += D.DHX[rr * D.lddhx + unit];
+      if (fin) {
+        if (D.dlast) {
+          dh += D.dlast[(long)b * D.ldl + D.hcol + unit];
+          if (G == 4 && D.ccol >= 0) dc = D.dlast[(long)b * D.ldl + D.ccol + unit];
+        }
+      } else {
+        if (G == 4) dc = D.DC[rr * H + unit];
+        else dh += D.DC[rr * H + unit];
+      }
+    }
+    pdh[k] = dh;
+    pdc[k] = dc;
+  }
   f4 acc[1][NR];
   acc_zero(acc);
   const int ar[1] = {rt * 16 + r};
@@ -177,37 +235,29 @@ __global__ __launch_bounds__(256) void rnn_bwd_step(BwdArgs a) {
     wave_mma<1, NR>(acc, KC{D.Az, D.ldz, D.zrows}, ar, KC{D.W1T, D.ldz, H}, br, first_chunk(w, nchg), D.nchz, 4,
                     q);
   reduce_waves_to_lds<1, NR>(acc, lds, w, lane);
-  for (int e = threadIdx.x; e < 16 * TN; e += 256) {
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + 256 * k;
     const int row = e / TN, cu = e % TN;
     const int b = rt * 16 + row;
     if (b >= D.bs) continue;
     const int unit = ut * TN + cu;
     const long rr = D.off + b;
-    float dh = lds[row * LD + cu];
-    if (D.DHX) dh += D.DHX[rr * D.lddhx + unit];
-    const bool fin = b >= D.next_bs;
-    if (fin && D.dlast) dh += D.dlast[(long)b * D.ldl + D.hcol + unit];
     const bool haspred = b < D.prev_valid;
-    const float* Gr = D.Gst + rr * 4 * H;
+    const float dh = lds[row * LD + cu] + pdh[k];
     if (G == 4) {
-      float dcin = 0.f;
-      if (!fin) dcin = D.DC[rr * H + unit];
-      else if (D.dlast && D.ccol >= 0) dcin = D.dlast[(long)b * D.ldl + D.ccol + unit];
-      const float i_ = Gr[unit], f_ = Gr[H + unit], g_ = Gr[2 * H + unit], o_ = Gr[3 * H + unit];
-      const float c = D.Cst[rr * H + unit];
-      const float cp = haspred ? D.Cprev[rr * H + unit] : 0.f;
-      const float tc = tanhf(c);
-      const float dc = dcin + dh * o_ * (1.f - tc * tc);
+      const float i_ = pg[k][0], f_ = pg[k][1], g_ = pg[k][2], o_ = pg[k][3];
+      const float tc = tanhf(pc[k]);
+      const float dc = pdc[k] + dh * o_ * (1.f - tc * tc);
       float* dg = D.dGX + rr * GH;
       dg[unit] = dc * g_ * i_ * (1.f - i_);
-      dg[H + unit] = dc * cp * f_ * (1.f - f_);
+      dg[H + unit] = dc * pcp[k] * f_ * (1.f - f_);
       dg[2 * H + unit] = dc * i_ * (1.f - g_ * g_);
       dg[3 * H + unit] = dh * tc * o_ * (1.f - o_);
       if (haspred) D.DCpred[(long)(D.pred_off + b) * H + unit] = dc * f_;
     } else {
-      if (!fin) dh += D.DC[rr * H + unit];
-      const float r_ = Gr[unit], z_ = Gr[H + unit], n_ = Gr[2 * H + unit], ghn = Gr[3 * H + unit];
-      const float hp = haspred ? D.Hprev[rr * H + unit] : 0.f;
+      const float r_ = pg[k][0], z_ = pg[k][1], n_ = pg[k][2], ghn = pg[k][3];
+      const float hp = pcp[k];
       const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
       const float dzp = dh * (hp - n_) * z_ * (1.f - z_);
       const float drp = dnp * ghn * r_ * (1.f - r_);
@@ -342,10 +392,11 @@ extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encode
     const float* X = l == 0 ? w.Xp : w.Y[l - 1];
     ABCD_TRY((hipError_t)gemm(s, L, D * G * H, Inp, opKC(X, Inp, L), opKC(w.Wihp[l], Inp, D * G * H), w.GX,
                               (long)D * G * H, 1.f, 0.f, w.bcat[l], ACT_NONE, w.scratch, w.scratch_floats));
-    for (int i = 0; i < T; ++i) {
+    for (int i = 0; i < T && !(diag_mask() & 8); ++i) {
       FwdArgs a{};
       a.H = H;
       a.nd = D;
+      a.diag = diag_mask();
       for (int d = 0; d < D; ++d) {
         const bool rev = d == 1;
         const int t = rev ? T - 1 - i : i;
@@ -372,8 +423,11 @@ extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encode
         f.tiles = cdiv(f.bs, 16) * (H / 16);
       }
       const int grid = a.d[0].tiles + (D == 2 ? a.d[1].tiles : 0);
-      if (G == 4) rnn_fwd_step<4><<<grid, 256, 0, s>>>(a);
-      else rnn_fwd_step<3><<<grid, 256, 0, s>>>(a);
+      {
+        TimedScope ts(s);
+        if (G == 4) rnn_fwd_step<4><<<grid, 256, 0, s>>>(a);
+        else rnn_fwd_step<3><<<grid, 256, 0, s>>>(a);
+      }
       ABCD_CHECK_LAUNCH();
     }
   }
@@ -431,6 +485,7 @@ extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encod
         b.tiles = cdiv(b.bs, 16) * (H / TN);
       }
       const int grid = a.d[0].tiles + (D == 2 ? a.d[1].tiles : 0);
+      TimedScope ts(s);
       if (G == 4) ABCD_TRY((hipError_t)launch_bwd_step<4>(s, a, grid, H));
       else ABCD_TRY((hipError_t)launch_bwd_step<3>(s, a, grid, H));
     }
@@ -850,8 +905,11 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
     f.out = nullptr; f.ldo = 0; f.hcol = 0; f.ccol = 0;
     f.off = off[t]; f.bs = b_t; f.next_off = off[t + 1]; f.next_bs = nb;
     f.tiles = cdiv(b_t, 16) * (H / 16);
-    if (G == 4) rnn_fwd_step<4><<<f.tiles, 256, 0, s>>>(a);
-    else rnn_fwd_step<3><<<f.tiles, 256, 0, s>>>(a);
+    {
+      TimedScope ts(s);
+      if (G == 4) rnn_fwd_step<4><<<f.tiles, 256, 0, s>>>(a);
+      else rnn_fwd_step<3><<<f.tiles, 256, 0, s>>>(a);
+    }
     ABCD_CHECK_LAUNCH();
     ABCD_TRY((hipError_t)gemm(s, b_t, 2 * Hm, H, opKC(w.Hs + (size_t)off[t] * H, H, b_t), opKC(w.W1cat, H, 2 * Hm),
                               w.Aact + (size_t)off[t] * 2 * Hm, 2 * Hm, 1.f, 0.f, w.b1cat, ACT_TANH, nullptr, 0));
@@ -955,6 +1013,7 @@ extern "C" int abcd_decoder_backward(const abcd_decoder_cfg* c, const abcd_decod
     bd.DCpred = t > 0 ? w.DC : w.DC0; bd.pred_off = t > 0 ? off[t - 1] : 0;
     bd.off = off[t]; bd.bs = b_t; bd.prev_valid = b_t; bd.next_bs = nb;
     bd.tiles = cdiv(b_t, 16) * (H / TN);
+    TimedScope ts(s);
     if (G == 4) ABCD_TRY((hipError_t)launch_bwd_step<4>(s, a, bd.tiles, H));
     else ABCD_TRY((hipError_t)launch_bwd_step<3>(s, a, bd.tiles, H));
   }

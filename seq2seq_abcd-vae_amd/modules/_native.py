@@ -115,6 +115,9 @@ _SIGS = {
                              c_void_p, c_size_t, c_void_p]),
     "abcd_linear": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_void_p,
                             c_long, c_void_p, c_size_t, c_void_p]),
+    "abcd_timing_enable": (None, [c_int]),
+    "abcd_timing_reset": (None, []),
+    "abcd_timing_read": (c_int, [ctypes.POINTER(c_double)]),
     "abcd_fill_normal": (c_int, [c_void_p, c_long, c_uint64, c_uint64, c_void_p]),
 }
 EXPORTED = sorted(_SIGS)

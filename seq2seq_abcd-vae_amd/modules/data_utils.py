@@ -1,0 +1,186 @@
+# coding: utf-8
+"""Host-side data pipeline with the reference API (ABCD-VAE/modules/data_utils.py).
+
+CSV annotation + WAV -> STFT amplitude -> log(x + eps) / N -> length-sorted
+PackedSequence.  This is the hot path's INPUT CONTRACT:
+batches are popped from the END of the BatchSampler list, sorted by length
+(desc) inside the batch, and `is_offset` marks each segment's last frame.  The
+sampler draws from torch's global CPU generator exactly like the reference,
+so epoch/batch order matches a reference run with the same seed.
+
+Differences from the reference are compatibility fixes only (the reference
+targets PyTorch 1.2 / pandas 1.x): frame indices are kept as int, and
+`Tensor.stft` is called with `return_complex=True` and turned into the same
+real-pair amplitude.
+"""
+import os.path
+
+import numpy as np
+import pandas as pd
+import scipy.io.wavfile as spw
+import torch
+import torch.utils.data
+
+
+class Data_Parser(object):
+    """data_utils.py:10-57"""
+
+    def __init__(self, input_root, annotation_file, data_type_col_name="data_type", annotation_sep=",",
+                 speaker2ix=None):
+        self.df_annotation = pd.read_csv(annotation_file, sep=annotation_sep)
+        self.input_root = input_root
+        self.data_type_col_name = data_type_col_name
+        self.index_speakers(speaker2ix)
+
+    def index_speakers(self, speaker2ix):
+        if "speaker" in self.df_annotation.columns:
+            self.df_annotation["speaker"] = self.df_annotation["speaker"].astype(str)
+            if speaker2ix is None:
+                self.speaker2ix = {spk: ix for ix, spk in enumerate(self.df_annotation.speaker.unique())}
+            else:
+                self.speaker2ix = speaker2ix
+        else:
+            self.speaker2ix = None
+
+    def get_num_speakers(self):
+        return 0 if self.speaker2ix is None else len(self.speaker2ix)
+
+    def get_data(self, data_type=None, transform=None, channel=0):
+        if data_type is None:
+            sub_df = self.df_annotation.copy()
+        else:
+            sub_df = self.df_annotation[self.df_annotation[self.data_type_col_name] == data_type].copy()
+        return Dataset(sub_df, self.input_root, transform=transform, channel=channel, speaker2ix=self.speaker2ix)
+
+    def get_sample_freq(self, input_path=None):
+        if input_path is None:
+            input_path = self.df_annotation.loc[0, "input_path"]
+        fs, _ = spw.read(os.path.join(self.input_root, input_path))
+        return fs
+
+
+class Dataset(torch.utils.data.Dataset):
+    """data_utils.py:60-103"""
+
+    def __init__(self, df_annotation, input_root, transform=None, channel=0, speaker2ix=None):
+        self.df_annotation = df_annotation
+        self.input_root = input_root
+        self.transform = transform
+        self.channel = channel
+        self.speaker2ix = speaker2ix
+        self._wav_cache = {}
+        self.get_discrete_bounds()
+
+    def get_discrete_bounds(self):
+        onset = np.zeros(len(self.df_annotation), dtype=np.int64)
+        offset = np.zeros(len(self.df_annotation), dtype=np.int64)
+        pos = {ix: i for i, ix in enumerate(self.df_annotation.index)}
+        for input_path, sub_df in self.df_annotation.groupby("input_path"):
+            fs, _ = spw.read(os.path.join(self.input_root, input_path))
+            for ix, on, off in zip(sub_df.index, (sub_df.onset * fs).round(), (sub_df.offset * fs).round()):
+                onset[pos[ix]] = int(on)
+                offset[pos[ix]] = int(off)
+        self.df_annotation["onset_ix"] = onset
+        self.df_annotation["offset_ix"] = offset
+        self.df_annotation["length"] = offset - onset
+
+    def sort_indices_by_length(self, ixs):
+        return self.df_annotation.iloc[ixs, :].sort_values("length", ascending=False).index
+
+    def __len__(self):
+        return self.df_annotation.shape[0]
+
+    def _read(self, input_path):
+        # the reference re-reads the WAV for every item (data_utils.py:91); a per-file cache gives
+        # identical samples without the repeated I/O
+        if input_path not in self._wav_cache:
+            self._wav_cache[input_path] = spw.read(os.path.join(self.input_root, input_path))[1]
+        return self._wav_cache[input_path]
+
+    def __getitem__(self, ix):
+        row = self.df_annotation.loc[ix]
+        input_data = self._read(row["input_path"])
+        if input_data.ndim > 1:
+            input_data = input_data[:, self.channel]
+        input_data = input_data[int(row["onset_ix"]):int(row["offset_ix"])].astype(np.float32)
+        if self.speaker2ix is None:
+            speaker = float("nan")
+        else:
+            speaker = self.speaker2ix[row["speaker"]]
+        if self.transform:
+            input_data = self.transform(input_data)
+        return input_data, speaker
+
+
+class ToTensor(object):
+    def __call__(self, input_data):
+        return torch.from_numpy(input_data)
+
+
+class Transform(object):
+    def __init__(self, in_trans):
+        self.in_trans = in_trans
+
+    def __call__(self, input_data):
+        return self.in_trans(input_data)
+
+
+class STFT(object):
+    """data_utils.py:124-139: |STFT| with time as dim 0."""
+
+    def __init__(self, frame_length, step_size, window="hann_window", centering=True):
+        self.frame_length = frame_length
+        self.step_size = step_size
+        self.window = getattr(torch, window)(frame_length)
+        self.centering = centering
+
+    def __call__(self, input_data):
+        z = input_data.stft(self.frame_length, hop_length=self.step_size, window=self.window,
+                            center=self.centering, return_complex=True)
+        return torch.view_as_real(z).pow(2).sum(-1).sqrt().transpose(0, 1).contiguous()
+
+
+class Compose(object):
+    def __init__(self, transforms):
+        self.transforms = transforms
+
+    def __call__(self, data):
+        for trans in self.transforms:
+            data = trans(data)
+        return data
+
+
+class DataLoader(object):
+    """data_utils.py:150-185: yields (PackedSequence, packed is_offset, speakers, ixs)."""
+
+    def __init__(self, dataset, batch_size=1, shuffle=False):
+        self.dataset = dataset
+        self.shuffle = shuffle
+        if shuffle:
+            sampler = torch.utils.data.RandomSampler(self.dataset, replacement=False)
+        else:
+            sampler = torch.utils.data.SequentialSampler(self.dataset)
+        self.batch_sampler = torch.utils.data.BatchSampler(sampler, batch_size, drop_last=False)
+
+    def __iter__(self):
+        self.batches = list(self.batch_sampler)
+        return self
+
+    def __next__(self):
+        if not self.batches:
+            raise StopIteration
+        ixs = self.batches.pop()
+        ixs = self.dataset.sort_indices_by_length(ixs)
+        batched_input, speakers, is_offset = [], [], []
+        for ix in ixs:
+            seq, spk = self.dataset[ix]
+            batched_input.append(seq)
+            speakers.append(spk)
+            is_offset.append(torch.tensor([0.0] * (seq.size(0) - 1) + [1.0]))
+        batched_input = torch.nn.utils.rnn.pack_sequence(batched_input)
+        is_offset = torch.nn.utils.rnn.pack_sequence(is_offset)
+        speakers = torch.tensor(speakers)
+        return batched_input, is_offset, speakers, ixs
+
+    def get_num_batches(self):
+        return len(self.batch_sampler)
