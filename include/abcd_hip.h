@@ -212,6 +212,11 @@ int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offset, void* s
 void abcd_timing_enable(int on);
 void abcd_timing_reset(void);
 int abcd_timing_read(double* out);
+/* 0 if no persistent recurrent kernel has timed out waiting for its group
+ * since the last call (a timeout means the grid was not co-resident; the
+ * results of that launch are invalid).  Reads and clears the device word;
+ * synchronises the device.  Returns -1 on a HIP error. */
+int abcd_device_status(void);
 /* library build identification (gfx target, version) */
 const char* abcd_version(void);
 

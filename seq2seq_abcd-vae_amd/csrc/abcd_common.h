@@ -31,6 +31,10 @@ DEV f4 f4zero() { f4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
 
 DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 DEV float tanhf_(float x) { return tanhf(x); }
+// short-latency forms for the recurrent critical path (v_exp + v_rcp, ~1 ulp
+// each; tanh via 1 - 2/(1 + e^{2x}): absolute error ~1e-7 near 0)
+DEV float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+DEV float ftanh(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * x)); }
 
 // ---------------------------------------------------------------------------
 // operand views
@@ -174,4 +178,104 @@ DEV float philox_gumbel(uint64_t seed, uint64_t idx) {
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 inline int rup16(int x) { return (x + 15) & ~15; }
 
+}  // namespace abcd
+
+namespace abcd {
+// ---------------------------------------------------------------------------
+// "row-block" step GEMM: a workgroup owns 64 rows x NR*16 columns; each of its
+// 4 waves owns 16 rows over the FULL K (no wave split-K, so no LDS reduce and
+// the epilogue runs from the accumulator registers).  The B slice (NR*16 rows
+// of a weight matrix x K) is staged ONCE per workgroup into LDS in
+// fragment-major order -- [subtile j][chunk kc][lane] float4 -- so every B
+// fragment read is one conflict-free ds_read_b128 of 64 consecutive 16-B
+// slots; A rows stream from L2/HBM through a PD-deep register ring.
+// Two accumulator sets alternate by chunk parity so single-subtile tiles
+// still have two independent MFMA chains (16x16x4 f32: 32-cycle issue,
+// 40-cycle dependent latency).
+// ---------------------------------------------------------------------------
+
+// Fill LDS with B rows brow(j)+0..15 (j < nsub), chunks [0, nch), source
+// element (row, k) at W[row*ldw + k].  Global reads are row-contiguous
+// float4s (coalesced); LDS writes land in fragment order.
+template <class RowFn>
+DEV void stage_b_frag(f4* dst, const float* W, long ldw, int nsub, int nch, RowFn brow) {
+  // UNR loads in flight per thread before any LDS write: one memory round
+  // trip per UNR*256 float4s instead of one per 256 (the fill is latency-bound)
+  constexpr int UNR = 16;
+  const int total = nsub * 16 * nch * 4;  // float4s
+  for (int base = 0; base < total; base += UNR * 256) {
+    f4 v[UNR];
+    int dsti[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int e = base + u * 256 + threadIdx.x;
+      dsti[u] = -1;
+      if (e < total) {
+        const int q = e & 3;
+        const int kc = (e >> 2) % nch;
+        const int rowi = (e >> 2) / nch;  // 0 .. nsub*16-1
+        const int j = rowi >> 4, r = rowi & 15;
+        v[u] = *reinterpret_cast<const f4*>(W + (long)(brow(j) + r) * ldw + kc * 16 + 4 * q);
+        dsti[u] = (j * nch + kc) * 64 + q * 16 + r;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (dsti[u] >= 0) dst[dsti[u]] = v[u];
+  }
+}
+
+// acc[p][j] += A(row, k) * B_j(k) over chunks [0, nch) of one segment.
+// Bl: the segment's fragment-major LDS image ([j][kc][lane]).  REQUIRES
+// nch % PD == 0: the ring loop is then branch-free, so the compiler can wait
+// with `s_waitcnt vmcnt(PD-1)` for the oldest chunk instead of draining every
+// load (a guarded refill forces vmcnt(0) per chunk).
+template <int NR, int PD, class OA>
+DEV void wave_mma_lds(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q) {
+  f4 a[PD], b[NR];
+#pragma unroll
+  for (int p = 0; p < PD; ++p) a[p] = A.frag(arow, p, q);
+#pragma unroll
+  for (int j = 0; j < NR; ++j) b[j] = Bl[j * nch * 64 + lane];
+  // one chunk: LDS reads of the NEXT chunk's B fragments are issued before
+  // this chunk's MFMAs (their latency hides behind them); the A slot is
+  // refilled PD chunks ahead when `refill`
+  auto chunk = [&](int kc, int p, bool refill) {
+    const int kn = kc + 1 < nch ? kc + 1 : kc;
+    f4 bn[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) bn[j] = Bl[(j * nch + kn) * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) acc[p & 1][j] = mfma4(a[p][s], b[j][s], acc[p & 1][j]);
+    if (refill) a[p] = A.frag(arow, kc + PD, q);
+#pragma unroll
+    for (int j = 0; j < NR; ++j) b[j] = bn[j];
+    // keep each refill right behind its chunk's MFMAs (the scheduler would
+    // otherwise sink all refills to the end of the block)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int base = 0;
+  for (; base + PD < nch; base += PD) {
+#pragma unroll
+    for (int p = 0; p < PD; ++p) chunk(base + p, p, true);
+  }
+#pragma unroll
+  for (int p = 0; p < PD; ++p) chunk(base + p, p, false);
+}
+
+template <int NR>
+DEV void acc2_zero(f4 (&acc)[2][NR]) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[p][j] = f4zero();
+}
+template <int NR>
+DEV void acc2_fold(f4 (&acc)[2][NR]) {
+#pragma unroll
+  for (int j = 0; j < NR; ++j) acc[0][j] += acc[1][j];
+}
 }  // namespace abcd

@@ -1,0 +1,462 @@
+// abcd_persist.hip -- persistent recurrent kernels: the whole packed time loop
+// of one encoder layer (both directions) in ONE launch.
+//
+// Why: the per-step design of abcd_rnn.hip pays, at every one of the T steps,
+// a kernel boundary plus a re-staging of the recurrent weight slice and a
+// cold round trip for every operand -- ~15-20 us per step for ~2 us of MFMA
+// work at the ABCD-VAE sizes (H = 256, batch 512).  Here each workgroup owns a
+// fixed tile for the whole sequence:
+//   forward : 64 rows x 16 units x G gates.  W_hh's 16-unit slice (G*16 x H)
+//             is staged into LDS once; the cell state of the lane's 4 cells
+//             stays in registers across steps.
+//   backward: 64 rows x 16 units.  W_hh^T's 16-row slice (16 x G*H) in LDS;
+//             the carry (LSTM dc*f, GRU dh*z) stays in registers.
+// The only cross-workgroup dependency is the recurrent operand: step t's
+// 64-row block needs all H (forward) / G*H (backward) columns of the previous
+// step, produced by the NUT = H/16 workgroups of the same "group" (direction,
+// row tile).  Hand-off per step (MI355X_MICROARCH.md, visibility table row 1):
+// the payload is stored write-through (`sc1`), every storing wave drains
+// (`s_waitcnt vmcnt(0)`), a workgroup barrier, ONE lane adds 1 to the group's
+// counter (agent-scope atomic); the consumer's lane 0 polls the counter with
+// `sc1` loads, a workgroup barrier releases the other waves, and EVERY load
+// of the payload is an `sc1` buffer load (L1 bypass).  Stash rows are
+// distinct per step, so no buffer is ever rewritten inside a launch (no WAR).
+//
+// Residency: every workgroup of a group must be resident for the group to
+// progress, so the launcher checks grid <= CUs x occupancy and otherwise
+// declines (the caller runs the per-step kernels).  Spins are bounded; a
+// timeout sets abcd_device_status() and lets the grid drain.
+#include <mutex>
+#include <vector>
+#include <cstdlib>
+
+#include "abcd_common.h"
+#include "abcd_internal.h"
+#include "abcd_persist.h"
+
+namespace abcd {
+
+__device__ unsigned g_persist_status = 0;
+
+// ---------------------------------------------------------------------------
+// hand-off primitives
+// ---------------------------------------------------------------------------
+// The descriptor must live in SGPRs: its inputs are wave-uniform, but when
+// divergence analysis cannot prove it the compiler wraps every load in a
+// readfirstlane "waterfall" loop -- so make the uniformity explicit.
+DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
+}
+// K-contiguous operand read through a buffer resource with `sc1` (bypasses
+// this CU's L1, so it sees other workgroups' write-through stores); rows at
+// or beyond the resource's extent read as zero (hardware range check).
+struct BufKC {
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t ld_bytes;
+  DEV f4 frag(int row, int kc, int q) const {
+    const uint32_t o = (uint32_t)row * ld_bytes + (uint32_t)(kc * 16 + 4 * q) * 4u;
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
+  }
+};
+DEV void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// lane 0 of the workgroup polls until *cnt >= target (bounded), then the
+// barrier releases every wave
+DEV void group_wait(unsigned* cnt, unsigned target) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {
+        __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __syncthreads();
+}
+// every wave drains its stores, barrier, one lane signals
+DEV void group_publish(unsigned* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// diagnostics: thread 0 stamps s_memtime at the phase boundaries of step i
+#define PSTAMP(k)                                                                                   \
+  do {                                                                                              \
+    if (a.prof && threadIdx.x == 0) a.prof[((size_t)blockIdx.x * T + i) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+static unsigned long long* g_prof = nullptr;
+
+// Workgroup -> (group, member).  Members of a group get equal blockIdx % 8,
+// i.e. one XCD under round-robin dispatch (L2 locality; speed only -- the
+// protocol above does not depend on placement).
+DEV void group_role(int bid, int ngroups, int nmem, int& grp, int& mem) {
+  if (ngroups % 8 == 0) {
+    const int s = bid & 7, k = bid >> 3;
+    grp = s + 8 * (k / nmem);
+    mem = k % nmem;
+  } else {
+    grp = bid / nmem;
+    mem = bid % nmem;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// encoder forward: one launch per layer, both directions
+// ---------------------------------------------------------------------------
+template <int G, int PD>
+__global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  const int H = a.H, nut = H / 16, nch = H / 16, T = a.T;
+  int grp, mem;
+  group_role(blockIdx.x, a.nd * a.nrt, nut, grp, mem);
+  const int dir = grp / a.nrt, rt = grp % a.nrt;
+  const PFwdDir& D = a.d[dir];
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+  const int u0 = mem * 16, unit = u0 + r;
+  const int row0 = rt * PERSIST_ROWS + w * 16;  // this wave's first row inside a step
+  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  stage_b_frag(smem, D.Whh, H, G, nch, [&](int j) { return j * H + u0; });
+  float bh[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) bh[j] = (G == 3) ? D.bhh[j * H + unit] : 0.f;
+  __syncthreads();
+  float st[4] = {0.f, 0.f, 0.f, 0.f};  // c (LSTM) / h (GRU) of the lane's 4 cells
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = D.rev ? T - 1 - i : i;
+    const int o = off[t], bs = off[t + 1] - o;
+    int prev_valid, next_off, next_bs;
+    if (D.rev) {
+      prev_valid = t == T - 1 ? 0 : off[t + 2] - off[t + 1];
+      next_off = t >= 1 ? off[t - 1] : 0;
+      next_bs = t >= 1 ? bs : 0;
+    } else {
+      prev_valid = t == 0 ? 0 : bs;
+      next_off = off[t + 1];
+      next_bs = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+    }
+    PSTAMP(0);
+    // input projection of this step (independent of the recurrence: issued
+    // before the wait so its latency hides behind it)
+    float gxp[4][G];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      const bool live = b < bs;
+      const long rr = o + (live ? b : 0);
+#pragma unroll
+      for (int j = 0; j < G; ++j) gxp[g][j] = live ? D.GX[rr * D.ldgx + j * H + unit] : 0.f;
+    }
+    if (i > 0) group_wait(cnt, (unsigned)(nut * i));
+    PSTAMP(1);
+    f4 acc[2][G];
+    acc2_zero(acc);
+    if (row0 < bs && prev_valid > 0) {
+      const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u), (uint32_t)H * 4u};
+      wave_mma_lds<G, PD>(acc, A, row0 + r, smem, nch, lane, q);
+    }
+    acc2_fold(acc);
+    PSTAMP(2);
+    // pass 1: cell update and the hand-off store of h (write-through), then
+    // signal the group before any stash store is issued
+    float gv[4][4], hv[4], cv[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      const bool haspred = b < prev_valid;
+      if (G == 4) {
+        gv[g][0] = fsigmoid(gxp[g][0] + acc[0][0][g]);
+        gv[g][1] = fsigmoid(gxp[g][1] + acc[0][1][g]);
+        gv[g][2] = ftanh(gxp[g][2] + acc[0][2][g]);
+        gv[g][3] = fsigmoid(gxp[g][3] + acc[0][3][g]);
+        cv[g] = gv[g][1] * (haspred ? st[g] : 0.f) + gv[g][0] * gv[g][2];
+        hv[g] = gv[g][3] * ftanh(cv[g]);
+        st[g] = cv[g];
+      } else {
+        const float ghr = acc[0][0][g] + bh[0], ghz = acc[0][1][g] + bh[1], ghn = acc[0][2][g] + bh[2];
+        gv[g][0] = fsigmoid(gxp[g][0] + ghr);
+        gv[g][1] = fsigmoid(gxp[g][1] + ghz);
+        gv[g][2] = ftanh(gxp[g][2] + gv[g][0] * ghn);
+        gv[g][3] = ghn;
+        hv[g] = (1.f - gv[g][1]) * gv[g][2] + gv[g][1] * (haspred ? st[g] : 0.f);
+        cv[g] = 0.f;
+        st[g] = hv[g];
+      }
+      if (b < bs && b < next_bs) st_sc1(D.Hprev + (long)(next_off + b) * H + unit, hv[g]);
+    }
+    PSTAMP(3);
+    group_publish(cnt);
+    // pass 2: stashes for the backward pass and the outputs (plain stores,
+    // drained while the next step waits for its operand)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      if (b >= bs) continue;
+      const long rr = o + b;
+      const bool haspred = b < prev_valid;
+      float* Gr = D.Gst + rr * 4 * H;
+      Gr[unit] = gv[g][0]; Gr[H + unit] = gv[g][1]; Gr[2 * H + unit] = gv[g][2]; Gr[3 * H + unit] = gv[g][3];
+      if (G == 4) D.Cst[rr * H + unit] = cv[g];
+      if (!haspred) {
+        if (G == 4) D.Cprev[rr * H + unit] = 0.f;
+        D.Hprev[rr * H + unit] = 0.f;
+      }
+      D.Y[rr * D.ldy + unit] = hv[g];
+      if (b < next_bs) {
+        if (G == 4) D.Cprev[(long)(next_off + b) * H + unit] = cv[g];
+      } else if (D.out) {
+        D.out[(long)b * D.ldo + D.hcol + unit] = hv[g];
+        if (G == 4) D.out[(long)b * D.ldo + D.ccol + unit] = cv[g];
+      }
+    }
+    PSTAMP(4);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// encoder backward (BPTT): one launch per layer, both directions
+// ---------------------------------------------------------------------------
+template <int G, int PD>
+__global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  const int H = a.H, GH = G * H, nut = H / 16, nchg = GH / 16, T = a.T;
+  int grp, mem;
+  group_role(blockIdx.x, a.nd * a.nrt, nut, grp, mem);
+  const int dir = grp / a.nrt, rt = grp % a.nrt;
+  const PBwdDir& D = a.d[dir];
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+  const int u0 = mem * 16, unit = u0 + r;
+  const int row0 = rt * PERSIST_ROWS + w * 16;
+  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  stage_b_frag(smem, D.WhhT, GH, 1, nchg, [&](int) { return u0; });
+  __syncthreads();
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};  // LSTM dc*f / GRU dh*z flowing to the predecessor
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = D.rev ? i : T - 1 - i;
+    const int o = off[t], bs = off[t + 1] - o;
+    int succ_off, succ_valid, prev_valid;
+    if (!D.rev) {
+      succ_off = t + 1 < T ? off[t + 1] : 0;
+      succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+      prev_valid = t == 0 ? 0 : bs;
+    } else {
+      succ_off = t >= 1 ? off[t - 1] : 0;
+      succ_valid = t >= 1 ? bs : 0;
+      prev_valid = t == T - 1 ? 0 : off[t + 2] - off[t + 1];
+    }
+    PSTAMP(0);
+    // epilogue operands (forward stashes, upper-layer dh, final-state grads)
+    float pg[4][4], pc[4], pcp[4], pdh[4], pdc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      const bool live = b < bs;
+      const long rr = o + (live ? b : 0);
+      const bool fin = b >= succ_valid;
+      const bool haspred = live && b < prev_valid;
+      const float* Gr = D.Gst + rr * 4 * H;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pg[g][j] = live ? Gr[j * H + unit] : 0.f;
+      pc[g] = (live && G == 4) ? D.Cst[rr * H + unit] : 0.f;
+      pcp[g] = 0.f;
+      if (haspred) pcp[g] = G == 4 ? D.Cprev[rr * H + unit] : D.Hprev[rr * H + unit];
+      float dh = 0.f, dc = 0.f;
+      if (live) {
+        if (D.DHX) dh += D.DHX[rr * D.lddhx + unit];
+        if (fin && D.dlast) {
+          dh += D.dlast[(long)b * D.ldl + D.hcol + unit];
+          if (G == 4 && D.ccol >= 0) dc = D.dlast[(long)b * D.ldl + D.ccol + unit];
+        }
+      }
+      pdh[g] = dh;
+      pdc[g] = dc;
+    }
+    if (i > 0) group_wait(cnt, (unsigned)(nut * i));
+    PSTAMP(1);
+    f4 acc[2][1];
+    acc2_zero(acc);
+    if (row0 < bs && succ_valid > 0) {
+      const BufKC A{make_rsrc(D.dGH + (size_t)succ_off * GH, (uint32_t)succ_valid * GH * 4u), (uint32_t)GH * 4u};
+      wave_mma_lds<1, PD>(acc, A, row0 + r, smem, nchg, lane, q);
+    }
+    acc2_fold(acc);
+    PSTAMP(2);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      if (b >= bs) continue;
+      const long rr = o + b;
+      const bool fin = b >= succ_valid;
+      float dh = acc[0][0][g] + pdh[g];
+      if (G == 4) {
+        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
+        const float tc = ftanh(pc[g]);
+        const float dc = (fin ? pdc[g] : carry[g]) + dh * o_ * (1.f - tc * tc);
+        float* dg = D.dGX + rr * GH;
+        st_sc1(dg + unit, dc * g_ * i_ * (1.f - i_));
+        st_sc1(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_));
+        st_sc1(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_));
+        st_sc1(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_));
+        carry[g] = dc * f_;
+      } else {
+        if (!fin) dh += carry[g];
+        const float r_ = pg[g][0], z_ = pg[g][1], n_ = pg[g][2], ghn = pg[g][3];
+        const float hp = pcp[g];  // h_{t-1} of this cell (forward stash; 0 without predecessor)
+        const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
+        const float dzp = dh * (hp - n_) * z_ * (1.f - z_);
+        const float drp = dnp * ghn * r_ * (1.f - r_);
+        float* dx = D.dGX + rr * GH;
+        float* dhh = D.dGH + rr * GH;
+        dx[unit] = drp; dx[H + unit] = dzp; dx[2 * H + unit] = dnp;
+        st_sc1(dhh + unit, drp); st_sc1(dhh + H + unit, dzp); st_sc1(dhh + 2 * H + unit, dnp * r_);
+        carry[g] = dh * z_;
+      }
+    }
+    PSTAMP(3);
+    group_publish(cnt);
+    PSTAMP(4);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+bool persist_enabled() {
+  const char* v = getenv("ABCD_PERSIST");  // read per call: tests flip it in-process
+  return !(v && v[0] == '0');
+}
+
+int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst) {
+  constexpr int NSLOT = 32;
+  constexpr size_t SLOT = 64 * 1024;
+  static std::mutex mu;
+  static char* ring = nullptr;
+  static hipEvent_t ev[NSLOT];
+  static bool used[NSLOT];
+  static int next = 0;
+  const size_t bytes = off.size() * sizeof(int);
+  if (bytes > SLOT) return (int)hipErrorInvalidValue;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!ring) {
+    ABCD_TRY(hipHostMalloc((void**)&ring, SLOT * NSLOT, hipHostMallocDefault));
+    for (int k = 0; k < NSLOT; ++k) {
+      ABCD_TRY(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+      used[k] = false;
+    }
+  }
+  const int k = next;
+  next = (next + 1) % NSLOT;
+  if (used[k]) ABCD_TRY(hipEventSynchronize(ev[k]));  // the copy that last read this slot is done
+  std::copy(off.begin(), off.end(), (int*)(ring + k * SLOT));
+  ABCD_TRY(hipMemcpyAsync(dst, ring + k * SLOT, bytes, hipMemcpyHostToDevice, s));
+  ABCD_TRY(hipEventRecord(ev[k], s));
+  used[k] = true;
+  return 0;
+}
+
+template <class K>
+static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
+  *ok = false;
+  if (lds > 160 * 1024) return 0;
+  ABCD_TRY(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  int dev = 0, cus = 0, per = 0;
+  ABCD_TRY(hipGetDevice(&dev));
+  ABCD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  ABCD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kernel, 256, lds));
+  *ok = per > 0 && (long)grid <= (long)cus * per;
+  return 0;
+}
+
+// ring depth: the largest of 16 / 4 / 1 dividing the chunk count
+static int ring_depth(int nch) { return nch % 16 == 0 ? 16 : (nch % 4 == 0 ? 4 : 1); }
+
+template <int G, int PD>
+static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
+  const int grid = a.nd * a.nrt * (a.H / 16);
+  const size_t lds = (size_t)G * 16 * a.H * sizeof(float);
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD>, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(hipMemsetAsync(a.sync, 0, persist_sync_uints(a.nd, a.nrt * PERSIST_ROWS) * sizeof(unsigned), s));
+  PFwdArgs b = a;
+  b.prof = g_prof;
+  {
+    TimedScope ts(s);
+    enc_fwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
+  }
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+template <int G, int PD>
+static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
+  const int grid = a.nd * a.nrt * (a.H / 16);
+  const size_t lds = (size_t)16 * G * a.H * sizeof(float);
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(enc_bwd_persist<G, PD>, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(hipMemsetAsync(a.sync, 0, persist_sync_uints(a.nd, a.nrt * PERSIST_ROWS) * sizeof(unsigned), s));
+  PBwdArgs b = a;
+  b.prof = g_prof;
+  {
+    TimedScope ts(s);
+    enc_bwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
+  }
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+
+int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched) {
+  *launched = false;
+  if (!persist_enabled()) return 0;
+  const int pd = ring_depth(a.H / 16);
+  if (G == 4) {
+    if (pd == 16) return launch_fwd<4, 16>(s, a, launched);
+    if (pd == 4) return launch_fwd<4, 4>(s, a, launched);
+    return launch_fwd<4, 1>(s, a, launched);
+  }
+  if (pd == 16) return launch_fwd<3, 16>(s, a, launched);
+  if (pd == 4) return launch_fwd<3, 4>(s, a, launched);
+  return launch_fwd<3, 1>(s, a, launched);
+}
+
+int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
+  *launched = false;
+  if (!persist_enabled()) return 0;
+  const int pd = ring_depth(G * a.H / 16);
+  if (G == 4) {
+    if (pd == 16) return launch_bwd<4, 16>(s, a, launched);
+    if (pd == 4) return launch_bwd<4, 4>(s, a, launched);
+    return launch_bwd<4, 1>(s, a, launched);
+  }
+  if (pd == 16) return launch_bwd<3, 16>(s, a, launched);
+  if (pd == 4) return launch_bwd<3, 4>(s, a, launched);
+  return launch_bwd<3, 1>(s, a, launched);
+}
+
+}  // namespace abcd
+
+// diagnostics only (not in the public header): stamp buffer for the
+// persistent kernels, grid x T x 5 u64, or null to disable
+extern "C" void abcd_debug_persist_prof(unsigned long long* dev_buf) { abcd::g_prof = dev_buf; }
+
+// 0 = no persistent-kernel spin has timed out since the last call (reads and
+// clears the device word; synchronises the device)
+extern "C" int abcd_device_status(void) {
+  unsigned v = 0, z = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(abcd::g_persist_status), sizeof(v)) != hipSuccess) return -1;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(abcd::g_persist_status), &z, sizeof(z));
+  return (int)v;
+}

@@ -22,6 +22,7 @@
 
 #include "abcd_common.h"
 #include "abcd_internal.h"
+#include "abcd_persist.h"
 
 namespace abcd {
 
@@ -302,6 +303,8 @@ struct EncWS {
   float* dGH[ABCD_MAX_LAYERS][2];
   float* DC[ABCD_MAX_LAYERS][2];
   float* DHX[ABCD_MAX_LAYERS];
+  int* off;          // device copy of the step offsets (persistent kernels)
+  unsigned* sync;    // persistent-kernel group counters
   float* scratch;
   size_t scratch_floats;
 };
@@ -339,9 +342,10 @@ static EncWS carve_encoder(Arena& A, const abcd_encoder_cfg* c, int T, int L, in
     maxMN = std::max(maxMN, (size_t)G * H * std::max(In, H));
   }
   w.GX = A.f((size_t)L * D * G * H);
+  w.off = (int*)A.f((size_t)T + 1);
+  w.sync = (unsigned*)A.f(persist_sync_uints(D, B));
   w.scratch_floats = std::max(maxMN * 16, (size_t)1 << 20);
   w.scratch = A.f(w.scratch_floats);
-  (void)T; (void)B;
   return w;
 }
 
@@ -392,7 +396,28 @@ extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encode
     const float* X = l == 0 ? w.Xp : w.Y[l - 1];
     ABCD_TRY((hipError_t)gemm(s, L, D * G * H, Inp, opKC(X, Inp, L), opKC(w.Wihp[l], Inp, D * G * H), w.GX,
                               (long)D * G * H, 1.f, 0.f, w.bcat[l], ACT_NONE, w.scratch, w.scratch_floats));
-    for (int i = 0; i < T && !(diag_mask() & 8); ++i) {
+    bool done = false;
+    {
+      PFwdArgs pa{};
+      pa.H = H; pa.nd = D; pa.T = T; pa.nrt = cdiv(x->B, PERSIST_ROWS); pa.off = w.off; pa.sync = w.sync;
+      for (int d = 0; d < D; ++d) {
+        const abcd_rnn_w& W = p->w[l][d];
+        PFwdDir& f = pa.d[d];
+        f.Whh = W.w_hh;
+        f.GX = w.GX + (size_t)d * G * H; f.ldgx = (long)D * G * H;
+        f.bhh = G == 3 ? W.b_hh : nullptr;
+        f.Gst = w.Gst[l][d]; f.Cst = w.Cst[l][d];
+        f.Y = w.Y[l] + (size_t)d * H; f.ldy = (long)D * H;
+        f.Hprev = w.Hprev[l][d]; f.Cprev = w.Cprev[l][d];
+        f.out = last_hidden; f.ldo = E;
+        const int base = (l * D + d) * (G == 4 ? 2 * H : H);
+        f.hcol = base; f.ccol = G == 4 ? base + H : -1;
+        f.rev = d == 1;
+      }
+      if (l == 0 && persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+      ABCD_TRY((hipError_t)persist_encoder_fwd(s, G, pa, &done));
+    }
+    for (int i = 0; i < T && !done && !(diag_mask() & 8); ++i) {
       FwdArgs a{};
       a.H = H;
       a.nd = D;
@@ -453,7 +478,26 @@ extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encod
     const int In = l == 0 ? F : D * H;
     for (int d = 0; d < D; ++d)
       ABCD_TRY((hipError_t)pack2d(s, p->w[l][d].w_hh, H, H, GH, true, w.WhhT[l][d], GH, H, GH));
-    for (int i = 0; i < T; ++i) {
+    bool done = false;
+    {
+      PBwdArgs pa{};
+      pa.H = H; pa.nd = D; pa.T = T; pa.nrt = cdiv(x->B, PERSIST_ROWS); pa.off = w.off; pa.sync = w.sync;
+      for (int d = 0; d < D; ++d) {
+        PBwdDir& b = pa.d[d];
+        b.WhhT = w.WhhT[l][d];
+        b.DHX = l + 1 < c->layers ? w.DHX[l] + (size_t)d * H : nullptr;
+        b.lddhx = (long)D * H;
+        b.dlast = d_last_hidden; b.ldl = E;
+        const int base = (l * D + d) * (G == 4 ? 2 * H : H);
+        b.hcol = base; b.ccol = G == 4 ? base + H : -1;
+        b.Gst = w.Gst[l][d]; b.Cst = w.Cst[l][d]; b.Cprev = w.Cprev[l][d]; b.Hprev = w.Hprev[l][d];
+        b.dGX = w.dGX[l][d]; b.dGH = w.dGH[l][d];
+        b.rev = d == 1;
+      }
+      if (l == c->layers - 1 && persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+      ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done));
+    }
+    for (int i = 0; i < T && !done; ++i) {
       BwdArgs a{};
       a.H = H;
       a.nd = D;

@@ -1,0 +1,104 @@
+"""Persistent recurrent kernels (abcd_persist.hip): the whole encoder time loop
+in one launch per layer, workgroups handing the recurrent state to each other
+inside the launch.
+
+* against torch.nn.LSTM/GRU in float64 on the CPU (the op the reference's
+  encoder is, ABCD-VAE/modules/model.py:53,60-66) on ragged packed batches
+  whose row-tile count is not a multiple of 8 (the non-XCD group mapping);
+* against the per-step kernels (ABCD_PERSIST=0) at the benchmark size
+  (H=256, batch 512, T=200: 16 groups of 16 workgroups, XCD-aware mapping);
+* every run ends with abcd_device_status() == 0 (no hand-off wait timed out).
+"""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _enc(F, H, rnn, layers, bidir, seed):
+    from modules import model as M
+    torch.manual_seed(seed)
+    return M.RNN_Variational_Encoder(F, H, rnn_type=rnn, rnn_layers=layers, bidirectional=bidir).cuda()
+
+
+def _batch(B, Tmax, F, seed):
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(1, Tmax + 1, (B,), generator=g)
+    lens[0] = Tmax
+    lens = lens.sort(descending=True).values
+    seqs = [torch.randn(int(n), F, generator=g) for n in lens]
+    return torch.nn.utils.rnn.pack_sequence(seqs)
+
+
+def _run(enc, packed, dout, persist):
+    from modules import _native as Nn
+    old = os.environ.get("ABCD_PERSIST")
+    os.environ["ABCD_PERSIST"] = "1" if persist else "0"
+    try:
+        data = packed.data.cuda()
+        for p in enc.parameters():
+            p.grad = None
+        out = enc(torch.nn.utils.rnn.PackedSequence(data, packed.batch_sizes))
+        (out * dout).sum().backward()
+        torch.cuda.synchronize()
+        assert Nn.lib().abcd_device_status() == 0
+        return out.detach().cpu().double(), {n: p.grad.detach().cpu().double() for n, p in enc.rnn.named_parameters()}
+    finally:
+        if old is None:
+            os.environ.pop("ABCD_PERSIST", None)
+        else:
+            os.environ["ABCD_PERSIST"] = old
+
+
+def _torch_ref(enc, packed, dout):
+    rnn = enc.rnn
+    cls = torch.nn.LSTM if rnn.mode == "LSTM" else torch.nn.GRU
+    ref = cls(rnn.input_size, rnn.hidden_size, rnn.num_layers, bidirectional=rnn.bidirectional,
+              batch_first=True).double()
+    with torch.no_grad():
+        for n, p in ref.named_parameters():
+            p.copy_(getattr(rnn, n).detach().cpu().double())
+    _, hn = ref(torch.nn.utils.rnn.PackedSequence(packed.data.double(), packed.batch_sizes))
+    if rnn.mode == "LSTM":
+        hn = torch.cat(hn, dim=-1)
+    out = hn.transpose(0, 1).contiguous().view(hn.shape[1], -1)
+    (out * dout.cpu().double()).sum().backward()
+    return out.detach(), {n: p.grad for n, p in ref.named_parameters()}
+
+
+def _rel(a, b):
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("rnn,layers,bidir", [("LSTM", 1, True), ("GRU", 1, True), ("LSTM", 2, True),
+                                              ("LSTM", 1, False), ("GRU", 2, False)])
+def test_persistent_encoder_vs_torch_f64(rnn, layers, bidir):
+    F, H, B, Tmax = 33, 64, 150, 40
+    enc = _enc(F, H, rnn, layers, bidir, seed=7)
+    packed = _batch(B, Tmax, F, seed=11)
+    dout = torch.randn(B, enc.hidden_size_total, device="cuda")
+    out, grads = _run(enc, packed, dout, persist=True)
+    rout, rgrads = _torch_ref(enc, packed, dout)
+    assert _rel(out, rout) < 1e-5
+    for n, g in rgrads.items():
+        assert _rel(grads[n], g) < 1e-4, n
+
+
+@pytest.mark.parametrize("rnn", ["LSTM", "GRU"])
+def test_persistent_encoder_vs_stepwise_bench_size(rnn):
+    F, H, B, Tmax = 129, 256, 512, 200
+    enc = _enc(F, H, rnn, 1, True, seed=3)
+    packed = _batch(B, Tmax, F, seed=5)
+    dout = torch.randn(B, enc.hidden_size_total, device="cuda")
+    out_p, g_p = _run(enc, packed, dout, persist=True)
+    out_s, g_s = _run(enc, packed, dout, persist=False)
+    assert _rel(out_p, out_s) < 1e-5
+    for n in g_s:
+        assert _rel(g_p[n], g_s[n]) < 1e-4, n
+    # repeated launches reuse the zeroed counters: identical results
+    out_p2, g_p2 = _run(enc, packed, dout, persist=True)
+    assert torch.equal(out_p, out_p2)
+    for n in g_p:
+        assert torch.equal(g_p[n], g_p2[n]), n
