@@ -194,11 +194,11 @@ namespace abcd {
 // 40-cycle dependent latency).
 // ---------------------------------------------------------------------------
 
-// Fill LDS with B rows brow(j)+0..15 (j < nsub), chunks [0, nch), source
-// element (row, k) at W[row*ldw + k].  Global reads are row-contiguous
-// float4s (coalesced); LDS writes land in fragment order.
+// Fill LDS with the B rows rowfn(j, r) (subtile j < nsub, r < 16), chunks
+// [0, nch), source element (row, k) at W[row*ldw + k].  Global reads are
+// row-contiguous float4s (coalesced); LDS writes land in fragment order.
 template <class RowFn>
-DEV void stage_b_frag(f4* dst, const float* W, long ldw, int nsub, int nch, RowFn brow) {
+DEV void stage_rows(f4* dst, const float* W, long ldw, int nsub, int nch, RowFn rowfn) {
   // UNR loads in flight per thread before any LDS write: one memory round
   // trip per UNR*256 float4s instead of one per 256 (the fill is latency-bound)
   constexpr int UNR = 16;
@@ -215,7 +215,7 @@ DEV void stage_b_frag(f4* dst, const float* W, long ldw, int nsub, int nch, RowF
         const int kc = (e >> 2) % nch;
         const int rowi = (e >> 2) / nch;  // 0 .. nsub*16-1
         const int j = rowi >> 4, r = rowi & 15;
-        v[u] = *reinterpret_cast<const f4*>(W + (long)(brow(j) + r) * ldw + kc * 16 + 4 * q);
+        v[u] = *reinterpret_cast<const f4*>(W + (long)rowfn(j, r) * ldw + kc * 16 + 4 * q);
         dsti[u] = (j * nch + kc) * 64 + q * 16 + r;
       }
     }
@@ -224,13 +224,21 @@ DEV void stage_b_frag(f4* dst, const float* W, long ldw, int nsub, int nch, RowF
       if (dsti[u] >= 0) dst[dsti[u]] = v[u];
   }
 }
+// rows brow(j) + 0..15
+template <class RowFn>
+DEV void stage_b_frag(f4* dst, const float* W, long ldw, int nsub, int nch, RowFn brow) {
+  stage_rows(dst, W, ldw, nsub, nch, [&](int j, int r) { return brow(j) + r; });
+}
 
 // acc[p][j] += A(row, k) * B_j(k) over chunks [0, nch) of one segment.
-// Bl: the segment's fragment-major LDS image ([j][kc][lane]).  REQUIRES
-// nch % PD == 0: the ring loop is then branch-free, so the compiler can wait
-// with `s_waitcnt vmcnt(PD-1)` for the oldest chunk instead of draining every
-// load (a guarded refill forces vmcnt(0) per chunk).
-template <int NR, int PD, class OA>
+// Bl: the segment's fragment-major LDS image ([j][kc][lane]).  The ring of PD
+// A chunks is refilled unconditionally (the loop is branch-free, so the
+// compiler waits with `s_waitcnt vmcnt(PD-1)` for the oldest chunk instead of
+// draining every load).  TAIL = false requires nch % PD == 0; TAIL = true
+// guards the MFMAs of a final partial block (uniform branches, which cost a
+// full drain there), so A must be readable up to chunk roundup(nch, PD)
+// (BufKC: range-checked).
+template <int NR, int PD, bool TAIL = false, class OA>
 DEV void wave_mma_lds(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q) {
   f4 a[PD], b[NR];
 #pragma unroll
@@ -263,7 +271,8 @@ DEV void wave_mma_lds(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int
     for (int p = 0; p < PD; ++p) chunk(base + p, p, true);
   }
 #pragma unroll
-  for (int p = 0; p < PD; ++p) chunk(base + p, p, false);
+  for (int p = 0; p < PD; ++p)
+    if (!TAIL || base + p < nch) chunk(base + p, p, false);
 }
 
 template <int NR>

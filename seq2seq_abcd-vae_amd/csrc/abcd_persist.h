@@ -49,6 +49,41 @@ struct PBwdArgs {
   unsigned long long* prof;
 };
 
+// Decoder forward (self-feedback LSTM, model.py:147-196): one launch for the
+// whole time loop; per step three phases handed off inside a row-tile group:
+//   cell : gates = Xin_t W_ih^T + Hprev_t W_hh^T + b  -> c, h (8 units / member)
+//   mlp  : Aact = tanh(h W1cat^T + b1cat)              (16 columns / member)
+//   emit : mu, lv = Aact W2^T + b2; x = mu + e^{lv/2} eps -> Xin_{t+1}
+struct PDecFwdArgs {
+  int H, Hm, F, Fp, T, nrt, feedback;
+  const int* off;
+  unsigned* sync;
+  unsigned long long* prof;
+  const float *Wih, *Whh, *bias;   // GH x Fp (padded), GH x H, GH (b_ih + b_hh)
+  const float *W1, *b1;            // 2Hm x H, 2Hm  ([mu; lv] first layers)
+  const float *W2m, *W2l, *b2m, *b2l;  // Fp x Hm (padded rows), Fp
+  const float* eps; uint64_t seed, offset;  // explicit noise (rows x F) or Philox stream
+  float *Xin, *Hprev, *Cprev, *Gst, *Cst, *Hs, *Aact, *MU, *LV, *OUT;
+};
+
+// Decoder backward (BPTT of the same loop), per step t = T-1 .. 0, three phases:
+//   P0: [dx_{t+1} | dh_rec] = dG_{t+1} [W_ih | W_hh]; dx -> dMU, dLV (+ emission NLL grads)
+//   P1: dZ = [dMU W2m | dLV W2l] * (1 - Aact^2)
+//   P2: dh = dZ W1cat + dh_rec + dh_offset -> LSTM cell backward -> dG_t
+struct PDecBwdArgs {
+  int H, Hm, F, Fp, T, nrt, feedback;
+  const int* off;
+  unsigned* sync;
+  unsigned long long* prof;
+  const float *WihT, *WhhT;        // Fp x GH (rows >= F zero), H x GH
+  const float *W2mT, *W2lT;        // Hm x Fp
+  const float* W1T;                // H x 2Hm
+  const float *Gst, *Cst, *Cprev, *MU, *LV, *OUT, *Aact, *DHO;
+  const float* Y;                  // target frames (rows x F)
+  const float* s_em;               // device scalar: d loss / d emission NLL
+  float *dG, *dMU, *dLV, *dZ, *DHR, *DC0;
+};
+
 constexpr int PERSIST_ROWS = 64;        // rows per workgroup
 constexpr int PERSIST_SYNC_STRIDE = 32;  // uints per counter (128 B)
 
@@ -64,6 +99,8 @@ int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst);
 // per-step kernels).  Returns 0 or a hipError_t.
 int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched);
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched);
+int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched);
+int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched);
 
 // ABCD_PERSIST=0 disables the persistent path (parity/timing comparisons).
 bool persist_enabled();

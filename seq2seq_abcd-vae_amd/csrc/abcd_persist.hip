@@ -62,6 +62,21 @@ struct BufKC {
     return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
   }
 };
+// Two K segments back to back (e.g. [x | h] of a recurrent cell): chunks
+// [0, n0) come from segment 0, [n0, ntot) from segment 1; chunks >= ntot read
+// zero without touching memory (offset past the descriptor's extent).
+struct BufKC2 {
+  __amdgpu_buffer_rsrc_t r0, r1;
+  uint32_t ld0, ld1;
+  int n0, ntot;
+  DEV f4 frag(int row, int kc, int q) const {
+    const bool s0 = kc < n0;
+    const int k = s0 ? kc : kc - n0;
+    uint32_t o = (uint32_t)row * (s0 ? ld0 : ld1) + (uint32_t)(k * 16 + 4 * q) * 4u;
+    if (kc >= ntot) o = 0x80000000u;
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(s0 ? r0 : r1, o, 0, 16));
+  }
+};
 DEV void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // lane 0 of the workgroup polls until *cnt >= target (bounded), then the
@@ -90,9 +105,10 @@ DEV void group_publish(unsigned* cnt) {
 // diagnostics: thread 0 stamps s_memtime at the phase boundaries of step i
 #define PSTAMP(k)                                                                                   \
   do {                                                                                              \
-    if (a.prof && threadIdx.x == 0) a.prof[((size_t)blockIdx.x * T + i) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (a.prof && threadIdx.x == 0) a.prof[((size_t)blockIdx.x * T + i) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 static unsigned long long* g_prof = nullptr;
+static int g_prof_mask = 0;  // 1 enc fwd, 2 enc bwd, 4 dec fwd, 8 dec bwd
 
 // Workgroup -> (group, member).  Members of a group get equal blockIdx % 8,
 // i.e. one XCD under round-robin dispatch (L2 locality; speed only -- the
@@ -329,6 +345,375 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
   }
 }
 
+
+// stage chunks [0, nseg) of W's rows into chunks [kc0, kc0 + nseg) of an
+// image with nch chunks per subtile
+template <class RowFn>
+DEV void stage_rows_seg(f4* dst, const float* W, long ldw, int nsub, int nseg, int kc0, int nch, RowFn rowfn) {
+  constexpr int UNR = 16;
+  const int total = nsub * 16 * nseg * 4;
+  for (int base = 0; base < total; base += UNR * 256) {
+    f4 v[UNR];
+    int dsti[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int e = base + u * 256 + threadIdx.x;
+      dsti[u] = -1;
+      if (e < total) {
+        const int q = e & 3, kc = (e >> 2) % nseg, rowi = (e >> 2) / nseg;
+        const int j = rowi >> 4, r = rowi & 15;
+        v[u] = *reinterpret_cast<const f4*>(W + (long)rowfn(j, r) * ldw + kc * 16 + 4 * q);
+        dsti[u] = (j * nch + kc0 + kc) * 64 + q * 16 + r;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (dsti[u] >= 0) dst[dsti[u]] = v[u];
+  }
+}
+
+// ring of 16 chunks; exact (drain-free) when nch is a multiple of 16
+template <int NR, class OA>
+DEV void mma16(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q) {
+  if (nch % 16 == 0) wave_mma_lds<NR, 16, false>(acc, A, arow, Bl, nch, lane, q);
+  else wave_mma_lds<NR, 16, true>(acc, A, arow, Bl, nch, lane, q);
+}
+
+// ---------------------------------------------------------------------------
+// decoder forward (LSTM): one launch for the whole time loop
+// ---------------------------------------------------------------------------
+// Group = 64-row tile, M = H/8 members.  Cell phase: member m owns units
+// [8m, 8m+8) x 4 gates as two 16-column subtiles [i|f] and [g|o]; lanes r and
+// r^8 swap their halves (one shuffle) so both hold all four gates of unit
+// 8m + (r&7) and run the cell update redundantly (identical results).
+// MLP / emit phases: 16-column tiles dealt round-robin over the members.
+// Phase hand-offs use the group counter: every member adds 1 after each of
+// the three phases; phase p of step i waits for M * (3i + p).
+__device__ __forceinline__ int dec_cell_row(int H, int u0, int j, int r) { return (2 * j + (r >> 3)) * H + u0 + (r & 7); }
+
+__global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
+  const int M = H / 8, nchx = a.feedback ? Fp / 16 : 0, nchh = H / 16, nchm = Hm / 16, nchc = nchx + nchh;
+  const int n1t = 2 * Hm / 16, n2t = Fp / 16;
+  int grp, mem;
+  group_role(blockIdx.x, a.nrt, M, grp, mem);
+  const int rt = grp;
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row0 = rt * PERSIST_ROWS + w * 16;
+  const int u0 = mem * 8, unit = u0 + (r & 7);
+  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  // LDS images
+  f4* BC = smem;                       // cell [x | h]  [2][nchc][64]
+  f4* B1 = BC + 2 * nchc * 64;          // mlp tiles     [k][nchh][64]
+  const int n1 = mem < n1t ? (n1t - 1 - mem) / M + 1 : 0;
+  f4* B2 = B1 + n1 * nchh * 64;         // emit tiles   [k][2][nchm][64]
+  const int n2 = mem < n2t ? (n2t - 1 - mem) / M + 1 : 0;
+  if (nchx) stage_rows_seg(BC, a.Wih, Fp, 2, nchx, 0, nchc, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+  stage_rows_seg(BC, a.Whh, H, 2, nchh, nchx, nchc, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+  for (int k = 0; k < n1; ++k) {
+    const int j1 = mem + k * M;
+    stage_b_frag(B1 + k * nchh * 64, a.W1, H, 1, nchh, [&](int) { return 16 * j1; });
+  }
+  for (int k = 0; k < n2; ++k) {
+    const int j2 = mem + k * M;
+    stage_b_frag(B2 + (2 * k) * nchm * 64, a.W2m, Hm, 1, nchm, [&](int) { return 16 * j2; });
+    stage_b_frag(B2 + (2 * k + 1) * nchm * 64, a.W2l, Hm, 1, nchm, [&](int) { return 16 * j2; });
+  }
+  const float bias0 = a.bias[dec_cell_row(H, u0, 0, r)], bias1 = a.bias[dec_cell_row(H, u0, 1, r)];
+  const bool lo = r < 8;
+  __syncthreads();
+  float cst[4] = {0.f, 0.f, 0.f, 0.f};
+  bool cinit = false;
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = i;
+    const int o = off[t], bs = off[t + 1] - o;
+    const int next_off = off[t + 1];
+    const int next_bs = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+    // ---------------- cell ----------------
+    if (!cinit) {  // c_0 from feature2hidden (dec_init wrote it to the stash rows of step 0)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        cst[g] = b < bs ? a.Cprev[(long)(o + b) * H + unit] : 0.f;
+      }
+      cinit = true;
+    }
+    if (i > 0) group_wait(cnt, (unsigned)(M * 3 * i));
+    PSTAMP(0);
+    f4 acc[2][2];
+    acc2_zero(acc);
+    if (row0 < bs) {
+      // [x_t | h_{t-1}] in one ring (x is zero at t = 0: empty descriptor)
+      const BufKC2 A{make_rsrc(a.Xin + (size_t)o * Fp, t > 0 ? (uint32_t)bs * Fp * 4u : 0u),
+                     make_rsrc(a.Hprev + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)Fp * 4u, (uint32_t)H * 4u,
+                     nchx, nchc};
+      mma16<2>(acc, A, row0 + r, BC, nchc, lane, q);
+    }
+    acc2_fold(acc);
+    float gi[4], gf[4], gg[4], go[4], hv[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float v0 = acc[0][0][g] + bias0, v1 = acc[0][1][g] + bias1;
+      const float w0 = __shfl_xor(v0, 8, 64), w1 = __shfl_xor(v1, 8, 64);
+      gi[g] = fsigmoid(lo ? v0 : w0);
+      gf[g] = fsigmoid(lo ? w0 : v0);
+      gg[g] = ftanh(lo ? v1 : w1);
+      go[g] = fsigmoid(lo ? w1 : v1);
+      cst[g] = gf[g] * cst[g] + gi[g] * gg[g];
+      hv[g] = go[g] * ftanh(cst[g]);
+      const int b = row0 + 4 * q + g;
+      if (b < bs) {
+        if (lo) st_sc1(a.Hs + (long)(o + b) * H + unit, hv[g]);                       // -> mlp
+        else if (b < next_bs) st_sc1(a.Hprev + (long)(next_off + b) * H + unit, hv[g]);  // -> next cell
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      if (b >= bs) continue;
+      const long rr = o + b;
+      float* Gr = a.Gst + rr * 4 * H;
+      if (lo) {
+        Gr[unit] = gi[g]; Gr[H + unit] = gf[g];
+        a.Cst[rr * H + unit] = cst[g];
+      } else {
+        Gr[2 * H + unit] = gg[g]; Gr[3 * H + unit] = go[g];
+        if (b < next_bs) a.Cprev[(long)(next_off + b) * H + unit] = cst[g];
+      }
+    }
+    // ---------------- mlp ----------------
+    group_wait(cnt, (unsigned)(M * (3 * i + 1)));
+    PSTAMP(2);
+    for (int k = 0; k < n1; ++k) {
+      const int j1 = mem + k * M;
+      f4 acc1[2][1];
+      acc2_zero(acc1);
+      if (row0 < bs) {
+        const BufKC Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
+        mma16<1>(acc1, Hs, row0 + r, B1 + k * nchh * 64, nchh, lane, q);
+      }
+      acc2_fold(acc1);
+      const int col = 16 * j1 + r;
+      const float bb = a.b1[col];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b < bs) st_sc1(a.Aact + (long)(o + b) * 2 * Hm + col, ftanh(acc1[0][0][g] + bb));
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(3);
+    // ---------------- emit ----------------
+    group_wait(cnt, (unsigned)(M * (3 * i + 2)));
+    PSTAMP(4);
+    for (int k = 0; k < n2; ++k) {
+      const int j2 = mem + k * M;
+      f4 am[2][1], al[2][1];
+      acc2_zero(am);
+      acc2_zero(al);
+      if (row0 < bs) {
+        const BufKC Am{make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u), (uint32_t)2 * Hm * 4u};
+        const BufKC Al{make_rsrc(a.Aact + (size_t)o * 2 * Hm + Hm, (uint32_t)(bs * 2 * Hm - Hm) * 4u),
+                       (uint32_t)2 * Hm * 4u};
+        mma16<1>(am, Am, row0 + r, B2 + (2 * k) * nchm * 64, nchm, lane, q);
+        mma16<1>(al, Al, row0 + r, B2 + (2 * k + 1) * nchm * 64, nchm, lane, q);
+      }
+      acc2_fold(am);
+      acc2_fold(al);
+      const int col = 16 * j2 + r;
+      const float bm = a.b2m[col], bl = a.b2l[col];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b >= bs) continue;
+        const long rr = o + b;
+        float mu = 0.f, lv = 0.f, x = 0.f;
+        if (col < F) {
+          mu = am[0][0][g] + bm;
+          lv = al[0][0][g] + bl;
+          const float e = a.eps ? a.eps[rr * F + col] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col);
+          x = mu + __expf(0.5f * lv) * e;
+        }
+        if (a.feedback && b < next_bs) st_sc1(a.Xin + (long)(next_off + b) * Fp + col, x);
+        a.MU[rr * Fp + col] = mu;
+        a.LV[rr * Fp + col] = lv;
+        a.OUT[rr * Fp + col] = x;
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(5);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// decoder backward (LSTM): one launch for the whole BPTT loop
+// ---------------------------------------------------------------------------
+// Group = 64-row tile, M = H/8 members (as the forward).  Tiles of 16 columns
+// dealt round-robin: P0 over Fp/16 + H/16 tiles, P1 over 2Hm/16, P2 over H/16
+// (member m < H/16 owns unit tile m for the whole loop, so the dc carry of its
+// cells stays in registers).
+__global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T, GH = 4 * H;
+  const int M = H / 8, nchg = GH / 16, nchx = Fp / 16, nchz = 2 * Hm / 16;
+  const int nFt = Fp / 16, n0t = nFt + H / 16, n1t = 2 * Hm / 16, n2t = H / 16;
+  int grp, mem;
+  group_role(blockIdx.x, a.nrt, M, grp, mem);
+  const int rt = grp;
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row0 = rt * PERSIST_ROWS + w * 16;
+  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  const int n0 = mem < n0t ? (n0t - 1 - mem) / M + 1 : 0;
+  const int n1 = mem < n1t ? (n1t - 1 - mem) / M + 1 : 0;
+  const bool own2 = mem < n2t;
+  f4* B0 = smem;                       // P0 tiles [k][nchg][64]
+  f4* B1 = B0 + n0 * nchg * 64;        // P1 tiles [k][nchx][64]
+  f4* B2 = B1 + n1 * nchx * 64;        // P2 tile  [nchz][64]
+  for (int k = 0; k < n0; ++k) {
+    const int j0 = mem + k * M;
+    if (j0 < nFt) stage_b_frag(B0 + k * nchg * 64, a.WihT, GH, 1, nchg, [&](int) { return 16 * j0; });
+    else stage_b_frag(B0 + k * nchg * 64, a.WhhT, GH, 1, nchg, [&](int) { return 16 * (j0 - nFt); });
+  }
+  for (int k = 0; k < n1; ++k) {
+    const int j1 = mem + k * M;
+    if (j1 < Hm / 16) stage_b_frag(B1 + k * nchx * 64, a.W2mT, Fp, 1, nchx, [&](int) { return 16 * j1; });
+    else stage_b_frag(B1 + k * nchx * 64, a.W2lT, Fp, 1, nchx, [&](int) { return 16 * (j1 - Hm / 16); });
+  }
+  if (own2) stage_b_frag(B2, a.W1T, 2 * Hm, 1, nchz, [&](int) { return 16 * mem; });
+  const float s_em = *a.s_em;
+  __syncthreads();
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = T - 1 - i;
+    const int o = off[t], bs = off[t + 1] - o;
+    const int succ_off = t + 1 < T ? off[t + 1] : 0;
+    const int succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+    // ---------------- P0: dG_{t+1} [W_ih | W_hh] ----------------
+    if (i > 0) group_wait(cnt, (unsigned)(M * 3 * i));
+    PSTAMP(0);
+    for (int k = 0; k < n0; ++k) {
+      const int j0 = mem + k * M;
+      const bool isx = j0 < nFt;
+      f4 acc[2][1];
+      acc2_zero(acc);
+      if (row0 < bs && succ_valid > 0 && (!isx || a.feedback)) {
+        const BufKC A{make_rsrc(a.dG + (size_t)succ_off * GH, (uint32_t)succ_valid * GH * 4u), (uint32_t)GH * 4u};
+        mma16<1>(acc, A, row0 + r, B0 + k * nchg * 64, nchg, lane, q);
+      }
+      acc2_fold(acc);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b >= bs) continue;
+        const long rr = o + b;
+        if (isx) {
+          const int col = 16 * j0 + r;
+          float dmu = 0.f, dlv = 0.f;
+          if (col < F) {
+            const float dx = acc[0][0][g];
+            const float mu = a.MU[rr * Fp + col], lv = a.LV[rr * Fp + col], ox = a.OUT[rr * Fp + col];
+            const float y = a.Y[rr * F + col];
+            const float iv = __expf(-lv), d = y - mu;
+            dmu = dx + s_em * (-d) * iv;
+            dlv = dx * 0.5f * (ox - mu) + s_em * 0.5f * (1.f - d * d * iv);
+          }
+          st_sc1(a.dMU + rr * Fp + col, dmu);
+          st_sc1(a.dLV + rr * Fp + col, dlv);
+        } else {
+          st_sc1(a.DHR + rr * H + 16 * (j0 - nFt) + r, acc[0][0][g]);
+        }
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(1);
+    // ---------------- P1: dZ ----------------
+    group_wait(cnt, (unsigned)(M * (3 * i + 1)));
+    PSTAMP(2);
+    for (int k = 0; k < n1; ++k) {
+      const int j1 = mem + k * M;
+      const bool ismu = j1 < Hm / 16;
+      f4 acc[2][1];
+      acc2_zero(acc);
+      if (row0 < bs) {
+        const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
+        mma16<1>(acc, A, row0 + r, B1 + k * nchx * 64, nchx, lane, q);
+      }
+      acc2_fold(acc);
+      const int col = 16 * j1 + r;  // column of [mu | lv] (2Hm)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b >= bs) continue;
+        const long rr = o + b;
+        const float z = a.Aact[rr * 2 * Hm + col];
+        st_sc1(a.dZ + rr * 2 * Hm + col, acc[0][0][g] * (1.f - z * z));
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(3);
+    // ---------------- P2: dh -> cell backward -> dG_t ----------------
+    // epilogue operands of the owned cells (plain: written by earlier launches)
+    const int unit = 16 * mem + r;
+    float pg[4][4], pc[4], pcp[4], pdho[4];
+    if (own2) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        const bool live = b < bs;
+        const long rr = o + (live ? b : 0);
+        const float* Gr = a.Gst + rr * 4 * H;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pg[g][j] = live ? Gr[j * H + unit] : 0.f;
+        pc[g] = live ? a.Cst[rr * H + unit] : 0.f;
+        pcp[g] = live ? a.Cprev[rr * H + unit] : 0.f;
+        pdho[g] = live ? a.DHO[rr * H + unit] : 0.f;
+      }
+    }
+    group_wait(cnt, (unsigned)(M * (3 * i + 2)));
+    PSTAMP(4);
+    if (own2) {
+      f4 acc[2][1];
+      acc2_zero(acc);
+      if (row0 < bs) {
+        const BufKC A{make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u), (uint32_t)2 * Hm * 4u};
+        mma16<1>(acc, A, row0 + r, B2, nchz, lane, q);
+      }
+      acc2_fold(acc);
+      const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.DHR + (size_t)o * H, (uint32_t)bs * H * 4u);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b >= bs) continue;
+        const long rr = o + b;
+        const bool fin = b >= succ_valid;
+        const float dhr = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rd, (uint32_t)(b * H + unit) * 4u, 0, 16));
+        const float dh = acc[0][0][g] + dhr + pdho[g];
+        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
+        const float tc = ftanh(pc[g]);
+        const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
+        float* dg = a.dG + rr * GH;
+        st_sc1(dg + unit, dc * g_ * i_ * (1.f - i_));
+        st_sc1(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_));
+        st_sc1(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_));
+        st_sc1(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_));
+        carry[g] = dc * f_;
+        if (t == 0) a.DC0[(long)b * H + unit] = dc * f_;
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(5);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -390,7 +775,7 @@ static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   if (!ok) return 0;
   ABCD_TRY(hipMemsetAsync(a.sync, 0, persist_sync_uints(a.nd, a.nrt * PERSIST_ROWS) * sizeof(unsigned), s));
   PFwdArgs b = a;
-  b.prof = g_prof;
+  b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
   {
     TimedScope ts(s);
     enc_fwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
@@ -408,7 +793,7 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   if (!ok) return 0;
   ABCD_TRY(hipMemsetAsync(a.sync, 0, persist_sync_uints(a.nd, a.nrt * PERSIST_ROWS) * sizeof(unsigned), s));
   PBwdArgs b = a;
-  b.prof = g_prof;
+  b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
     TimedScope ts(s);
     enc_bwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
@@ -446,11 +831,60 @@ int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched)
   return launch_bwd<3, 1>(s, a, launched);
 }
 
+
+int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {
+  *launched = false;
+  if (!persist_enabled() || G != 4 || a.H % 8) return 0;
+  const int M = a.H / 8, nchx = a.feedback ? a.Fp / 16 : 0, nchh = a.H / 16, nchm = a.Hm / 16;
+  const int n1 = cdiv(2 * a.Hm / 16, M), n2 = cdiv(a.Fp / 16, M);
+  const size_t lds = (size_t)64 * 16 * (2 * nchx + 2 * nchh + n1 * nchh + 2 * n2 * nchm);
+  const int grid = a.nrt * M;
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_persist, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(hipMemsetAsync(a.sync, 0, (size_t)a.nrt * PERSIST_SYNC_STRIDE * sizeof(unsigned), s));
+  PDecFwdArgs b = a;
+  b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
+  {
+    TimedScope ts(s);
+    dec_fwd_persist<<<grid, 256, lds, s>>>(b);
+  }
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+
+
+int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {
+  *launched = false;
+  if (!persist_enabled() || G != 4 || a.H % 8) return 0;
+  const int M = a.H / 8, nchg = 4 * a.H / 16, nchx = a.Fp / 16, nchz = 2 * a.Hm / 16;
+  const int n0 = cdiv(a.Fp / 16 + a.H / 16, M), n1 = cdiv(2 * a.Hm / 16, M);
+  const size_t lds = (size_t)64 * 16 * (n0 * nchg + n1 * nchx + nchz);
+  const int grid = a.nrt * M;
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_persist, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(hipMemsetAsync(a.sync, 0, (size_t)a.nrt * PERSIST_SYNC_STRIDE * sizeof(unsigned), s));
+  PDecBwdArgs b = a;
+  b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
+  {
+    TimedScope ts(s);
+    dec_bwd_persist<<<grid, 256, lds, s>>>(b);
+  }
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+
 }  // namespace abcd
 
 // diagnostics only (not in the public header): stamp buffer for the
-// persistent kernels, grid x T x 5 u64, or null to disable
-extern "C" void abcd_debug_persist_prof(unsigned long long* dev_buf) { abcd::g_prof = dev_buf; }
+// persistent kernels selected by mask, grid x T x 5 u64, or null to disable
+extern "C" void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask) {
+  abcd::g_prof = dev_buf;
+  abcd::g_prof_mask = mask;
+}
 
 // 0 = no persistent-kernel spin has timed out since the last call (reads and
 // clears the device word; synchronises the device)

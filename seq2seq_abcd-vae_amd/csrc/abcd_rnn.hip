@@ -831,6 +831,8 @@ struct DecWS {
   double* part;
   // backward
   float *dGX, *dGH, *DC, *DC0, *dH0, *dhid, *dFS, *DHO, *dMU, *dLV, *dZ, *dZo, *dlog_s;
+  int* off;          // device step offsets (persistent kernels)
+  unsigned* sync;    // persistent-kernel group counters
   float* scratch;
   size_t scratch_floats;
 };
@@ -873,9 +875,10 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
   w.dZo = A.f((size_t)L * Hm); w.dlog_s = A.f(L);
   size_t maxMN = std::max<size_t>({(size_t)GH * std::max(Fp, H), (size_t)Fp * Hm, (size_t)Hm * H,
                                    (size_t)Htot * DS, (size_t)L});
+  w.off = (int*)A.f((size_t)T + 1);
+  w.sync = (unsigned*)A.f(persist_sync_uints(1, B));
   w.scratch_floats = std::max(maxMN * 16, (size_t)1 << 20);
   w.scratch = A.f(w.scratch_floats);
-  (void)T;
   return w;
 }
 
@@ -933,8 +936,23 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
                             p->f2h_b, ACT_NONE, nullptr, 0));
   dec_init<<<launch_grid((long)B * std::max(H, Fp)), 256, 0, s>>>(w.Hinit, B, H, G == 4, w.Hprev, w.Cprev, w.Xin, Fp);
   ABCD_CHECK_LAUNCH();
-  // ---- time loop ----
-  for (int t = 0; t < T; ++t) {
+  // ---- time loop: one persistent launch, or one launch per phase and step ----
+  bool done = false;
+  {
+    PDecFwdArgs pa{};
+    pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS);
+    pa.feedback = c->feedback;
+    pa.off = w.off; pa.sync = w.sync;
+    pa.Wih = w.Wihp; pa.Whh = cw.w_hh; pa.bias = w.bcomb;
+    pa.W1 = w.W1cat; pa.b1 = w.b1cat;
+    pa.W2m = w.W2mp; pa.W2l = w.W2lp; pa.b2m = w.b2mp; pa.b2l = w.b2lp;
+    pa.eps = eps; pa.seed = seed; pa.offset = offset;
+    pa.Xin = w.Xin; pa.Hprev = w.Hprev; pa.Cprev = w.Cprev; pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Hs = w.Hs;
+    pa.Aact = w.Aact; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
+    if (persist_enabled() && G == 4) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+    ABCD_TRY((hipError_t)persist_decoder_fwd(s, G, pa, &done));
+  }
+  for (int t = 0; t < T && !done; ++t) {
     const int b_t = (int)bs[t];
     const int nb = t + 1 < T ? (int)bs[t + 1] : 0;
     FwdArgs a{};
@@ -1024,9 +1042,22 @@ extern "C" int abcd_decoder_backward(const abcd_decoder_cfg* c, const abcd_decod
   ABCD_CHECK_LAUNCH();
   ABCD_TRY((hipError_t)gemm(s, L, H, Hm, opKC(w.dZo, Hm, L), opKC(w.W1oT, Hm, H), w.DHO, H, 1.f, 0.f, nullptr,
                             ACT_NONE, sc, scf));
-  // ---- BPTT ----
+  // ---- BPTT: one persistent launch, or three launches per step ----
+  bool done = false;
+  {
+    PDecBwdArgs pa{};
+    pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS);
+    pa.feedback = c->feedback;
+    pa.off = w.off; pa.sync = w.sync;
+    pa.WihT = w.WihTp; pa.WhhT = w.WhhT; pa.W2mT = w.W2mT; pa.W2lT = w.W2lT; pa.W1T = w.W1catT;
+    pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Cprev = w.Cprev; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
+    pa.Aact = w.Aact; pa.DHO = w.DHO; pa.Y = x->data; pa.s_em = d_em;
+    pa.dG = w.dGX; pa.dMU = w.dMU; pa.dLV = w.dLV; pa.dZ = w.dZ; pa.DHR = w.DC; pa.DC0 = w.DC0;
+    if (persist_enabled() && G == 4) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+    ABCD_TRY((hipError_t)persist_decoder_bwd(s, G, pa, &done));
+  }
   const int TN = bwd_tn(H);
-  for (int t = T - 1; t >= 0; --t) {
+  for (int t = T - 1; t >= 0 && !done; --t) {
     const int b_t = (int)bs[t];
     const int nb = t + 1 < T ? (int)bs[t + 1] : 0;
     EmitBwdX e{};

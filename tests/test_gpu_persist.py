@@ -102,3 +102,45 @@ def test_persistent_encoder_vs_stepwise_bench_size(rnn):
     assert torch.equal(out_p, out_p2)
     for n in g_p:
         assert torch.equal(g_p[n], g_p2[n]), n
+
+
+def _fused_run(step, batch, persist, seed=77):
+    from modules import _native as Nn, noise
+    old = os.environ.get("ABCD_PERSIST")
+    os.environ["ABCD_PERSIST"] = "1" if persist else "0"
+    try:
+        noise.set_mode("philox")
+        noise.manual_seed(seed)
+        step.flat.grad.zero_()
+        sc, logits = step.forward_backward(batch["data"], batch["batch_sizes"], batch["is_offset"],
+                                           batch["speakers"], 10000)
+        torch.cuda.synchronize()
+        assert Nn.lib().abcd_device_status() == 0
+        return sc.detach().cpu().double().clone(), step.flat.grad.detach().cpu().double().clone()
+    finally:
+        if old is None:
+            os.environ.pop("ABCD_PERSIST", None)
+        else:
+            os.environ["ABCD_PERSIST"] = old
+
+
+ODD = dict(workload="odd shapes", F=33, H=48, Hm=32, D=32, K=16, rnn="LSTM", plain=False, tmin=3, tmax=30, B=100,
+           N=1000, spk=0, sdim=None)
+
+
+@pytest.mark.parametrize("cfg_name", ["c2", "c4", "odd"])
+def test_fused_step_persist_vs_stepwise_bench_size(cfg_name):
+    """Whole training step (encoder + sampler + decoder, forward + backward) at
+    the benchmark configuration: persistent kernels vs the per-step kernels;
+    "odd": K-chunk counts that are not multiples of the ring depth (H = 48,
+    Fp = 48), two row tiles with a ragged one."""
+    import bench
+    cfg = ODD if cfg_name == "odd" else bench.CONFIGS[cfg_name]
+    step = bench.build(cfg, "cuda")
+    batch = bench.make_batch(cfg, 0, "cuda")
+    sc_p, g_p = _fused_run(step, batch, True)
+    sc_s, g_s = _fused_run(step, batch, False)
+    # losses (EM, OFF, KL, LOSS) within 1e-5 relative; gradient vector within 1e-4 of its max
+    for k in range(4):
+        assert abs(sc_p[k] - sc_s[k]) <= 1e-5 * abs(sc_s[k]) + 1e-6, (k, sc_p[k].item(), sc_s[k].item())
+    assert _rel(g_p, g_s) < 1e-4
