@@ -199,6 +199,11 @@ int abcd_total_loss(const float* losses, const float* kl, int B, float* loss, vo
 /* C = A(MxK) @ B(NxK)^T (+bias[n]); row-major, plain GEMM used by tests */
 int abcd_gemm_nt(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
                  const float* bias, void* ws, size_t ws_bytes, void* stream);
+/* C = A^T @ B, A K x M (lda >= M), B K x N (ldb >= N), row-major: the
+ * weight-gradient GEMM (reduction over packed frames); ws enables split-K
+ * (>= 16 * M * N * 4 bytes recommended) */
+int abcd_gemm_tn(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C, long ldc,
+                 void* ws, size_t ws_bytes, void* stream);
 /* y = act(x @ W^T + b): nn.Linear (act 0) / Linear->Tanh (act 1); x M x K, W N x K.
  * Used by the standalone MLP modules (model.py:316-334) outside the training step;
  * ws >= (M + N) * roundup(K,16) * 4 bytes when K is not a multiple of 16. */

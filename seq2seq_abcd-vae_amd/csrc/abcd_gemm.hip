@@ -134,6 +134,145 @@ static int gemm_launch(hipStream_t s, int M, int N, int K, OA A, OB B, EpiArgs e
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// gemm_tn: C[m][n] = sum_k A[k*lda + m] * B[k*ldb + n] -- both operands
+// K-major, the weight-gradient shape (dW = dG^T X with K = all packed frames).
+// A 16-deep K slab of each operand is staged into LDS with coalesced 16-B row
+// loads (double-buffered; the next slab's global loads are in flight while the
+// current one feeds the MFMAs); fragments are read back with conflict-free
+// 4-B LDS reads (row pitch BM+4 / BN+4).  WG tile (32 MR) x (32 NR), 4 waves
+// as 2 x 2, each (16 MR) x (16 NR): at 256 x 256 one K slab is 32 KB of loads
+// for 8192 MFMA cycles per SIMD, so the kernel stays MFMA-bound with HBM
+// traffic ~2.5 TB/s (only MR = 4 is instantiated: larger accumulator arrays
+// are demoted to scratch by the compiler).  The grid splits K into fp32 slabs
+// (slab_reduce_kernel).
+// ---------------------------------------------------------------------------
+template <int MR, int NR>
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict__ A, long lda,
+                                                      const float* __restrict__ B, long ldb, int K, int kps,
+                                                      EpiArgs e) {
+  constexpr int BM = 32 * MR, BN = 32 * NR, BK = 16, LA = BM + 4, LB = BN + 4;
+  constexpr int AVT = BK * BM / 4, BVT = BK * BN / 4;   // f4 per slab
+  constexpr int AV = (AVT + 255) / 256, BV = (BVT + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float As[2][BK * LA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * LB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kb = blockIdx.z * kps, ke = min(K, kb + kps);
+  const int M = e.M, N = e.N;
+  f4 ra[AV], rb[BV];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int x = threadIdx.x + 256 * u, k = x / (BM / 4), m = (x % (BM / 4)) * 4;
+      ra[u] = (x < AVT && k0 + k < ke && m0 + m < M) ? *reinterpret_cast<const f4*>(A + (long)(k0 + k) * lda + m0 + m)
+                                                      : f4zero();
+    }
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      const int x = threadIdx.x + 256 * u, k = x / (BN / 4), n = (x % (BN / 4)) * 4;
+      rb[u] = (x < BVT && k0 + k < ke && n0 + n < N) ? *reinterpret_cast<const f4*>(B + (long)(k0 + k) * ldb + n0 + n)
+                                                      : f4zero();
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int x = threadIdx.x + 256 * u, k = x / (BM / 4), m = (x % (BM / 4)) * 4;
+      if (x < AVT) *reinterpret_cast<f4*>(&As[buf][k * LA + m]) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      const int x = threadIdx.x + 256 * u, k = x / (BN / 4), n = (x % (BN / 4)) * 4;
+      if (x < BVT) *reinterpret_cast<f4*>(&Bs[buf][k * LB + n]) = rb[u];
+    }
+  };
+  f4 acc[MR][NR];
+  acc_zero(acc);
+  gload(kb);
+  lstore(0);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) gload(k0 + BK);
+    const float* as = As[cur] + wm * 16 * MR + r;
+    const float* bs = Bs[cur] + wn * 16 * NR + r;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 4 * q + s;
+      float a[MR], b[NR];
+#pragma unroll
+      for (int i = 0; i < MR; ++i) a[i] = as[k * LA + 16 * i];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) b[j] = bs[k * LB + 16 * j];
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
+    }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int row = m0 + wm * 16 * MR + 16 * i + 4 * q + g, col = n0 + wn * 16 * NR + 16 * j + r;
+        if (row < M && col < N) {
+          if (e.slab)
+            e.slab[(long)blockIdx.z * M * N + (long)row * N + col] = acc[i][j][g];
+          else
+            e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, acc[i][j][g]);
+        }
+      }
+}
+
+template <int MR, int NR>
+static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                          EpiArgs e, float* scratch, size_t scratch_floats) {
+  const int BM = 32 * MR, BN = 32 * NR;
+  const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  int Z = std::max(1, std::min(cdiv(512, tiles), cdiv(K, 16 * 32)));
+  if (scratch) Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)M * N)));
+  else Z = 1;
+  Z = std::max(Z, 1);
+  const int kps = rup16(cdiv(K, Z));
+  Z = cdiv(K, kps);
+  EpiArgs ek = e;
+  if (Z > 1) ek.slab = scratch;
+  gemm_tn_kernel<MR, NR><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek);
+  ABCD_CHECK_LAUNCH();
+  if (Z > 1) {
+    const long n = (long)M * N;
+    slab_reduce_kernel<<<std::min<long>(2048, cdiv(n, 256)), 256, 0, s>>>(scratch, Z, e);
+    ABCD_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// both operands K-major with 16-B aligned rows covering roundup(M|N, 4).
+// Tile: 128 rows x 32*NR columns covering N up to 256 per tile.
+static int gemm_tn(hipStream_t s, int M, int N, int K, const Operand& A, const Operand& B, EpiArgs e,
+                   float* scratch, size_t scratch_floats) {
+  const int nr = std::min(8, cdiv(N, 32));
+#define TN_CASE(n) \
+  case n: return gemm_tn_launch<4, n>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+  switch (nr) {
+    TN_CASE(1) TN_CASE(2) TN_CASE(3) TN_CASE(4) TN_CASE(5) TN_CASE(6) TN_CASE(7)
+    default: return gemm_tn_launch<4, 8>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+  }
+#undef TN_CASE
+}
+static bool tn_ok(const Operand& o, int rows) {
+  return o.kmajor && o.ld % 4 == 0 && ((uintptr_t)o.p % 16) == 0 && o.ld >= ((rows + 3) & ~3);
+}
+
 int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, long ldc, float alpha,
          float beta, const float* bias, int act, float* scratch, size_t scratch_floats) {
   if (M <= 0 || N <= 0) return 0;
@@ -154,6 +293,8 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
   if (!A.kmajor && B.kmajor)
     return gemm_launch(s, M, N, K, KC{A.p, A.ld, std::min(A.nrows, M)}, KM{B.p, B.ld, std::min(B.nrows, N), K}, e,
                        scratch, scratch_floats);
+  if (K >= 512 && A.nrows >= M && B.nrows >= N && tn_ok(A, M) && tn_ok(B, N))
+    return gemm_tn(s, M, N, K, A, B, e, scratch, scratch_floats);
   return gemm_launch(s, M, N, K, KM{A.p, A.ld, std::min(A.nrows, M), K}, KM{B.p, B.ld, std::min(B.nrows, N), K},
                      e, scratch, scratch_floats);
 }
@@ -186,17 +327,28 @@ __global__ __launch_bounds__(256) void colsum_pass1(const float* Z, long ldz, in
   __syncthreads();
   if (rg == 0 && j < ncols) part[(long)blockIdx.y * ncols + j] = (sh[0][cg] + sh[1][cg]) + (sh[2][cg] + sh[3][cg]);
 }
-__global__ void colsum_pass2(const float* part, int nslices, int ncols, float* out, float beta) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= ncols) return;
-  float s0 = 0.f, s1 = 0.f;
-  int z = 0;
-  for (; z + 1 < nslices; z += 2) {
-    s0 += part[(long)z * ncols + j];
-    s1 += part[(long)(z + 1) * ncols + j];
+// pass 2: 64 columns x 4 slice groups per block, 4 independent accumulators
+// per thread (the slice count reaches 256: keep many loads in flight)
+__global__ __launch_bounds__(256) void colsum_pass2(const float* part, int nslices, int ncols, float* out,
+                                                    float beta) {
+  __shared__ float sh[4][64];
+  const int cg = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cg;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < ncols) {
+    int z = sg;
+    for (; z + 12 < nslices; z += 16) {
+      s0 += part[(long)z * ncols + j];
+      s1 += part[(long)(z + 4) * ncols + j];
+      s2 += part[(long)(z + 8) * ncols + j];
+      s3 += part[(long)(z + 12) * ncols + j];
+    }
+    for (; z < nslices; z += 4) s0 += part[(long)z * ncols + j];
   }
-  if (z < nslices) s0 += part[(long)z * ncols + j];
-  out[j] = (beta != 0.f ? beta * out[j] : 0.f) + (s0 + s1);
+  sh[sg][cg] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (sg == 0 && j < ncols)
+    out[j] = (beta != 0.f ? beta * out[j] : 0.f) + ((sh[0][cg] + sh[1][cg]) + (sh[2][cg] + sh[3][cg]));
 }
 
 int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const float* w, float* out,
@@ -210,7 +362,7 @@ int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const 
   slices = std::max(1, cdiv(std::max(nrows, 1), rows_per));
   colsum_pass1<<<dim3(cblocks, slices), 256, 0, s>>>(Z, ldz, nrows, ncols, w, rows_per, scratch);
   ABCD_CHECK_LAUNCH();
-  colsum_pass2<<<cdiv(ncols, 256), 256, 0, s>>>(scratch, slices, ncols, out, beta);
+  colsum_pass2<<<cdiv(ncols, 64), 256, 0, s>>>(scratch, slices, ncols, out, beta);
   ABCD_CHECK_LAUNCH();
   return 0;
 }
@@ -313,6 +465,16 @@ extern "C" int abcd_gemm_nt(int M, int N, int K, const float* A, long lda, const
   float* rest = Bp + (size_t)N * Kp;
   const size_t rest_f = ws_bytes / 4 - need;
   return gemm(s, M, N, Kp, opKC(Ap, Kp, M), opKC(Bp, Kp, N), C, ldc, 1.f, 0.f, bias, ACT_NONE, rest, rest_f);
+}
+
+// C ABI: C = A^T @ B with A (K x M, lda) and B (K x N, ldb) row-major: the
+// weight-gradient GEMM shape (reduction over rows); used by tests
+extern "C" int abcd_gemm_tn(int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C,
+                            long ldc, void* ws, size_t ws_bytes, void* stream) {
+  using namespace abcd;
+  if (M < 0 || N < 0 || K < 0 || !A || !B || !C || lda < M || ldb < N) return ABCD_EINVAL;
+  return gemm((hipStream_t)stream, M, N, K, opKM(A, lda, M), opKM(B, ldb, N), C, ldc, 1.f, 0.f, nullptr, ACT_NONE,
+              (float*)ws, ws_bytes / 4);
 }
 
 // C ABI: y = act(x @ W^T + b), act 0 = none, 1 = tanh (nn.Linear [+ Tanh]); any K

@@ -344,7 +344,7 @@ static EncWS carve_encoder(Arena& A, const abcd_encoder_cfg* c, int T, int L, in
   w.GX = A.f((size_t)L * D * G * H);
   w.off = (int*)A.f((size_t)T + 1);
   w.sync = (unsigned*)A.f(persist_sync_uints(D, B));
-  w.scratch_floats = std::max(maxMN * 16, (size_t)1 << 20);
+  w.scratch_floats = std::max(maxMN * 64, (size_t)1 << 20);  // split-K slabs of the wgrad GEMMs
   w.scratch = A.f(w.scratch_floats);
   return w;
 }
@@ -536,8 +536,8 @@ extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encod
     // weight gradients: reductions over all L packed frames (K = L, K-major operands)
     for (int d = 0; d < D; ++d) {
       const abcd_rnn_g& gr = g->g[l][d];
-      const float* X = l == 0 ? x->data : w.Y[l - 1];
-      const long ldxx = l == 0 ? F : (long)D * H;
+      const float* X = l == 0 ? w.Xp : w.Y[l - 1];  // Xp: the padded copy made by the forward
+      const long ldxx = l == 0 ? rup16(F) : (long)D * H;
       if (gr.w_ih)
         ABCD_TRY((hipError_t)gemm(s, GH, In, L, opKM(w.dGX[l][d], GH, GH), opKM(X, ldxx, In), gr.w_ih, In, 1.f, 0.f,
                                   nullptr, ACT_NONE, w.scratch, w.scratch_floats));
@@ -877,7 +877,7 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
                                    (size_t)Htot * DS, (size_t)L});
   w.off = (int*)A.f((size_t)T + 1);
   w.sync = (unsigned*)A.f(persist_sync_uints(1, B));
-  w.scratch_floats = std::max(maxMN * 16, (size_t)1 << 20);
+  w.scratch_floats = std::max(maxMN * 64, (size_t)1 << 20);  // split-K slabs of the wgrad GEMMs
   w.scratch = A.f(w.scratch_floats);
   return w;
 }

@@ -113,6 +113,8 @@ _SIGS = {
     "abcd_total_loss": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "abcd_gemm_nt": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p,
                              c_void_p, c_size_t, c_void_p]),
+    "abcd_gemm_tn": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p,
+                             c_size_t, c_void_p]),
     "abcd_linear": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_void_p,
                             c_long, c_void_p, c_size_t, c_void_p]),
     "abcd_timing_enable": (None, [c_int]),

@@ -23,6 +23,24 @@ def test_gemm_nt_vs_torch(M, N, K):
     assert err <= 1e-5 * K ** 0.5 * 4 + 1e-5, err
 
 
+@pytest.mark.parametrize("M,N,K,lda,ldb", [(1024, 256, 64045, 1024, 256), (1024, 129, 20000, 1024, 144),
+                                           (129, 256, 7001, 144, 512), (33, 48, 45, 48, 48), (256, 256, 513, 260, 256),
+                                           (1024, 1024, 4096, 1024, 1024)])
+def test_gemm_tn_vs_torch(M, N, K, lda, ldb):
+    """weight-gradient GEMM C = A^T B over K rows (LDS-staged K-major kernel for K >= 512)"""
+    from modules import _native as Nn
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn(K, lda, device="cuda", generator=g)
+    B = torch.randn(K, ldb, device="cuda", generator=g)
+    C = torch.empty(M, N, device="cuda")
+    ws = Nn.workspace(64 * M * N * 4 + (1 << 20), "cuda")
+    Nn.check(Nn.lib().abcd_gemm_tn(M, N, K, Nn.ptr(A), lda, Nn.ptr(B), ldb, Nn.ptr(C), N, Nn.ptr(ws), ws.numel(),
+                                   Nn.stream()), "gemm_tn")
+    ref = (A[:, :M].double().t() @ B[:, :N].double()).float()
+    err = (C - ref).abs().max().item()
+    assert err <= 2e-6 * K ** 0.5 * 4 + 1e-5, err
+
+
 def test_linear_tanh():
     from modules import _native as Nn
     x = torch.randn(100, 256, device="cuda")
