@@ -67,15 +67,21 @@ def flops_per_step(cfg, L, B):
     return 3 * ((enc + dec) * L + seg * B)
 
 
-def recurrent_flops(cfg, L):
-    """FLOPs of the recurrent-step kernel family (encoder + decoder cell GEMMs,
-    forward and backward), per step of training."""
+# persistent recurrent kernels: id (abcd_timing_read_kernel), rocprof symbol
+KERNELS = {1: "enc_fwd_persist", 2: "enc_bwd_persist", 3: "dec_fwd_persist", 4: "dec_bwd_persist"}
+
+
+def kernel_flops_per_frame(cfg, kid):
+    """Algorithmic FLOPs per packed frame of one persistent kernel (unpadded
+    dims, 2 per multiply-add).  Encoder: the recurrent products of both
+    directions (the input projection is a separate GEMM).  Decoder forward:
+    [x|h] W^T of the cell + the two emission MLP layers; decoder backward the
+    transposed products of the same three layers."""
     F, H, Hm = cfg["F"], cfg["H"], cfg["Hm"]
     G = 4 if cfg["rnn"] == "LSTM" else 3
-    enc_rec = 2 * 2 * H * G * H  # both directions, h @ W_hh^T (fwd) / dG @ W_hh (bwd)
-    dec_cell = 2 * (F + H) * G * H  # [x | h] @ [W_ih | W_hh]^T
-    dec_bwd = 2 * (G * H + 2 * Hm) * H  # dG @ W_hh + dZ @ [W1_mu; W1_lv]
-    return (enc_rec + dec_cell + enc_rec + dec_bwd) * L
+    if kid in (1, 2):
+        return 2 * 2 * H * G * H
+    return 2 * (F + H) * G * H + 2 * H * 2 * Hm + 2 * 2 * Hm * F
 
 
 def make_batch(cfg, seed, device):
@@ -225,14 +231,28 @@ def main():
         dist.destroy_process_group()
 
 
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the rocprofv3 PMC passes committed
+    under profiles/ (scripts/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, the
+    gfx950 correction of MI355X_MICROARCH.md), or None."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        e = t["kernels"][kernel]
+        return int(e["hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def kernel_roofline(step, batches, cfg, run):
-    """Dominant kernel family = the per-time-step recurrent kernels.  Their
-    device time is measured live with HIP events recorded by the library
-    around every launch of the family (abcd_timing_*), over the same steps."""
+    """Roofline of the dominant kernel: the persistent recurrent kernel with
+    the largest device time.  Its launches are bracketed live with HIP events
+    on the launch stream by the library (abcd_timing_*); `achieved` =
+    algorithmic FLOPs per launch (kernel_flops_per_frame x packed frames) /
+    mean launch duration."""
     from modules import _native as N
     lib = N.lib()
-    if not hasattr(lib, "abcd_timing_enable"):
-        return None
     nsteps = 3
     lib.abcd_timing_reset()
     lib.abcd_timing_enable(1)
@@ -240,19 +260,28 @@ def kernel_roofline(step, batches, cfg, run):
         run(i)
     torch.cuda.synchronize()
     lib.abcd_timing_enable(0)
-    res = (N.c_double * 4)()
-    lib.abcd_timing_read(res)
-    total_ms, launches = res[0], res[1]
-    Ls = sum(batches[i % len(batches)]["L"] for i in range(nsteps))
-    fl = recurrent_flops(cfg, Ls)
-    per_launch_flops = fl / max(launches, 1)
-    avg_s = total_ms / 1e3 / max(launches, 1)
-    achieved = per_launch_flops / avg_s / 1e12
-    return {"bound": "mfma", "kernel": "rnn_fwd_step/rnn_bwd_step (recurrent cell GEMM + fused cell)",
-            "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
-            "avg_launch_us": round(avg_s * 1e6, 3), "launches": int(launches),
-            "flops_per_launch": round(per_launch_flops)}
+    frames = [batches[i % len(batches)]["L"] for i in range(nsteps)]
+    per = {}
+    for kid, name in KERNELS.items():
+        res = (N.c_double * 4)()
+        lib.abcd_timing_read_kernel(kid, res)
+        ms, launches = res[0], int(res[1])
+        if launches == 0:
+            continue
+        fl = kernel_flops_per_frame(cfg, kid) * sum(frames) / launches
+        avg_s = ms / 1e3 / launches
+        per[name] = {"avg_launch_us": round(avg_s * 1e6, 3), "launches": launches,
+                     "flops_per_launch": round(fl), "tflops": round(fl / avg_s / 1e12, 3)}
+    if not per:
+        return None
+    dom = max(per, key=lambda k: per[k]["avg_launch_us"] * per[k]["launches"])
+    d = per[dom]
+    achieved = d["tflops"]
+    traffic = load_traffic(dom)
+    return {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
+            "avg_launch_us": d["avg_launch_us"], "launches": d["launches"],
+            "flops_per_launch": d["flops_per_launch"], "all_kernels": per}
 
 
 if __name__ == "__main__":

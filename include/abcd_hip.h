@@ -211,12 +211,15 @@ int abcd_linear(int M, int N, int K, const float* x, long ldx, const float* W, l
                 float* y, long ldy, void* ws, size_t ws_bytes, void* stream);
 /* n standard normals from Philox-4x32-10(seed, offset + i) */
 int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offset, void* stream);
-/* live device timing of the recurrent-step kernel family (encoder and decoder
- * rnn_fwd_step / rnn_bwd_step): HIP events around every launch while enabled;
+/* live device timing of the recurrent kernel family (encoder and decoder,
+ * persistent or per-step): HIP events around every launch while enabled;
  * read: out[0] = summed device ms, out[1] = number of launches */
 void abcd_timing_enable(int on);
 void abcd_timing_reset(void);
 int abcd_timing_read(double* out);
+/* the same for one kernel: 0 per-step recurrent kernels, 1 encoder forward,
+ * 2 encoder backward, 3 decoder forward, 4 decoder backward (persistent) */
+int abcd_timing_read_kernel(int kid, double* out);
 /* 0 if no persistent recurrent kernel has timed out waiting for its group
  * since the last call (a timeout means the grid was not co-resident; the
  * results of that launch are invalid).  Reads and clears the device word;

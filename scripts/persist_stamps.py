@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Diagnostics: per-phase timing of the persistent recurrent kernels.
+
+Runs the bench.py c2 workload, enables the s_memtime stamps of one persistent
+kernel at a time (abcd_debug_persist_prof), and prints, per kernel, the median
+over workgroups of each phase's cycles averaged over the time steps, plus
+the kernel's event-timed duration (to convert cycles to microseconds).
+
+    python scripts/persist_stamps.py
+"""
+import ctypes
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "seq2seq_abcd-vae_amd"))
+
+import bench  # noqa: E402
+
+NAMES = {1: ("enc_fwd", ["gxload+wait", "mma", "cell+st", "publish+stash"]),
+         2: ("enc_bwd", ["epiload+wait", "mma", "cell+st", "publish"]),
+         4: ("dec_fwd", ["cell", "mlp-wait", "mlp", "emit-wait", "emit"]),
+         8: ("dec_bwd", ["P0", "P1-wait", "P1", "P2-wait", "P2"])}
+
+
+def main():
+    from modules import _native as N, noise
+    lib = N.lib()
+    lib.abcd_debug_persist_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.abcd_debug_persist_prof.restype = None
+    cfg = bench.CONFIGS["c2"]
+    dev = torch.device("cuda", 0)
+    noise.set_mode("philox")
+    noise.manual_seed(1234)
+    step = bench.build(cfg, dev)
+    b = bench.make_batch(cfg, 0, dev)
+    T = b["T"]
+
+    def run():
+        step.step(b["data"], b["batch_sizes"], b["is_offset"], b["speakers"], cfg["N"], is_pretraining=False,
+                  lr=0.0, momentum=0.0, clip=1.0)
+
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    grid = 256
+    buf = torch.zeros(grid * T * 8, dtype=torch.int64, device=dev)
+    for mask, (name, phases) in NAMES.items():
+        buf.zero_()
+        lib.abcd_debug_persist_prof(ctypes.c_void_p(buf.data_ptr()), mask)
+        run()
+        torch.cuda.synchronize()
+        lib.abcd_debug_persist_prof(None, 0)
+        st = buf.view(grid, T, 8).cpu().double()
+        nst = len(phases) + 1
+        s = st[:, :, :nst]
+        ok = (s > 0).all(dim=2)
+        d = s[:, :, 1:] - s[:, :, :-1]  # phase k = stamp k+1 - stamp k
+        # step wall: stamp0 of step i+1 - stamp0 of step i
+        wall = s[:, 1:, 0] - s[:, :-1, 0]
+        okw = ok[:, 1:] & ok[:, :-1]
+        res = []
+        for k in range(nst - 1):
+            v = d[:, :, k][ok]
+            res.append(float(v.median()) if v.numel() else float("nan"))
+        w = wall[okw]
+        # steps split into early (full batch) / late halves
+        print(f"{name}: valid (wg,step) {int(ok.sum())}/{grid * T}; median cycles per phase:")
+        print("   " + "  ".join(f"{p}={c:.0f}" for p, c in zip(phases, res)))
+        first = s[:, 0, 0][ok[:, 0]].min()
+        last = s[:, -1, nst - 1][ok[:, -1]].max()
+        print(f"   span first->last stamp {float(last - first):.0f} cyc")
+        if w.numel():
+            print(f"   step wall median {float(w.median()):.0f} cyc, mean {float(w.mean()):.0f} cyc")
+        # first 40 steps (full batch)
+        early = [float(d[:, :40, k][ok[:, :40]].median()) for k in range(nst - 1)]
+        print("   first-40-steps: " + "  ".join(f"{p}={c:.0f}" for p, c in zip(phases, early)))
+        if name in ("dec_fwd", "dec_bwd"):
+            sel = slice(0, 40) if name == "dec_fwd" else slice(T - 40, T)
+            full = st[:, sel, :]
+            okf = (full[:, :, :8] > 0).all(dim=2)
+            def med(a, b):
+                v = (full[:, :, a] - full[:, :, b])[okf]
+                return float(v.median()) if v.numel() else float("nan")
+            if name == "dec_fwd":
+                print(f"   full-batch: cell-mma={med(7, 0):.0f} cell-epi+pub={med(1, 7):.0f} "
+                      f"mlp-mma={med(6, 2):.0f} mlp-epi+pub={med(3, 6):.0f} step={med(5, 0):.0f}")
+            else:
+                print(f"   full-batch: P0-mma={med(6, 0):.0f} P0-epi+pub={med(1, 6):.0f} "
+                      f"P1-mma={med(7, 2):.0f} P1-epi+pub={med(3, 7):.0f}")
+    # event timing of the persistent kernels
+    lib.abcd_timing_reset()
+    lib.abcd_timing_enable(1)
+    run()
+    torch.cuda.synchronize()
+    lib.abcd_timing_enable(0)
+    res = (ctypes.c_double * 4)()
+    lib.abcd_timing_read(res)
+    print(f"timed launches {int(res[1])}: total {res[0]:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()

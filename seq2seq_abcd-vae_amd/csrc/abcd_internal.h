@@ -80,14 +80,17 @@ int validate_batch(const int64_t* bs, int T, int L, int B);
 }  // namespace abcd
 
 namespace abcd {
-// Optional live timing of the recurrent-step kernel family (bench.py roofline):
-// when enabled, a HIP event pair brackets every launch inside TimedScope.
+// Optional live timing of the recurrent kernel family (bench.py roofline):
+// when enabled, a HIP event pair brackets every launch inside TimedScope,
+// tagged with the kernel id (TK_*) so one kernel can be read back alone.
+enum TimedKernel { TK_STEP = 0, TK_ENC_FWD = 1, TK_ENC_BWD = 2, TK_DEC_FWD = 3, TK_DEC_BWD = 4, TK_N = 5 };
 bool timing_on();
-void timing_mark(hipStream_t s, bool begin);
+void timing_mark(hipStream_t s, int kid);
 struct TimedScope {
   hipStream_t s;
   bool on;
-  explicit TimedScope(hipStream_t st) : s(st), on(timing_on()) { if (on) timing_mark(s, true); }
-  ~TimedScope() { if (on) timing_mark(s, false); }
+  int kid;
+  explicit TimedScope(hipStream_t st, int k = TK_STEP) : s(st), on(timing_on()), kid(k) { if (on) timing_mark(s, kid); }
+  ~TimedScope() { if (on) timing_mark(s, kid); }
 };
 }  // namespace abcd

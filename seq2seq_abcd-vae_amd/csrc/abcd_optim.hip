@@ -134,43 +134,50 @@ extern "C" int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offs
 extern "C" const char* abcd_version(void) { return "abcd_hip 0.1 gfx950 fp32-mfma16x16x4"; }
 
 // ---------------------------------------------------------------------------
-// live kernel timing (bench.py): event pairs around recurrent-step launches
+// live kernel timing (bench.py): event pairs around recurrent-kernel launches
 // ---------------------------------------------------------------------------
 #include <vector>
 namespace abcd {
 struct TimingState {
   bool on = false;
   std::vector<hipEvent_t> ev;  // begin, end, begin, end, ...
+  std::vector<int> kid;        // kernel id of each event
   size_t used = 0;
 };
 static TimingState g_timing;
 bool timing_on() { return g_timing.on; }
-void timing_mark(hipStream_t s, bool begin) {
-  (void)begin;
+void timing_mark(hipStream_t s, int k) {
   if (g_timing.used == g_timing.ev.size()) {
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) { g_timing.on = false; return; }
     g_timing.ev.push_back(e);
+    g_timing.kid.push_back(0);
   }
+  g_timing.kid[g_timing.used] = k;
   (void)hipEventRecord(g_timing.ev[g_timing.used++], s);
+}
+static int timing_sum(int want, double* out) {
+  double tot = 0.0, n = 0.0;
+  const size_t pairs = g_timing.used / 2;
+  if (pairs) ABCD_TRY(hipEventSynchronize(g_timing.ev[2 * pairs - 1]));
+  for (size_t i = 0; i < pairs; ++i) {
+    if (want >= 0 && g_timing.kid[2 * i] != want) continue;
+    float ms = 0.f;
+    ABCD_TRY(hipEventElapsedTime(&ms, g_timing.ev[2 * i], g_timing.ev[2 * i + 1]));
+    tot += ms;
+    n += 1.0;
+  }
+  out[0] = tot;
+  out[1] = n;
+  out[2] = out[3] = 0.0;
+  return 0;
 }
 }  // namespace abcd
 
 extern "C" void abcd_timing_enable(int on) { abcd::g_timing.on = on != 0; }
 extern "C" void abcd_timing_reset(void) { abcd::g_timing.used = 0; }
 /* out[0] = total device ms inside the timed launches, out[1] = launches */
-extern "C" int abcd_timing_read(double* out) {
-  using namespace abcd;
-  double tot = 0.0;
-  const size_t n = g_timing.used / 2;
-  if (n) ABCD_TRY(hipEventSynchronize(g_timing.ev[2 * n - 1]));
-  for (size_t i = 0; i < n; ++i) {
-    float ms = 0.f;
-    ABCD_TRY(hipEventElapsedTime(&ms, g_timing.ev[2 * i], g_timing.ev[2 * i + 1]));
-    tot += ms;
-  }
-  out[0] = tot;
-  out[1] = (double)n;
-  out[2] = out[3] = 0.0;
-  return 0;
-}
+extern "C" int abcd_timing_read(double* out) { return abcd::timing_sum(-1, out); }
+/* the same restricted to one kernel id (0 per-step kernels, 1 encoder forward,
+ * 2 encoder backward, 3 decoder forward, 4 decoder backward) */
+extern "C" int abcd_timing_read_kernel(int kid, double* out) { return abcd::timing_sum(kid, out); }

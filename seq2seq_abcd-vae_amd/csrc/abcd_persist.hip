@@ -453,6 +453,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
       mma16<2>(acc, A, row0 + r, BC, nchc, lane, q);
     }
     acc2_fold(acc);
+    PSTAMP(7);
     float gi[4], gf[4], gg[4], go[4], hv[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -498,6 +499,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
         mma16<1>(acc1, Hs, row0 + r, B1 + k * nchh * 64, nchh, lane, q);
       }
       acc2_fold(acc1);
+      PSTAMP(6);
       const int col = 16 * j1 + r;
       const float bb = a.b1[col];
 #pragma unroll
@@ -609,6 +611,7 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
         mma16<1>(acc, A, row0 + r, B0 + k * nchg * 64, nchg, lane, q);
       }
       acc2_fold(acc);
+      PSTAMP(6);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int b = row0 + 4 * q + g;
@@ -647,6 +650,7 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
         mma16<1>(acc, A, row0 + r, B1 + k * nchx * 64, nchx, lane, q);
       }
       acc2_fold(acc);
+      PSTAMP(7);
       const int col = 16 * j1 + r;  // column of [mu | lv] (2Hm)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -777,7 +781,7 @@ static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   PFwdArgs b = a;
   b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
   {
-    TimedScope ts(s);
+    TimedScope ts(s, TK_ENC_FWD);
     enc_fwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
@@ -795,7 +799,7 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
-    TimedScope ts(s);
+    TimedScope ts(s, TK_ENC_BWD);
     enc_bwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
@@ -846,7 +850,7 @@ int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launch
   PDecFwdArgs b = a;
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
-    TimedScope ts(s);
+    TimedScope ts(s, TK_DEC_FWD);
     dec_fwd_persist<<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
@@ -869,7 +873,7 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   PDecBwdArgs b = a;
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
-    TimedScope ts(s);
+    TimedScope ts(s, TK_DEC_BWD);
     dec_bwd_persist<<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();

@@ -120,6 +120,7 @@ _SIGS = {
     "abcd_timing_enable": (None, [c_int]),
     "abcd_timing_reset": (None, []),
     "abcd_timing_read": (c_int, [ctypes.POINTER(c_double)]),
+    "abcd_timing_read_kernel": (c_int, [c_int, ctypes.POINTER(c_double)]),
     "abcd_fill_normal": (c_int, [c_void_p, c_long, c_uint64, c_uint64, c_void_p]),
     "abcd_device_status": (c_int, []),
 }
