@@ -30,6 +30,7 @@ struct PFwdArgs {
   const int* off;    // device: off[0..T]
   unsigned* sync;    // one 128-B counter line per group, zeroed before the launch
   unsigned long long* prof;  // diagnostics: per-step s_memtime stamps, or null
+  int exp;           // diagnostics (ABCD_PEXP): 1 = recurrent operand reads zero, 2 = no recurrent MMA
 };
 
 // One direction of an encoder layer, backward (BPTT).
@@ -88,7 +89,8 @@ constexpr int PERSIST_ROWS = 64;        // rows per workgroup
 constexpr int PERSIST_SYNC_STRIDE = 32;  // uints per counter (128 B)
 
 inline int persist_groups(int nd, int B) { return nd * cdiv(B, PERSIST_ROWS); }
-inline size_t persist_sync_uints(int nd, int B) { return (size_t)persist_groups(nd, B) * PERSIST_SYNC_STRIDE; }
+// group counters + the role registry (abcd_persist.hip: 8 XCD ticket lines + 1 arrival line)
+inline size_t persist_sync_uints(int nd, int B) { return (size_t)(persist_groups(nd, B) + 9) * PERSIST_SYNC_STRIDE; }
 
 // Copy off[0..T] to device memory `dst` on stream s through a pinned ring
 // (asynchronous, no host/device synchronisation).

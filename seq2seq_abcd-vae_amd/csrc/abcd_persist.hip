@@ -33,10 +33,12 @@
 #include "abcd_common.h"
 #include "abcd_internal.h"
 #include "abcd_persist.h"
+#include "abcd_x6.h"
 
 namespace abcd {
 
 __device__ unsigned g_persist_status = 0;
+__device__ unsigned g_local_wgs = 0;  // diagnostics: workgroups that ran in XCD-local mode
 
 // ---------------------------------------------------------------------------
 // hand-off primitives
@@ -60,6 +62,12 @@ struct BufKC {
   DEV f4 frag(int row, int kc, int q) const {
     const uint32_t o = (uint32_t)row * ld_bytes + (uint32_t)(kc * 16 + 4 * q) * 4u;
     return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
+  }
+  // x6 layout: k = 32c + 8q + 0..7
+  DEV void frag8(int row, int c, int q, f4& lo, f4& hi) const {
+    const uint32_t o = (uint32_t)row * ld_bytes + (uint32_t)(c * 32 + 8 * q) * 4u;
+    lo = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
+    hi = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16u, 0, 16));
   }
 };
 // Two K segments back to back (e.g. [x | h] of a recurrent cell): chunks
@@ -110,9 +118,9 @@ DEV void group_publish(unsigned* cnt) {
 static unsigned long long* g_prof = nullptr;
 static int g_prof_mask = 0;  // 1 enc fwd, 2 enc bwd, 4 dec fwd, 8 dec bwd
 
-// Workgroup -> (group, member).  Members of a group get equal blockIdx % 8,
-// i.e. one XCD under round-robin dispatch (L2 locality; speed only -- the
-// protocol above does not depend on placement).
+// Workgroup -> (group, member) by block index (fallback placement).  Members
+// of a group get equal blockIdx % 8, i.e. one XCD under round-robin dispatch
+// (L2 locality; speed only).
 DEV void group_role(int bid, int ngroups, int nmem, int& grp, int& mem) {
   if (ngroups % 8 == 0) {
     const int s = bid & 7, k = bid >> 3;
@@ -124,15 +132,91 @@ DEV void group_role(int bid, int ngroups, int nmem, int& grp, int& mem) {
   }
 }
 
+// XCD-local groups.  Every workgroup reads the XCD it actually runs on
+// (HW_REG_XCC_ID), takes a ticket on that XCD's counter, and waits until the
+// whole grid has registered.  If every XCD holds a multiple of nmem
+// workgroups, groups are formed INSIDE XCDs from the tickets ("local" mode):
+// all members of a group then share one L2, so hand-off payloads are stored
+// with plain stores (write-through L1 -> the shared L2, complete at the
+// producer's vmcnt(0) drain) and stay L2-resident for the consumers' L1-
+// bypassing sc1 loads, instead of being written through to the memory side
+// and re-fetched from it by every consumer (sc1 stores drop the L2 line).
+// Otherwise ("fallback" mode) roles come from group_role() and every
+// hand-off store is sc1 (write-through), which is correct under any
+// placement.  Registry: 8 ticket lines + 1 arrival line after the group
+// counters, zeroed with them before the launch.
+constexpr int PERSIST_REG_LINES = 9;
+struct Role {
+  int grp, mem;
+  bool local;
+};
+// `sh`: 3 ints of the kernel's dynamic LDS (no static LDS: the launchers
+// reserve the whole 160 KiB for the dynamic image); free again on return.
+DEV Role assign_role(unsigned* reg, int ngroups, int nmem, int* sh) {
+  if (threadIdx.x == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    xcc &= 7u;
+    const unsigned slot = __hip_atomic_fetch_add(reg + xcc * PERSIST_SYNC_STRIDE, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ticket performed before the arrival
+    unsigned* arrived = reg + 8 * PERSIST_SYNC_STRIDE;
+    __hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    bool ok = true;
+    while (__hip_atomic_load(arrived, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {
+        __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
+      }
+    }
+    int grp = 0, mem = 0, local = 0;
+    if (ok) {
+      int base = 0;
+      local = 1;
+      for (unsigned x = 0; x < 8; ++x) {
+        const int c = (int)__hip_atomic_load(reg + x * PERSIST_SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c % nmem) local = 0;
+        if (x < xcc) base += c / nmem;
+      }
+      if (local) {
+        grp = base + (int)slot / nmem;
+        mem = (int)slot % nmem;
+      }
+    }
+    if (!local) group_role(blockIdx.x, ngroups, nmem, grp, mem);
+    else __hip_atomic_fetch_add(&g_local_wgs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sh[0] = grp;
+    sh[1] = mem;
+    sh[2] = local;
+  }
+  __syncthreads();
+  Role r;
+  r.grp = __builtin_amdgcn_readfirstlane(sh[0]);
+  r.mem = __builtin_amdgcn_readfirstlane(sh[1]);
+  r.local = __builtin_amdgcn_readfirstlane(sh[2]) != 0;
+  __syncthreads();
+  return r;
+}
+// hand-off payload store: plain inside an XCD-local group, write-through otherwise
+DEV void st_ho(float* p, float v, bool local) {
+  if (local) *p = v;
+  else st_sc1(p, v);
+}
+
 // ---------------------------------------------------------------------------
 // encoder forward: one launch per layer, both directions
 // ---------------------------------------------------------------------------
-template <int G, int PD>
+// X6 > 0: split-fp32 recurrent MMA with X6 = H / 32 chunks (abcd_x6.h)
+template <int G, int PD, int X6>
 __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, nut = H / 16, nch = H / 16, T = a.T;
-  int grp, mem;
-  group_role(blockIdx.x, a.nd * a.nrt, nut, grp, mem);
+  const Role role = assign_role(a.sync + a.nd * a.nrt * PERSIST_SYNC_STRIDE, a.nd * a.nrt, nut, (int*)smem);
+  const int grp = role.grp, mem = role.mem;
+  const bool loc = role.local;
   const int dir = grp / a.nrt, rt = grp % a.nrt;
   const PFwdDir& D = a.d[dir];
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
@@ -140,7 +224,8 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
   const int u0 = mem * 16, unit = u0 + r;
   const int row0 = rt * PERSIST_ROWS + w * 16;  // this wave's first row inside a step
   unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
-  stage_b_frag(smem, D.Whh, H, G, nch, [&](int j) { return j * H + u0; });
+  if (X6) stage_x6(smem, D.Whh, H, H, G, H / 32, 0, H / 32, [&](int j, int rr) { return j * H + u0 + rr; });
+  else stage_b_frag(smem, D.Whh, H, G, nch, [&](int j) { return j * H + u0; });
   float bh[G];
 #pragma unroll
   for (int j = 0; j < G; ++j) bh[j] = (G == 3) ? D.bhh[j * H + unit] : 0.f;
@@ -176,9 +261,14 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
     PSTAMP(1);
     f4 acc[2][G];
     acc2_zero(acc);
-    if (row0 < bs && prev_valid > 0) {
-      const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u), (uint32_t)H * 4u};
-      wave_mma_lds<G, PD>(acc, A, row0 + r, smem, nch, lane, q);
+    if (row0 < bs && prev_valid > 0 && !(a.exp & 2)) {
+      const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (a.exp & 1) ? 0u : (uint32_t)prev_valid * H * 4u),
+                    (uint32_t)H * 4u};
+      if (X6) {
+        wave_mma_x6<G, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q);
+      } else {
+        wave_mma_lds<G, PD>(acc, A, row0 + r, smem, nch, lane, q);
+      }
     }
     acc2_fold(acc);
     PSTAMP(2);
@@ -207,7 +297,7 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
         cv[g] = 0.f;
         st[g] = hv[g];
       }
-      if (b < bs && b < next_bs) st_sc1(D.Hprev + (long)(next_off + b) * H + unit, hv[g]);
+      if (b < bs && b < next_bs) st_ho(D.Hprev + (long)(next_off + b) * H + unit, hv[g], loc);
     }
     PSTAMP(3);
     group_publish(cnt);
@@ -245,8 +335,9 @@ template <int G, int PD>
 __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, GH = G * H, nut = H / 16, nchg = GH / 16, T = a.T;
-  int grp, mem;
-  group_role(blockIdx.x, a.nd * a.nrt, nut, grp, mem);
+  const Role role = assign_role(a.sync + a.nd * a.nrt * PERSIST_SYNC_STRIDE, a.nd * a.nrt, nut, (int*)smem);
+  const int grp = role.grp, mem = role.mem;
+  const bool loc = role.local;
   const int dir = grp / a.nrt, rt = grp % a.nrt;
   const PBwdDir& D = a.d[dir];
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
@@ -320,10 +411,10 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
         const float tc = ftanh(pc[g]);
         const float dc = (fin ? pdc[g] : carry[g]) + dh * o_ * (1.f - tc * tc);
         float* dg = D.dGX + rr * GH;
-        st_sc1(dg + unit, dc * g_ * i_ * (1.f - i_));
-        st_sc1(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_));
-        st_sc1(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_));
-        st_sc1(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_));
+        st_ho(dg + unit, dc * g_ * i_ * (1.f - i_), loc);
+        st_ho(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_), loc);
+        st_ho(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_), loc);
+        st_ho(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_), loc);
         carry[g] = dc * f_;
       } else {
         if (!fin) dh += carry[g];
@@ -335,7 +426,7 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
         float* dx = D.dGX + rr * GH;
         float* dhh = D.dGH + rr * GH;
         dx[unit] = drp; dx[H + unit] = dzp; dx[2 * H + unit] = dnp;
-        st_sc1(dhh + unit, drp); st_sc1(dhh + H + unit, dzp); st_sc1(dhh + 2 * H + unit, dnp * r_);
+        st_ho(dhh + unit, drp, loc); st_ho(dhh + H + unit, dzp, loc); st_ho(dhh + 2 * H + unit, dnp * r_, loc);
         carry[g] = dh * z_;
       }
     }
@@ -396,8 +487,9 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
   const int M = H / 8, nchx = a.feedback ? Fp / 16 : 0, nchh = H / 16, nchm = Hm / 16, nchc = nchx + nchh;
   const int n1t = 2 * Hm / 16, n2t = Fp / 16;
-  int grp, mem;
-  group_role(blockIdx.x, a.nrt, M, grp, mem);
+  const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
+  const int grp = role.grp, mem = role.mem;
+  const bool loc = role.local;
   const int rt = grp;
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -467,8 +559,8 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
       hv[g] = go[g] * ftanh(cst[g]);
       const int b = row0 + 4 * q + g;
       if (b < bs) {
-        if (lo) st_sc1(a.Hs + (long)(o + b) * H + unit, hv[g]);                       // -> mlp
-        else if (b < next_bs) st_sc1(a.Hprev + (long)(next_off + b) * H + unit, hv[g]);  // -> next cell
+        if (lo) st_ho(a.Hs + (long)(o + b) * H + unit, hv[g], loc);                       // -> mlp
+        else if (b < next_bs) st_ho(a.Hprev + (long)(next_off + b) * H + unit, hv[g], loc);  // -> next cell
       }
     }
     group_publish(cnt);
@@ -505,12 +597,26 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int b = row0 + 4 * q + g;
-        if (b < bs) st_sc1(a.Aact + (long)(o + b) * 2 * Hm + col, ftanh(acc1[0][0][g] + bb));
+        if (b < bs) st_ho(a.Aact + (long)(o + b) * 2 * Hm + col, ftanh(acc1[0][0][g] + bb), loc);
       }
     }
     group_publish(cnt);
     PSTAMP(3);
     // ---------------- emit ----------------
+    // noise of the first owned tile, drawn before the wait (independent of
+    // the recurrence); its stash stores go out after the hand-off publish
+    float epre[4] = {0.f, 0.f, 0.f, 0.f}, mu0[4], lv0[4], x0[4];
+    if (n2 > 0) {
+      const int col = 16 * mem + r;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b < bs && col < F) {
+          const long rr = o + b;
+          epre[g] = a.eps ? a.eps[rr * F + col] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col);
+        }
+      }
+    }
     group_wait(cnt, (unsigned)(M * (3 * i + 2)));
     PSTAMP(4);
     for (int k = 0; k < n2; ++k) {
@@ -532,22 +638,39 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int b = row0 + 4 * q + g;
-        if (b >= bs) continue;
         const long rr = o + b;
         float mu = 0.f, lv = 0.f, x = 0.f;
         if (col < F) {
           mu = am[0][0][g] + bm;
           lv = al[0][0][g] + bl;
-          const float e = a.eps ? a.eps[rr * F + col] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col);
+          const float e = k == 0 ? epre[g]
+                                 : (a.eps ? a.eps[rr * F + col]
+                                          : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col));
           x = mu + __expf(0.5f * lv) * e;
         }
-        if (a.feedback && b < next_bs) st_sc1(a.Xin + (long)(next_off + b) * Fp + col, x);
-        a.MU[rr * Fp + col] = mu;
-        a.LV[rr * Fp + col] = lv;
-        a.OUT[rr * Fp + col] = x;
+        if (b < bs && a.feedback && b < next_bs) st_ho(a.Xin + (long)(next_off + b) * Fp + col, x, loc);
+        if (k == 0) {
+          mu0[g] = mu; lv0[g] = lv; x0[g] = x;
+        } else if (b < bs) {
+          a.MU[rr * Fp + col] = mu;
+          a.LV[rr * Fp + col] = lv;
+          a.OUT[rr * Fp + col] = x;
+        }
       }
     }
     group_publish(cnt);
+    if (n2 > 0) {
+      const int col = 16 * mem + r;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b >= bs) continue;
+        const long rr = o + b;
+        a.MU[rr * Fp + col] = mu0[g];
+        a.LV[rr * Fp + col] = lv0[g];
+        a.OUT[rr * Fp + col] = x0[g];
+      }
+    }
     PSTAMP(5);
   }
 }
@@ -565,8 +688,9 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T, GH = 4 * H;
   const int M = H / 8, nchg = GH / 16, nchx = Fp / 16, nchz = 2 * Hm / 16;
   const int nFt = Fp / 16, n0t = nFt + H / 16, n1t = 2 * Hm / 16, n2t = H / 16;
-  int grp, mem;
-  group_role(blockIdx.x, a.nrt, M, grp, mem);
+  const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
+  const int grp = role.grp, mem = role.mem;
+  const bool loc = role.local;
   const int rt = grp;
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -628,16 +752,25 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
             dmu = dx + s_em * (-d) * iv;
             dlv = dx * 0.5f * (ox - mu) + s_em * 0.5f * (1.f - d * d * iv);
           }
-          st_sc1(a.dMU + rr * Fp + col, dmu);
-          st_sc1(a.dLV + rr * Fp + col, dlv);
+          st_ho(a.dMU + rr * Fp + col, dmu, loc);
+          st_ho(a.dLV + rr * Fp + col, dlv, loc);
         } else {
-          st_sc1(a.DHR + rr * H + 16 * (j0 - nFt) + r, acc[0][0][g]);
+          st_ho(a.DHR + rr * H + 16 * (j0 - nFt) + r, acc[0][0][g], loc);
         }
       }
     }
     group_publish(cnt);
     PSTAMP(1);
     // ---------------- P1: dZ ----------------
+    // tanh outputs of the first owned tile, loaded before the wait
+    float zpre[4] = {0.f, 0.f, 0.f, 0.f};
+    if (n1 > 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b < bs) zpre[g] = a.Aact[(long)(o + b) * 2 * Hm + 16 * mem + r];
+      }
+    }
     group_wait(cnt, (unsigned)(M * (3 * i + 1)));
     PSTAMP(2);
     for (int k = 0; k < n1; ++k) {
@@ -657,8 +790,8 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
         const int b = row0 + 4 * q + g;
         if (b >= bs) continue;
         const long rr = o + b;
-        const float z = a.Aact[rr * 2 * Hm + col];
-        st_sc1(a.dZ + rr * 2 * Hm + col, acc[0][0][g] * (1.f - z * z));
+        const float z = k == 0 ? zpre[g] : a.Aact[rr * 2 * Hm + col];
+        st_ho(a.dZ + rr * 2 * Hm + col, acc[0][0][g] * (1.f - z * z), loc);
       }
     }
     group_publish(cnt);
@@ -705,10 +838,10 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
         const float tc = ftanh(pc[g]);
         const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
         float* dg = a.dG + rr * GH;
-        st_sc1(dg + unit, dc * g_ * i_ * (1.f - i_));
-        st_sc1(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_));
-        st_sc1(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_));
-        st_sc1(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_));
+        st_ho(dg + unit, dc * g_ * i_ * (1.f - i_), loc);
+        st_ho(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_), loc);
+        st_ho(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_), loc);
+        st_ho(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_), loc);
         carry[g] = dc * f_;
         if (t == 0) a.DC0[(long)b * H + unit] = dc * f_;
       }
@@ -767,22 +900,44 @@ static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
   return 0;
 }
 
+// zero the group counters and the role registry.  XCD-local mode is opt-in
+// (ABCD_XCD=1): measured on MI355X it is SLOWER than write-through hand-offs
+// (c2 step 19.05 vs 18.47 ms; the encoder's recurrent MMA 8.7k vs 7.8k
+// cycles per step), so by default XCD 0's ticket count is pre-loaded with 1,
+// the grid never looks evenly spread and every workgroup takes the fallback
+// roles with sc1 hand-off stores.
+static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
+  hipError_t e = hipMemsetAsync(sync, 0, (size_t)(ngroups + PERSIST_REG_LINES) * PERSIST_SYNC_STRIDE * sizeof(unsigned), s);
+  const char* v = getenv("ABCD_XCD");
+  if (e == hipSuccess && !(v && v[0] == '1')) e = hipMemsetAsync(sync + (size_t)ngroups * PERSIST_SYNC_STRIDE, 1, 1, s);
+  return e;
+}
+
 // ring depth: the largest of 16 / 4 / 1 dividing the chunk count
 static int ring_depth(int nch) { return nch % 16 == 0 ? 16 : (nch % 4 == 0 ? 4 : 1); }
 
-template <int G, int PD>
+// x6 (split-fp32 on the bf16 matrix cores) unless ABCD_X6=0 or the shape
+// is not one of the compiled chunk counts
+static bool x6_enabled(int K) {
+  const char* v = getenv("ABCD_X6");
+  return (K == 64 || K == 128 || K == 256) && !(v && v[0] == '0');
+}
+
+template <int G, int PD, int X6>
 static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * (a.H / 16);
-  const size_t lds = (size_t)G * 16 * a.H * sizeof(float);
+  const size_t lds = (size_t)G * 16 * a.H * (X6 ? 6 : 4);
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD, X6>, grid, lds, &ok));
   if (!ok) return 0;
-  ABCD_TRY(hipMemsetAsync(a.sync, 0, persist_sync_uints(a.nd, a.nrt * PERSIST_ROWS) * sizeof(unsigned), s));
+  ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PFwdArgs b = a;
   b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
+  const char* ex = getenv("ABCD_PEXP");
+  b.exp = ex ? atoi(ex) : 0;
   {
     TimedScope ts(s, TK_ENC_FWD);
-    enc_fwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
+    enc_fwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
   *launched = true;
@@ -795,7 +950,7 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(enc_bwd_persist<G, PD>, grid, lds, &ok));
   if (!ok) return 0;
-  ABCD_TRY(hipMemsetAsync(a.sync, 0, persist_sync_uints(a.nd, a.nrt * PERSIST_ROWS) * sizeof(unsigned), s));
+  ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
@@ -807,18 +962,26 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   return 0;
 }
 
+template <int G>
+static int launch_fwd_x6(hipStream_t s, const PFwdArgs& a, bool* launched) {
+  if (a.H == 64) return launch_fwd<G, 16, 2>(s, a, launched);
+  if (a.H == 128) return launch_fwd<G, 16, 4>(s, a, launched);
+  return launch_fwd<G, 16, 8>(s, a, launched);
+}
+
 int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled()) return 0;
+  if (x6_enabled(a.H)) return G == 4 ? launch_fwd_x6<4>(s, a, launched) : launch_fwd_x6<3>(s, a, launched);
   const int pd = ring_depth(a.H / 16);
   if (G == 4) {
-    if (pd == 16) return launch_fwd<4, 16>(s, a, launched);
-    if (pd == 4) return launch_fwd<4, 4>(s, a, launched);
-    return launch_fwd<4, 1>(s, a, launched);
+    if (pd == 16) return launch_fwd<4, 16, 0>(s, a, launched);
+    if (pd == 4) return launch_fwd<4, 4, 0>(s, a, launched);
+    return launch_fwd<4, 1, 0>(s, a, launched);
   }
-  if (pd == 16) return launch_fwd<3, 16>(s, a, launched);
-  if (pd == 4) return launch_fwd<3, 4>(s, a, launched);
-  return launch_fwd<3, 1>(s, a, launched);
+  if (pd == 16) return launch_fwd<3, 16, 0>(s, a, launched);
+  if (pd == 4) return launch_fwd<3, 4, 0>(s, a, launched);
+  return launch_fwd<3, 1, 0>(s, a, launched);
 }
 
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
@@ -846,7 +1009,7 @@ int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launch
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(dec_fwd_persist, grid, lds, &ok));
   if (!ok) return 0;
-  ABCD_TRY(hipMemsetAsync(a.sync, 0, (size_t)a.nrt * PERSIST_SYNC_STRIDE * sizeof(unsigned), s));
+  ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
@@ -869,7 +1032,7 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(dec_bwd_persist, grid, lds, &ok));
   if (!ok) return 0;
-  ABCD_TRY(hipMemsetAsync(a.sync, 0, (size_t)a.nrt * PERSIST_SYNC_STRIDE * sizeof(unsigned), s));
+  ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
@@ -896,5 +1059,14 @@ extern "C" int abcd_device_status(void) {
   unsigned v = 0, z = 0;
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(abcd::g_persist_status), sizeof(v)) != hipSuccess) return -1;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(abcd::g_persist_status), &z, sizeof(z));
+  return (int)v;
+}
+
+// diagnostics only: number of persistent workgroups that ran in XCD-local
+// mode since the last call (synchronises the device; resets the count)
+extern "C" int abcd_debug_local_wgs(void) {
+  unsigned v = 0, z = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(abcd::g_local_wgs), sizeof(v)) != hipSuccess) return -1;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(abcd::g_local_wgs), &z, sizeof(z));
   return (int)v;
 }
