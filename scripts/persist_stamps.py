@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(REPO, "seq2seq_abcd-vae_amd"))
 import bench  # noqa: E402
 
 NAMES = {1: ("enc_fwd", ["gxload+wait", "mma", "cell+st", "publish+stash"]),
-         2: ("enc_bwd", ["epiload+wait", "mma", "cell+st", "publish"]),
+         2: ("enc_bwd", ["epiload+wait+partials", "cell-bwd", "partial-mma+st", "publish"]),
          4: ("dec_fwd", ["cell", "mlp-wait", "mlp", "emit-wait", "emit"]),
          8: ("dec_bwd", ["P0", "P1-wait", "P1", "P2-wait", "P2"])}
 

@@ -48,6 +48,7 @@ struct PBwdArgs {
   const int* off;
   unsigned* sync;
   unsigned long long* prof;
+  float* part;       // split-K partials: 2 parity slots x groups x H/16 consumers x 4 waves x H/16 producers x 256
 };
 
 // Decoder forward (self-feedback LSTM, model.py:147-196): one launch for the
@@ -90,6 +91,10 @@ constexpr int PERSIST_SYNC_STRIDE = 32;  // uints per counter (128 B)
 
 inline int persist_groups(int nd, int B) { return nd * cdiv(B, PERSIST_ROWS); }
 // group counters + the role registry (abcd_persist.hip: 8 XCD ticket lines + 1 arrival line)
+inline size_t persist_part_floats(int nd, int B, int H) {
+  const size_t nut = (size_t)H / 16;
+  return 2 * (size_t)persist_groups(nd, B) * nut * 4 * nut * 256;
+}
 inline size_t persist_sync_uints(int nd, int B) { return (size_t)(persist_groups(nd, B) + 9) * PERSIST_SYNC_STRIDE; }
 
 // Copy off[0..T] to device memory `dst` on stream s through a pinned ring

@@ -85,6 +85,21 @@ struct BufKC2 {
     return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(s0 ? r0 : r1, o, 0, 16));
   }
 };
+// x6 form of BufKC2: 32-deep chunks, segment 0 holds n0 chunks of which the
+// first kv0 elements are real (the rest read zero without touching memory)
+struct BufKC2x {
+  __amdgpu_buffer_rsrc_t r0, r1;
+  uint32_t ld0, ld1;
+  int n0, kv0;
+  DEV void frag8(int row, int c, int q, f4& lo, f4& hi) const {
+    const bool s0 = c < n0;
+    const int k = (s0 ? c : c - n0) * 32 + 8 * q;
+    uint32_t o = (uint32_t)row * (s0 ? ld0 : ld1) + (uint32_t)k * 4u;
+    if (s0 && k >= kv0) o = 0x80000000u;
+    lo = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(s0 ? r0 : r1, o, 0, 16));
+    hi = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(s0 ? r0 : r1, o + 16u, 0, 16));
+  }
+};
 DEV void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // lane 0 of the workgroup polls until *cnt >= target (bounded), then the
@@ -331,7 +346,8 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
 // ---------------------------------------------------------------------------
 // encoder backward (BPTT): one launch per layer, both directions
 // ---------------------------------------------------------------------------
-template <int G, int PD>
+// X6 > 0: split-fp32 recurrent MMA over X6 = G * H / 32 chunks (abcd_x6.h)
+template <int G, int PD, int X6>
 __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, GH = G * H, nut = H / 16, nchg = GH / 16, T = a.T;
@@ -345,7 +361,8 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
   const int u0 = mem * 16, unit = u0 + r;
   const int row0 = rt * PERSIST_ROWS + w * 16;
   unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
-  stage_b_frag(smem, D.WhhT, GH, 1, nchg, [&](int) { return u0; });
+  if (X6) stage_x6(smem, D.WhhT, GH, GH, 1, GH / 32, 0, GH / 32, [&](int, int rr) { return u0 + rr; });
+  else stage_b_frag(smem, D.WhhT, GH, 1, nchg, [&](int) { return u0; });
   __syncthreads();
   float carry[4] = {0.f, 0.f, 0.f, 0.f};  // LSTM dc*f / GRU dh*z flowing to the predecessor
   const int* off = a.off;
@@ -395,7 +412,8 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
     acc2_zero(acc);
     if (row0 < bs && succ_valid > 0) {
       const BufKC A{make_rsrc(D.dGH + (size_t)succ_off * GH, (uint32_t)succ_valid * GH * 4u), (uint32_t)GH * 4u};
-      wave_mma_lds<1, PD>(acc, A, row0 + r, smem, nchg, lane, q);
+      if (X6) wave_mma_x6<1, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q);
+      else wave_mma_lds<1, PD>(acc, A, row0 + r, smem, nchg, lane, q);
     }
     acc2_fold(acc);
     PSTAMP(2);
@@ -433,6 +451,207 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
     PSTAMP(3);
     group_publish(cnt);
     PSTAMP(4);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// encoder backward, split-K form (x6).  The recurrent product of BPTT,
+//     dh_rec[b, u] = sum_k dG_succ[b, k] W_hh[k, u]     (k < G*H, u < H),
+// is split over k by OWNERSHIP: member m produced the 64 columns
+// k = gate*H + 16m + j of dG itself, so right after its cell-backward
+// epilogue it multiplies them (through a wave-private LDS transpose, no
+// global load) with its 64 rows of W_hh and publishes a partial
+//     P_m[b, u] = sum_{k in own(m)} dG[b, k] W_hh[k, u]   for all 256 u,
+// already in each consumer's accumulator layout (1 KiB per consumer and
+// wave: one dwordx4 per lane).  The next step's consumer m' sums the 16
+// partials of its unit tile.  Per wave and step this moves 16 KiB out and
+// 16 KiB in instead of loading the whole 64 KiB dG row block of the group
+// (the loads, not the MFMAs, bounded the gather form: tests/profiles).
+// Partials are double-buffered by step parity: a member writes slot
+// (i+1)&1 only after the wait for step i, which every member passes only
+// after all of them consumed step i-1's partials (slot (i-1)&1).
+// G = 3 (GRU) pads the own-column block to 64 with a zero gate.
+// ---------------------------------------------------------------------------
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+constexpr int SK_PITCH = 68;  // floats per row of the wave-private dG transpose (conflict-free b128 reads)
+template <int G, int NSUB>
+__global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  constexpr int H = NSUB * 16, GH = G * H, nut = NSUB;
+  const int T = a.T, ng = a.nd * a.nrt;
+  const Role role = assign_role(a.sync + ng * PERSIST_SYNC_STRIDE, ng, nut, (int*)smem);
+  const int grp = role.grp, mem = role.mem;
+  const bool loc = role.local;
+  const int dir = grp / a.nrt, rt = grp % a.nrt;
+  const PBwdDir& D = a.d[dir];
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int u0 = mem * 16, unit = u0 + r;
+  const int row0 = rt * PERSIST_ROWS + w * 16;
+  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  f4* Bimg = smem;                                         // [NSUB][2][3][64]
+  float* Ast = reinterpret_cast<float*>(smem + NSUB * 2 * 3 * 64) + w * 16 * SK_PITCH;
+  // B image: subtile j = output units 16j..16j+15, chunk c, lane (r, q):
+  // kappa = 32c + 8q + 0..7 -> gate kappa/16, own unit kappa%16
+  for (int e = threadIdx.x; e < NSUB * 16 * 2 * 4; e += 256) {
+    const int qq = e & 3, c = (e >> 2) & 1, u = e >> 3;
+    const int kap = 32 * c + 8 * qq, gate = kap >> 4, ju = kap & 15;
+    f4 v0 = f4zero(), v1 = f4zero();
+    if (gate < G) {
+      const float* src = D.WhhT + (long)u * GH + gate * H + u0 + ju;
+      v0 = *reinterpret_cast<const f4*>(src);
+      v1 = *reinterpret_cast<const f4*>(src + 4);
+    }
+    bf8 h, m, l;
+    split8(v0, v1, h, m, l);
+    const int j = u >> 4, rr = u & 15;
+    const int d = ((j * 2 + c) * 3) * 64 + qq * 16 + rr;
+    Bimg[d] = __builtin_bit_cast(f4, h);
+    Bimg[d + 64] = __builtin_bit_cast(f4, m);
+    Bimg[d + 128] = __builtin_bit_cast(f4, l);
+  }
+  __syncthreads();
+  const size_t slot_f = (size_t)ng * nut * 4 * nut * 256;  // floats per parity slot
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = D.rev ? i : T - 1 - i;
+    const int o = off[t], bs = off[t + 1] - o;
+    int succ_valid, prev_valid;
+    if (!D.rev) {
+      succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+      prev_valid = t == 0 ? 0 : bs;
+    } else {
+      succ_valid = t >= 1 ? bs : 0;
+      prev_valid = t == T - 1 ? 0 : off[t + 2] - off[t + 1];
+    }
+    PSTAMP(0);
+    float pg[4][4], pc[4], pcp[4], pdh[4], pdc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      const bool live = b < bs;
+      const long rr = o + (live ? b : 0);
+      const bool fin = b >= succ_valid;
+      const bool haspred = live && b < prev_valid;
+      const float* Gr = D.Gst + rr * 4 * H;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pg[g][j] = live ? Gr[j * H + unit] : 0.f;
+      pc[g] = (live && G == 4) ? D.Cst[rr * H + unit] : 0.f;
+      pcp[g] = 0.f;
+      if (haspred) pcp[g] = G == 4 ? D.Cprev[rr * H + unit] : D.Hprev[rr * H + unit];
+      float dh = 0.f, dc = 0.f;
+      if (live) {
+        if (D.DHX) dh += D.DHX[rr * D.lddhx + unit];
+        if (fin && D.dlast) {
+          dh += D.dlast[(long)b * D.ldl + D.hcol + unit];
+          if (G == 4 && D.ccol >= 0) dc = D.dlast[(long)b * D.ldl + D.ccol + unit];
+        }
+      }
+      pdh[g] = dh;
+      pdc[g] = dc;
+    }
+    f4 dhr = f4zero();
+    if (i > 0) {
+      group_wait(cnt, (unsigned)(nut * i));
+      if (row0 < succ_valid) {
+        const __amdgpu_buffer_rsrc_t pr = make_rsrc(a.part + (size_t)(i & 1) * slot_f, (uint32_t)(slot_f * 4));
+        const uint32_t base = (uint32_t)((((size_t)grp * nut + mem) * 4 + w) * nut * 256 + lane * 4) * 4u;
+        f4 v[NSUB];
+#pragma unroll
+        for (int m = 0; m < NSUB; ++m)
+          v[m] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(pr, base + m * 1024u, 0, 16));
+#pragma unroll
+        for (int m = 0; m < NSUB; ++m) dhr += v[m];
+      }
+    }
+    PSTAMP(1);
+    // cell backward -> dG (LSTM: dGX == dGH; GRU: dGH = [dr, dz, dn*r])
+    float dgh[4][4], dgx[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dgh[g][j] = dgx[g][j] = 0.f;
+      if (b >= bs) continue;
+      const bool fin = b >= succ_valid;
+      float dh = (fin ? 0.f : dhr[g]) + pdh[g];
+      if (G == 4) {
+        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
+        const float tc = ftanh(pc[g]);
+        const float dc = (fin ? pdc[g] : carry[g]) + dh * o_ * (1.f - tc * tc);
+        dgx[g][0] = dc * g_ * i_ * (1.f - i_);
+        dgx[g][1] = dc * pcp[g] * f_ * (1.f - f_);
+        dgx[g][2] = dc * i_ * (1.f - g_ * g_);
+        dgx[g][3] = dh * tc * o_ * (1.f - o_);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dgh[g][j] = dgx[g][j];
+        carry[g] = dc * f_;
+      } else {
+        if (!fin) dh += carry[g];
+        const float r_ = pg[g][0], z_ = pg[g][1], n_ = pg[g][2], ghn = pg[g][3];
+        const float hp = pcp[g];
+        const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
+        const float dzp = dh * (hp - n_) * z_ * (1.f - z_);
+        const float drp = dnp * ghn * r_ * (1.f - r_);
+        dgx[g][0] = drp; dgx[g][1] = dzp; dgx[g][2] = dnp;
+        dgh[g][0] = drp; dgh[g][1] = dzp; dgh[g][2] = dnp * r_;
+        carry[g] = dh * z_;
+      }
+    }
+    PSTAMP(2);
+    // partials for the next step from this step's own dG columns
+    if (i + 1 < T && row0 < bs) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Ast[(4 * q + g) * SK_PITCH + j * 16 + r] = dgh[g][j];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      f4 acc[NSUB];
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j) acc[j] = f4zero();
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float* ar = Ast + r * SK_PITCH + 32 * c + 8 * q;
+        const f4 x0 = *reinterpret_cast<const f4*>(ar), x1 = *reinterpret_cast<const f4*>(ar + 4);
+        bf8 a0, a1, a2;
+        split8(x0, x1, a0, a1, a2);
+#pragma unroll
+        for (int j = 0; j < NSUB; ++j) {
+          const f4* bp = Bimg + ((j * 2 + c) * 3) * 64 + lane;
+          acc[j] = mma_x6(acc[j], a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                          __builtin_bit_cast(bf8, bp[128]));
+        }
+      }
+      // consumer j's block of this step parity: (((grp*nut + j)*4 + w)*nut + mem)*256, lane's 4 floats (sc1)
+      const __amdgpu_buffer_rsrc_t pw = make_rsrc(a.part + (size_t)((i + 1) & 1) * slot_f, (uint32_t)(slot_f * 4));
+      const uint32_t base = (uint32_t)(((((size_t)grp * nut) * 4 + w) * nut + mem) * 256 + lane * 4) * 4u;
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[j]), pw, base + (uint32_t)j * (4u * nut * 1024u),
+                                               0, 16);
+    }
+    PSTAMP(3);
+    group_publish(cnt);
+    // stashes for the weight-gradient GEMMs (plain stores, after the publish)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      if (b >= bs) continue;
+      const long rr = o + b;
+      float* dx = D.dGX + rr * GH;
+#pragma unroll
+      for (int j = 0; j < G; ++j) dx[j * H + unit] = dgx[g][j];
+      if (G == 3) {
+        float* dhh = D.dGH + rr * GH;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) dhh[j * H + unit] = dgh[g][j];
+      }
+    }
+    PSTAMP(4);
+    (void)loc;
   }
 }
 
@@ -482,10 +701,14 @@ DEV void mma16(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, i
 // the three phases; phase p of step i waits for M * (3i + p).
 __device__ __forceinline__ int dec_cell_row(int H, int u0, int j, int r) { return (2 * j + (r >> 3)) * H + u0 + (r & 7); }
 
+// NCC > 0: the cell GEMM in split-fp32 (abcd_x6.h) over NCC 32-deep chunks
+// (cdiv(Fp, 32) for x when self-feeding, + H / 32 for h)
+template <int NCC>
 __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
   const int M = H / 8, nchx = a.feedback ? Fp / 16 : 0, nchh = H / 16, nchm = Hm / 16, nchc = nchx + nchh;
+  const int nx32 = a.feedback ? (Fp + 31) / 32 : 0;  // x6: chunks of x
   const int n1t = 2 * Hm / 16, n2t = Fp / 16;
   const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
   const int grp = role.grp, mem = role.mem;
@@ -497,13 +720,18 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
   const int u0 = mem * 8, unit = u0 + (r & 7);
   unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
   // LDS images
-  f4* BC = smem;                       // cell [x | h]  [2][nchc][64]
-  f4* B1 = BC + 2 * nchc * 64;          // mlp tiles     [k][nchh][64]
+  f4* BC = smem;                       // cell [x | h]  [2][nchc][64]  (x6: [2][NCC][3][64])
+  f4* B1 = BC + (NCC ? 2 * NCC * 3 : 2 * nchc) * 64;  // mlp tiles [k][nchh][64]
   const int n1 = mem < n1t ? (n1t - 1 - mem) / M + 1 : 0;
   f4* B2 = B1 + n1 * nchh * 64;         // emit tiles   [k][2][nchm][64]
   const int n2 = mem < n2t ? (n2t - 1 - mem) / M + 1 : 0;
-  if (nchx) stage_rows_seg(BC, a.Wih, Fp, 2, nchx, 0, nchc, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
-  stage_rows_seg(BC, a.Whh, H, 2, nchh, nchx, nchc, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+  if (NCC) {
+    if (nx32) stage_x6(BC, a.Wih, Fp, Fp, 2, nx32, 0, NCC, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+    stage_x6(BC, a.Whh, H, H, 2, H / 32, nx32, NCC, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+  } else {
+    if (nchx) stage_rows_seg(BC, a.Wih, Fp, 2, nchx, 0, nchc, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+    stage_rows_seg(BC, a.Whh, H, 2, nchh, nchx, nchc, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+  }
   for (int k = 0; k < n1; ++k) {
     const int j1 = mem + k * M;
     stage_b_frag(B1 + k * nchh * 64, a.W1, H, 1, nchh, [&](int) { return 16 * j1; });
@@ -539,10 +767,15 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
     acc2_zero(acc);
     if (row0 < bs) {
       // [x_t | h_{t-1}] in one ring (x is zero at t = 0: empty descriptor)
-      const BufKC2 A{make_rsrc(a.Xin + (size_t)o * Fp, t > 0 ? (uint32_t)bs * Fp * 4u : 0u),
-                     make_rsrc(a.Hprev + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)Fp * 4u, (uint32_t)H * 4u,
-                     nchx, nchc};
-      mma16<2>(acc, A, row0 + r, BC, nchc, lane, q);
+      const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.Xin + (size_t)o * Fp, t > 0 ? (uint32_t)bs * Fp * 4u : 0u);
+      const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.Hprev + (size_t)o * H, (uint32_t)bs * H * 4u);
+      if (NCC) {
+        const BufKC2x A{rx, rh, (uint32_t)Fp * 4u, (uint32_t)H * 4u, nx32, Fp};
+        wave_mma_x6<2, (NCC > 0 ? NCC : 1), 8>(acc[0], A, row0 + r, BC, NCC, lane, q);
+      } else {
+        const BufKC2 A{rx, rh, (uint32_t)Fp * 4u, (uint32_t)H * 4u, nchx, nchc};
+        mma16<2>(acc, A, row0 + r, BC, nchc, lane, q);
+      }
     }
     acc2_fold(acc);
     PSTAMP(7);
@@ -943,19 +1176,19 @@ static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   *launched = true;
   return 0;
 }
-template <int G, int PD>
+template <int G, int PD, int X6>
 static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * (a.H / 16);
-  const size_t lds = (size_t)16 * G * a.H * sizeof(float);
+  const size_t lds = (size_t)16 * G * a.H * (X6 ? 6 : 4);
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(enc_bwd_persist<G, PD>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(enc_bwd_persist<G, PD, X6>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_ENC_BWD);
-    enc_bwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
+    enc_bwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
   *launched = true;
@@ -984,41 +1217,97 @@ int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched)
   return launch_fwd<3, 1, 0>(s, a, launched);
 }
 
+template <int G, int NSUB>
+static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
+  const int grid = a.nd * a.nrt * NSUB;
+  const size_t lds = (size_t)NSUB * 2 * 3 * 64 * 16 + (size_t)4 * 16 * SK_PITCH * 4;
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(enc_bwd_sk<G, NSUB>, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
+  PBwdArgs b = a;
+  b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
+  {
+    TimedScope ts(s, TK_ENC_BWD);
+    enc_bwd_sk<G, NSUB><<<grid, 256, lds, s>>>(b);
+  }
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+
+// split-K form unless ABCD_SPLITK=0 (then the gather form)
+static bool splitk_enabled() {
+  const char* v = getenv("ABCD_SPLITK");
+  return !(v && v[0] == '0');
+}
+
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled()) return 0;
+  if (x6_enabled(a.H) && a.part && splitk_enabled()) {
+    if (G == 4) {
+      if (a.H == 64) return launch_bwd_sk<4, 4>(s, a, launched);
+      if (a.H == 128) return launch_bwd_sk<4, 8>(s, a, launched);
+      return launch_bwd_sk<4, 16>(s, a, launched);
+    }
+    if (a.H == 64) return launch_bwd_sk<3, 4>(s, a, launched);
+    if (a.H == 128) return launch_bwd_sk<3, 8>(s, a, launched);
+    return launch_bwd_sk<3, 16>(s, a, launched);
+  }
+  if (x6_enabled(a.H)) {
+    if (G == 4) {
+      if (a.H == 64) return launch_bwd<4, 16, 8>(s, a, launched);
+      if (a.H == 128) return launch_bwd<4, 16, 16>(s, a, launched);
+      return launch_bwd<4, 16, 32>(s, a, launched);
+    }
+    if (a.H == 64) return launch_bwd<3, 16, 6>(s, a, launched);
+    if (a.H == 128) return launch_bwd<3, 16, 12>(s, a, launched);
+    return launch_bwd<3, 16, 24>(s, a, launched);
+  }
   const int pd = ring_depth(G * a.H / 16);
   if (G == 4) {
-    if (pd == 16) return launch_bwd<4, 16>(s, a, launched);
-    if (pd == 4) return launch_bwd<4, 4>(s, a, launched);
-    return launch_bwd<4, 1>(s, a, launched);
+    if (pd == 16) return launch_bwd<4, 16, 0>(s, a, launched);
+    if (pd == 4) return launch_bwd<4, 4, 0>(s, a, launched);
+    return launch_bwd<4, 1, 0>(s, a, launched);
   }
-  if (pd == 16) return launch_bwd<3, 16>(s, a, launched);
-  if (pd == 4) return launch_bwd<3, 4>(s, a, launched);
-  return launch_bwd<3, 1>(s, a, launched);
+  if (pd == 16) return launch_bwd<3, 16, 0>(s, a, launched);
+  if (pd == 4) return launch_bwd<3, 4, 0>(s, a, launched);
+  return launch_bwd<3, 1, 0>(s, a, launched);
 }
 
 
-int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {
-  *launched = false;
-  if (!persist_enabled() || G != 4 || a.H % 8) return 0;
+template <int NCC>
+static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8, nchx = a.feedback ? a.Fp / 16 : 0, nchh = a.H / 16, nchm = a.Hm / 16;
   const int n1 = cdiv(2 * a.Hm / 16, M), n2 = cdiv(a.Fp / 16, M);
-  const size_t lds = (size_t)64 * 16 * (2 * nchx + 2 * nchh + n1 * nchh + 2 * n2 * nchm);
+  const size_t cell = NCC ? (size_t)2 * NCC * 3 : (size_t)2 * (nchx + nchh);
+  const size_t lds = (size_t)64 * 16 * (cell + n1 * nchh + 2 * n2 * nchm);
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_persist, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_persist<NCC>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_persist<<<grid, 256, lds, s>>>(b);
+    dec_fwd_persist<NCC><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
+}
+
+int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {
+  *launched = false;
+  if (!persist_enabled() || G != 4 || a.H % 8) return 0;
+  if (x6_enabled(a.H) && a.H == 256) {
+    const int ncc = (a.feedback ? cdiv(a.Fp, 32) : 0) + a.H / 32;
+    if (ncc == 13) return launch_dec_fwd<13>(s, a, launched);
+    if (ncc == 8) return launch_dec_fwd<8>(s, a, launched);
+  }
+  return launch_dec_fwd<0>(s, a, launched);
 }
 
 

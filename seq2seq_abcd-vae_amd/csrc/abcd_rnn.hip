@@ -305,6 +305,7 @@ struct EncWS {
   float* DHX[ABCD_MAX_LAYERS];
   int* off;          // device copy of the step offsets (persistent kernels)
   unsigned* sync;    // persistent-kernel group counters
+  float* part;       // split-K partials of the persistent backward
   float* scratch;
   size_t scratch_floats;
 };
@@ -344,6 +345,7 @@ static EncWS carve_encoder(Arena& A, const abcd_encoder_cfg* c, int T, int L, in
   w.GX = A.f((size_t)L * D * G * H);
   w.off = (int*)A.f((size_t)T + 1);
   w.sync = (unsigned*)A.f(persist_sync_uints(D, B));
+  w.part = A.f(persist_part_floats(D, B, H));
   w.scratch_floats = std::max(maxMN * 64, (size_t)1 << 20);  // split-K slabs of the wgrad GEMMs
   w.scratch = A.f(w.scratch_floats);
   return w;
@@ -482,6 +484,7 @@ extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encod
     {
       PBwdArgs pa{};
       pa.H = H; pa.nd = D; pa.T = T; pa.nrt = cdiv(x->B, PERSIST_ROWS); pa.off = w.off; pa.sync = w.sync;
+      pa.part = w.part;
       for (int d = 0; d < D; ++d) {
         PBwdDir& b = pa.d[d];
         b.WhhT = w.WhhT[l][d];

@@ -576,14 +576,18 @@ extern "C" int abcd_sampler_backward(const abcd_sampler_cfg* c, const abcd_sampl
                                        stream);
 }
 
-// learning.py:171-178 perplexities (single workgroup; diagnostics only)
-__global__ void perplex_kernel(const float* logits, int B, int K, const float* psl, float* out) {
-  extern __shared__ __attribute__((aligned(16))) float colsum_sh[];  // K floats
-  __shared__ double sh[16];
+// learning.py:171-178 perplexities (single workgroup; diagnostics only).
+// One wave per row (rows dealt round-robin over the waves); each wave keeps
+// its own column-sum row in LDS (no atomics, deterministic), summed over the
+// waves at the end.
+__global__ __launch_bounds__(1024) void perplex_kernel(const float* logits, int B, int K, const float* psl,
+                                                       float* out) {
+  extern __shared__ __attribute__((aligned(16))) float colsum_sh[];  // nw x K floats
+  __shared__ double sh[32];
   __shared__ double bc[2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
-  for (int k = tid; k < K; k += blockDim.x) colsum_sh[k] = 0.f;
-  __syncthreads();
+  float* mine = colsum_sh + (long)wv * K;
+  for (int k = lane; k < K; k += 64) mine[k] = 0.f;
   double ent = 0.0;
   for (int b = wv; b < B; b += nw) {
     const float* l = logits + (long)b * K;
@@ -593,18 +597,26 @@ __global__ void perplex_kernel(const float* logits, int B, int K, const float* p
     float s = 0.f;
     for (int k = lane; k < K; k += 64) s += __expf(l[k] - m);
     s = wave_sum(s);
+    const float ls = __logf(s), inv = 1.0f / s;
     float e = 0.f;
     for (int k = lane; k < K; k += 64) {
-      const float q = __expf(l[k] - m) / s;
-      e += -q * __logf(q);
-      atomicAdd(&colsum_sh[k], q);
+      const float z = l[k] - m;
+      const float q = __expf(z) * inv;
+      e += -q * (z - ls);
+      mine[k] += q;
     }
     e = wave_sum(e);
-    if (lane == 0) ent += e;
+    ent += e;
   }
   if (lane == 0) sh[wv] = ent;
   __syncthreads();
   if (tid == 0) { double t = 0; for (int i = 0; i < nw; ++i) t += sh[i]; bc[0] = t; }
+  // column sums over the waves (into wave 0's row)
+  for (int k = tid; k < K; k += blockDim.x) {
+    float c = 0.f;
+    for (int i = 0; i < nw; ++i) c += colsum_sh[(long)i * K + k];
+    colsum_sh[k] = c;
+  }
   __syncthreads();
   double tot = 0.0;
   for (int k = tid; k < K; k += blockDim.x) tot += colsum_sh[k];
@@ -622,9 +634,9 @@ __global__ void perplex_kernel(const float* logits, int B, int K, const float* p
   __syncthreads();
   if (lane == 0) sh[wv] = pm;
   __syncthreads();
-  if (tid == 0) { float t = -INFINITY; for (int i = 0; i < nw; ++i) t = fmaxf(t, (float)sh[i]); bc[0 + 1] = bc[1]; sh[15] = t; }
+  if (tid == 0) { float t = -INFINITY; for (int i = 0; i < nw; ++i) t = fmaxf(t, (float)sh[i]); sh[31] = t; }
   __syncthreads();
-  pm = (float)sh[15];
+  pm = (float)sh[31];
   double ps = 0.0;
   for (int k = tid; k < K; k += blockDim.x) ps += exp((double)psl[k] - pm);
   ps = wave_sum_d(ps);
@@ -643,11 +655,11 @@ __global__ void perplex_kernel(const float* logits, int B, int K, const float* p
   be = wave_sum_d(be);
   pe = wave_sum_d(pe);
   __syncthreads();
-  if (lane == 0) { sh[wv] = be; sh[8 + wv] = pe; }
+  if (lane == 0) { sh[wv] = be; sh[16 + wv] = pe; }
   __syncthreads();
   if (tid == 0) {
     double tb = 0, tp = 0;
-    for (int i = 0; i < nw; ++i) { tb += sh[i]; tp += sh[8 + i]; }
+    for (int i = 0; i < nw; ++i) { tb += sh[i]; tp += sh[16 + i]; }
     out[0] = (float)exp(bc[0] / B);
     out[1] = (float)exp(tb);
     out[2] = (float)exp(tp);
@@ -657,7 +669,11 @@ __global__ void perplex_kernel(const float* logits, int B, int K, const float* p
 extern "C" int abcd_perplexities(const float* logits, int B, int K, const float* psl, float* out, void* stream) {
   if (!logits || !psl || !out || B <= 0 || K <= 0) return ABCD_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  perplex_kernel<<<1, 512, K * sizeof(float), s>>>(logits, B, K, psl, out);
+  // as many waves (<= 16) as per-wave column-sum rows fit in 64 KiB of LDS
+  int nw = 16;
+  while (nw > 1 && (size_t)nw * K * sizeof(float) > 65536) nw >>= 1;
+  if ((size_t)nw * K * sizeof(float) > 160 * 1024) return ABCD_EINVAL;
+  perplex_kernel<<<1, 64 * nw, (size_t)nw * K * sizeof(float), s>>>(logits, B, K, psl, out);
   ABCD_CHECK_LAUNCH();
   return 0;
 }
