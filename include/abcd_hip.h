@@ -177,6 +177,19 @@ int abcd_decoder_backward(const abcd_decoder_cfg* cfg, const abcd_decoder_params
                           const float* features, const int64_t* speakers, const float* gt_offset,
                           const float* d_em, const float* d_off, float* d_features,
                           const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream);
+/* The same backward with the weight-gradient reductions (K = all packed
+ * frames) moved to `wgrad_stream`: d_features is complete in `stream` order
+ * on return (so the sampler/encoder backward can follow on `stream` at once),
+ * the weight gradients only in `wgrad_stream` order -- the caller joins the
+ * two streams before reading them (e.g. before clip_grad_norm_).  The
+ * weight-gradient kernels use a tiling that co-resides with the encoder's
+ * persistent BPTT kernel.  wgrad_stream == NULL or == stream: identical to
+ * abcd_decoder_backward. */
+int abcd_decoder_backward_overlap(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
+                                  const float* features, const int64_t* speakers, const float* gt_offset,
+                                  const float* d_em, const float* d_off, float* d_features,
+                                  const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream,
+                                  void* wgrad_stream);
 
 /* ------------------------------------------------------------------------
  * Optimiser: torch.nn.utils.clip_grad_norm_ + torch.optim.SGD

@@ -14,6 +14,15 @@
 
 namespace abcd {
 
+// Side-stream mode (GemmSideScope): weight-gradient GEMMs that run beside a
+// persistent recurrent kernel keep each workgroup small enough (LDS <= 34 KiB,
+// <= 112 VGPRs) to co-reside with it, and their grids to <= one workgroup per
+// CU, so they fill the SIMDs the latency-bound recurrence leaves idle instead
+// of displacing its workgroups.
+static thread_local int tl_side = 0;
+GemmSideScope::GemmSideScope(bool on) : prev(tl_side) { tl_side = on ? 1 : 0; }
+GemmSideScope::~GemmSideScope() { tl_side = prev; }
+
 struct EpiArgs {
   float* C; long ldc; int M, N; float alpha, beta; const float* bias; int act;
   float* slab;  // non-null when gridDim.z > 1: raw partials, slab[z][m*N + n]
@@ -113,7 +122,7 @@ static int gemm_launch(hipStream_t s, int M, int N, int K, OA A, OB B, EpiArgs e
   const int tiles = cdiv(M, 32) * cdiv(N, 64);
   int Z = 1;
   if (tiles < 768 && nch >= 16 && scratch) {
-    Z = cdiv(1024, tiles);
+    Z = cdiv(tl_side ? 256 : 1024, tiles);
     Z = std::min(Z, std::max(1, nch / 8));
     const long per = (long)M * N;
     Z = std::min<long>(Z, (long)(scratch_floats / (size_t)per));
@@ -238,7 +247,7 @@ static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, lo
                           EpiArgs e, float* scratch, size_t scratch_floats) {
   const int BM = 32 * MR, BN = 32 * NR;
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
-  int Z = std::max(1, std::min(cdiv(512, tiles), cdiv(K, 16 * 32)));
+  int Z = std::max(1, std::min(cdiv(tl_side ? 256 : 512, tiles), cdiv(K, 16 * 32)));
   if (scratch) Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)M * N)));
   else Z = 1;
   Z = std::max(Z, 1);
@@ -260,7 +269,7 @@ static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, lo
 // Tile: 128 rows x 32*NR columns covering N up to 256 per tile.
 static int gemm_tn(hipStream_t s, int M, int N, int K, const Operand& A, const Operand& B, EpiArgs e,
                    float* scratch, size_t scratch_floats) {
-  const int nr = std::min(8, cdiv(N, 32));
+  const int nr = std::min(tl_side ? 4 : 8, cdiv(N, 32));
 #define TN_CASE(n) \
   case n: return gemm_tn_launch<4, n>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
   switch (nr) {

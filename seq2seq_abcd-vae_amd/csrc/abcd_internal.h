@@ -55,6 +55,14 @@ int reduce_sum(hipStream_t s, const float* x, long n, double* partials, float* o
 
 size_t gemm_scratch_floats_hint(int M, int N, int K);
 
+// While alive (on this host thread), GEMMs use the co-residency-friendly
+// "side stream" tiling: see abcd_gemm.hip.
+struct GemmSideScope {
+  int prev;
+  explicit GemmSideScope(bool on);
+  ~GemmSideScope();
+};
+
 }  // namespace abcd
 
 namespace abcd {

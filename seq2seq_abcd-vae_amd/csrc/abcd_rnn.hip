@@ -17,6 +17,7 @@
 // One launch per time step (both encoder directions share it).  A workgroup
 // (4 waves, wave split-K) owns 16 rows x 16 units x G gates, so the LSTM/GRU
 // cell update runs in the GEMM epilogue out of LDS.
+#include <mutex>
 #include <vector>
 #include <cstdlib>
 
@@ -1010,10 +1011,33 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
   return 0;
 }
 
+// one reusable "data-gradient path done" event per device (re-recorded each
+// call: hipStreamWaitEvent captures the record that precedes it)
+static int fork_event(hipEvent_t* ev) {
+  static std::mutex mu;
+  static hipEvent_t evs[64] = {};
+  int dev = 0;
+  ABCD_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!evs[dev]) ABCD_TRY(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming));
+  *ev = evs[dev];
+  return 0;
+}
+
 extern "C" int abcd_decoder_backward(const abcd_decoder_cfg* c, const abcd_decoder_params* p, const abcd_packed* x,
                                      const float* features, const int64_t* speakers, const float* gt_offset,
                                      const float* d_em, const float* d_off, float* d_features,
                                      const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream) {
+  return abcd_decoder_backward_overlap(c, p, x, features, speakers, gt_offset, d_em, d_off, d_features, g, ws,
+                                       ws_bytes, stream, nullptr);
+}
+
+extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
+                                             const abcd_packed* x, const float* features, const int64_t* speakers,
+                                             const float* gt_offset, const float* d_em, const float* d_off,
+                                             float* d_features, const abcd_decoder_grads* g, void* ws,
+                                             size_t ws_bytes, void* stream, void* wgrad_stream) {
   ABCD_REQUIRE(dec_check(c) == 0 && p && x && x->data && features && g && ws && d_em && d_off && gt_offset);
   ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
   hipStream_t s = (hipStream_t)stream;
@@ -1111,6 +1135,18 @@ extern "C" int abcd_decoder_backward(const abcd_decoder_cfg* c, const abcd_decod
                               nullptr, ACT_NONE, sc, scf));
   if (g->f2h_b) ABCD_TRY((hipError_t)colsum(s, w.dhid, Htot, B, Htot, nullptr, g->f2h_b, 0.f, sc, scf));
   // ---- weight gradients, K = L frames ----
+  // With a separate wgrad stream they run there, behind the data-gradient
+  // path above, beside whatever the caller queues next on `stream` (the
+  // sampler and encoder backward); the caller joins before reading them.
+  const bool side = wgrad_stream && wgrad_stream != stream;
+  if (side) {
+    hipEvent_t ev;
+    ABCD_TRY((hipError_t)fork_event(&ev));
+    ABCD_TRY(hipEventRecord(ev, s));
+    s = (hipStream_t)wgrad_stream;
+    ABCD_TRY(hipStreamWaitEvent(s, ev, 0));
+  }
+  GemmSideScope side_tiles(side);
   const abcd_rnn_g& cg = g->cell;
   if (cg.w_ih) {
     if (c->feedback)

@@ -169,8 +169,12 @@ class FusedStep:
             return sc, logits
         inv = self._inv_b(B)
         d_feats = torch.empty(B, self.Dfeat, device=dev)
-        N.check(L_.abcd_decoder_backward(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off), N.ptr(inv),
-                                         N.ptr(inv), N.ptr(d_feats), self.dec_g, N.ptr(ws_d), ws_d.numel(), st),
+        # the decoder's weight-gradient reductions run on a side stream beside
+        # the sampler + encoder backward (joined below, before clip + SGD)
+        side = self._side_stream()
+        N.check(L_.abcd_decoder_backward_overlap(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
+                                                 N.ptr(inv), N.ptr(inv), N.ptr(d_feats), self.dec_g, N.ptr(ws_d),
+                                                 ws_d.numel(), st, N.c_void_p(side.cuda_stream)),
                 "decoder backward")
         d_h = torch.empty(B, self.E, device=dev)
         N.check(L_.abcd_sampler_backward(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, float(entire_data_size),
@@ -178,7 +182,14 @@ class FusedStep:
                                          ws_s.numel(), st), "sampler backward")
         N.check(L_.abcd_encoder_backward(self.enc_cfg, self.enc_p, pk, N.ptr(d_h), self.enc_g, N.ptr(ws_e),
                                          ws_e.numel(), st), "encoder backward")
+        torch.cuda.current_stream(dev).wait_stream(side)
         return sc, logits
+
+    def _side_stream(self):
+        s = getattr(self, "_side", None)
+        if s is None:
+            s = self._side = torch.cuda.Stream(self.device)
+        return s
 
     def optimizer_step(self, lr, momentum=0.0, clip=1.0):
         """clip_grad_norm_(all params, clip) + SGD(lr, momentum) on the flat buffers."""
