@@ -60,7 +60,7 @@ def main():
         run()
         torch.cuda.synchronize()
         lib.abcd_debug_persist_prof(None, 0)
-        st = buf.view(grid, T, 8).cpu().double()
+        st = buf.view(grid, T, 8).cpu().double() * 10.0  # s_memrealtime ticks (100 MHz) -> ns
         nst = len(phases) + 1
         s = st[:, :, :nst]
         ok = (s > 0).all(dim=2)
@@ -74,13 +74,13 @@ def main():
             res.append(float(v.median()) if v.numel() else float("nan"))
         w = wall[okw]
         # steps split into early (full batch) / late halves
-        print(f"{name}: valid (wg,step) {int(ok.sum())}/{grid * T}; median cycles per phase:")
+        print(f"{name}: valid (wg,step) {int(ok.sum())}/{grid * T}; median ns per phase:")
         print("   " + "  ".join(f"{p}={c:.0f}" for p, c in zip(phases, res)))
         first = s[:, 0, 0][ok[:, 0]].min()
         last = s[:, -1, nst - 1][ok[:, -1]].max()
-        print(f"   span first->last stamp {float(last - first):.0f} cyc")
+        print(f"   span first->last stamp {float(last - first):.0f} ns")
         if w.numel():
-            print(f"   step wall median {float(w.median()):.0f} cyc, mean {float(w.mean()):.0f} cyc")
+            print(f"   step wall median {float(w.median()):.0f} ns, mean {float(w.mean()):.0f} ns")
         # first 40 steps (full batch)
         early = [float(d[:, :40, k][ok[:, :40]].median()) for k in range(nst - 1)]
         print("   first-40-steps: " + "  ".join(f"{p}={c:.0f}" for p, c in zip(phases, early)))
@@ -91,12 +91,32 @@ def main():
             def med(a, b):
                 v = (full[:, :, a] - full[:, :, b])[okf]
                 return float(v.median()) if v.numel() else float("nan")
+            # critical path: per (group, step) the LAST member to reach each
+            # stamp (groups = blockIdx % 8 under the fallback roles)
+            g8 = st[:, :, :6].reshape(32, 8, T, 6)  # [member][group][step][stamp]
+            okg = (g8 > 0).all(dim=3).all(dim=0)
+            last = g8.max(dim=0).values  # [group][step][stamp]
+            first = g8.min(dim=0).values
+            def cp(a, b, src=last):
+                v = (src[:, :, a] - src[:, :, b])[okg]
+                return float(v.median()) if v.numel() else float("nan")
+            nxt = last[:, 1:, 0] - last[:, :-1, 5]
+            okn = okg[:, 1:] & okg[:, :-1]
+            print(f"   critical path (last member): 0->1 {cp(1, 0):.0f}  1->2 {cp(2, 1):.0f}  2->3 {cp(3, 2):.0f}  "
+                  f"3->4 {cp(4, 3):.0f}  4->5 {cp(5, 4):.0f}  5->next0 {float(nxt[okn].median()):.0f}")
+            for k in (1, 3, 5):
+                am = g8[:, :, :, k].argmax(dim=0)[okg]
+                h = torch.bincount(am, minlength=32)
+                top = torch.argsort(h, descending=True)[:6]
+                print(f"   last member at stamp {k}: " + " ".join(f"m{int(m)}:{int(h[m])}" for m in top))
+            sp = [(last[:, :, k] - first[:, :, k])[okg] for k in range(6)]
+            print("   member spread at each stamp (last-first): " + "  ".join(f"{k}:{float(v.median()):.0f}" for k, v in enumerate(sp)))
             if name == "dec_fwd":
                 print(f"   full-batch: cell-mma={med(7, 0):.0f} cell-epi+pub={med(1, 7):.0f} "
                       f"mlp-mma={med(6, 2):.0f} mlp-epi+pub={med(3, 6):.0f} step={med(5, 0):.0f}")
             else:
-                print(f"   full-batch: P0-mma={med(6, 0):.0f} P0-epi+pub={med(1, 6):.0f} "
-                      f"P1-mma={med(7, 2):.0f} P1-epi+pub={med(3, 7):.0f}")
+                print(f"   full-batch: P0pub-to-dhr-done={med(6, 1):.0f} P1-wait-after-dhr={med(2, 6):.0f} "
+                      f"P2-gather-mma={med(7, 4):.0f} P2-cell+splitk+pub={med(5, 7):.0f}")
     # event timing of the persistent kernels
     lib.abcd_timing_reset()
     lib.abcd_timing_enable(1)

@@ -84,18 +84,23 @@ struct PDecBwdArgs {
   const float* Y;                  // target frames (rows x F)
   const float* s_em;               // device scalar: d loss / d emission NLL
   float *dG, *dMU, *dLV, *dZ, *DHR, *DC0;
+  float* part;  // split-K partials (dec_bwd_sk): 2 parity slots x groups x (Fp+H)/16 subtiles x 4 waves x H/8 x 256
 };
+inline size_t dec_part_floats(int B, int H, int Fp) {
+  return 2 * (size_t)cdiv(B, 64) * (size_t)((Fp + H) / 16) * 4 * (size_t)(H / 8) * 256;
+}
 
 constexpr int PERSIST_ROWS = 64;        // rows per workgroup
 constexpr int PERSIST_SYNC_STRIDE = 32;  // uints per counter (128 B)
 
 inline int persist_groups(int nd, int B) { return nd * cdiv(B, PERSIST_ROWS); }
-// group counters + the role registry (abcd_persist.hip: 8 XCD ticket lines + 1 arrival line)
 inline size_t persist_part_floats(int nd, int B, int H) {
   const size_t nut = (size_t)H / 16;
   return 2 * (size_t)persist_groups(nd, B) * nut * 4 * nut * 256;
 }
-inline size_t persist_sync_uints(int nd, int B) { return (size_t)(persist_groups(nd, B) + 9) * PERSIST_SYNC_STRIDE; }
+// group counters + the role registry (abcd_persist.hip: 8 XCD ticket lines + 1
+// arrival line) + a second counter per group (dec_bwd_sk: split-K partials drained)
+inline size_t persist_sync_uints(int nd, int B) { return (size_t)(2 * persist_groups(nd, B) + 9) * PERSIST_SYNC_STRIDE; }
 
 // Copy off[0..T] to device memory `dst` on stream s through a pinned ring
 // (asynchronous, no host/device synchronisation).

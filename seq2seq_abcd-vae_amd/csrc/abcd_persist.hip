@@ -125,10 +125,11 @@ DEV void group_publish(unsigned* cnt) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// diagnostics: thread 0 stamps s_memtime at the phase boundaries of step i
+// diagnostics: thread 0 stamps s_memrealtime (100 MHz, one clock for the whole
+// device, so stamps of different workgroups compare) at the phase boundaries of step i
 #define PSTAMP(k)                                                                                   \
   do {                                                                                              \
-    if (a.prof && threadIdx.x == 0) a.prof[((size_t)blockIdx.x * T + i) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (a.prof && threadIdx.x == 0) a.prof[((size_t)blockIdx.x * T + i) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 static unsigned long long* g_prof = nullptr;
 static int g_prof_mask = 0;  // 1 enc fwd, 2 enc bwd, 4 dec fwd, 8 dec bwd
@@ -1085,6 +1086,275 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// decoder backward, split-K form (x6).  Same three phases per step as
+// dec_bwd_persist, but the big product of the BPTT step,
+//     [dx_{t+1} | dh_rec] = dG_{t+1} [W_ih | W_hh]^T-rows   (K = 4H),
+// is split over K by OWNERSHIP: in P2 every member m owns 8 hidden units (32
+// dG columns = 4 gates x 8 units; lanes r and r^8 run the cell backward of
+// the same unit, as dec_fwd_persist's cell phase does forward), and right
+// after its cell backward it multiplies those columns (wave-private LDS
+// transpose, ONE 32-deep x6 chunk) with its 32 rows of [W_ih | W_hh] and
+// publishes the partials of all NXS + NHS 16-column output subtiles in each
+// consumer's accumulator layout.  Consumers sum the M = H/8 partials:
+//   P0 (members < Fp/16): the dx tile -> dMU, dLV (+ emission NLL grads);
+//   P2 (every member):    dh_rec of its 8 units -- read right after the P0
+//                         wait, long before P2's own wait (the partials were
+//                         published one whole step earlier).
+// The gather form reads the 64-row x 4H dG block per wave (64 KiB on each of
+// 25 members, ~50 MiB per step through the fabric); here P0 moves 32 KiB per
+// wave on 9 members and P2's reads leave the critical path.  Partials are
+// double-buffered by step parity (written at step i into slot i&1, read at
+// step i+1; the slot is rewritten at step i+2 only after every member has
+// published P2 of step i+1, i.e. finished its reads).
+// NXS: Fp/16 with self-feedback, else 0; NHS = H/16; NZ = 2Hm/32 (P2's K chunks).
+// ---------------------------------------------------------------------------
+constexpr int DSK_PITCH = 36;  // floats per row of the wave-private dG transpose
+// acc += sum of NP partial f4s at base + p * 1 KiB, NB loads in flight
+template <int NP, int NB = NP>
+DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc) {
+#pragma unroll
+  for (int p0 = 0; p0 < NP; p0 += NB) {
+    f4 v[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      v[k] = p0 + k < NP ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (uint32_t)(p0 + k) * 1024u,
+                                                                                        0, 16))
+                         : f4zero();
+#pragma unroll
+    for (int k = 0; k < NB; ++k) acc += v[k];
+  }
+}
+template <int NXS, int NHS, int NZ>
+__global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  constexpr int H = NHS * 16, GH = 4 * H, M = H / 8, NS = NXS + NHS;
+  const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
+  const int nchx = Fp / 16, nFt = Fp / 16;
+  const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
+  const int grp = role.grp, mem = role.mem;
+  const bool loc = role.local;
+  const int rt = grp;
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row0 = rt * PERSIST_ROWS + w * 16;
+  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  // second counter: +1 per member once its dh partials of the previous step are drained
+  unsigned* cnt2 = a.sync + (a.nrt + PERSIST_REG_LINES + grp) * PERSIST_SYNC_STRIDE;
+  const int u0 = mem * 8, unit = u0 + (r & 7);
+  const bool lo = r < 8;
+  // LDS: split-K image [NS][3][64] | P2 image [NZ][3][64] | P1 image [nchx][64] | dG transposes [4][16][PITCH]
+  f4* SK = smem;
+  f4* B2 = SK + NS * 3 * 64;
+  f4* B1 = B2 + NZ * 3 * 64;
+  float* Ast = reinterpret_cast<float*>(B1 + nchx * 64) + w * 16 * DSK_PITCH;
+  // split-K image: subtile s, lane (rr, qq) holds rows k = 8qq + 0..7 (gate qq,
+  // own units 0..7) of output column 16s + rr: [W_ih | W_hh]^T row (col) ...
+  for (int e = threadIdx.x; e < NS * 64; e += 256) {
+    const int s = e >> 6, ln = e & 63, rr = ln & 15, qq = ln >> 4;
+    const float* src = s < NXS ? a.WihT + (long)(16 * s + rr) * GH + qq * H + u0
+                               : a.WhhT + (long)(16 * (s - NXS) + rr) * GH + qq * H + u0;
+    bf8 h, m, l;
+    split8(*reinterpret_cast<const f4*>(src), *reinterpret_cast<const f4*>(src + 4), h, m, l);
+    SK[(s * 3) * 64 + ln] = __builtin_bit_cast(f4, h);
+    SK[(s * 3 + 1) * 64 + ln] = __builtin_bit_cast(f4, m);
+    SK[(s * 3 + 2) * 64 + ln] = __builtin_bit_cast(f4, l);
+  }
+  // P2: dh of the 8 own units (columns r and r + 8 both map to unit u0 + (r & 7))
+  stage_x6(B2, a.W1T, 2 * Hm, 2 * Hm, 1, NZ, 0, NZ, [&](int, int rr) { return u0 + (rr & 7); });
+  // P1: dZ tile j1 = mem (2Hm/16 == M: checked by the launcher)
+  const bool ismu = mem < Hm / 16;
+  if (ismu) stage_b_frag(B1, a.W2mT, Fp, 1, nchx, [&](int) { return 16 * mem; });
+  else stage_b_frag(B1, a.W2lT, Fp, 1, nchx, [&](int) { return 16 * (mem - Hm / 16); });
+  const float s_em = *a.s_em;
+  __syncthreads();
+  const size_t slot_f = (size_t)a.nrt * NS * 4 * M * 256;  // floats per parity slot
+  const __amdgpu_buffer_rsrc_t pr0 = make_rsrc(a.part, (uint32_t)(slot_f * 4));
+  const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
+  // this wave's block of subtile s: (((grp*NS + s)*4 + w)*M + producer)*256 floats
+  auto blk = [&](int s) { return (uint32_t)((((size_t)grp * NS + s) * 4 + w) * M) * 1024u; };
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = T - 1 - i;
+    const int o = off[t], bs = off[t + 1] - o;
+    const int succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+    const bool has_part = i > 0 && row0 < succ_valid;  // step t+1's producers covered this wave's rows
+    const __amdgpu_buffer_rsrc_t prd = (i & 1) ? pr0 : pr1;  // slot (i - 1) & 1
+    // ---------------- P0: dx_{t+1} tile -> dMU, dLV ----------------
+    // emission operands of the tile: independent of the hand-off, loaded before the wait
+    const int col0 = 16 * mem + r;
+    float emu[4], elv[4], eox[4], ey[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      const bool live = mem < nFt && b < bs && col0 < F;
+      const long rr = o + (live ? b : 0);
+      emu[g] = live ? a.MU[rr * Fp + col0] : 0.f;
+      elv[g] = live ? a.LV[rr * Fp + col0] : 0.f;
+      eox[g] = live ? a.OUT[rr * Fp + col0] : 0.f;
+      ey[g] = live ? a.Y[rr * F + col0] : 0.f;
+    }
+    if (i > 0) {
+      group_wait(cnt, (unsigned)(M * 3 * i));
+      // the dh partials stored after the previous P2 publish have had a whole
+      // hand-off to land: drain and announce them on the second counter
+      group_publish(cnt2);
+    }
+    PSTAMP(0);
+    if (mem < nFt) {
+      f4 dx = f4zero();
+      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b >= bs) continue;
+        const long rr = o + b;
+        float dmu = 0.f, dlv = 0.f;
+        if (col0 < F) {
+          const float dxv = dx[g], mu = emu[g], lv = elv[g];
+          const float iv = __expf(-lv), d = ey[g] - mu;
+          dmu = dxv + s_em * (-d) * iv;
+          dlv = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);
+        }
+        st_ho(a.dMU + rr * Fp + col0, dmu, loc);
+        st_ho(a.dLV + rr * Fp + col0, dlv, loc);
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(1);
+    // dh_rec of the own units from step t+1's partials (lane takes column
+    // (mem & 1) * 8 + (r & 7) of subtile NXS + mem / 2 from each producer):
+    // members without P0 work overlap it with the P0 members' work, the P0
+    // members with the hand-off latency into P1 (measured: reading it after
+    // the P1 publish instead is no faster)
+    f4 dhr = f4zero();
+    auto read_dhr = [&]() {
+      if (i > 0) group_wait(cnt2, (unsigned)(M * i));  // every wave: it holds a workgroup barrier
+      if (has_part) {
+        const int pl = q * 16 + (mem & 1) * 8 + (r & 7);
+        sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr);
+      }
+    };
+    read_dhr();
+    PSTAMP(6);
+    // ---------------- P1: dZ tile ----------------
+    float zpre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      zpre[g] = b < bs ? a.Aact[(long)(o + b) * 2 * Hm + 16 * mem + r] : 0.f;
+    }
+    group_wait(cnt, (unsigned)(M * (3 * i + 1)));
+    PSTAMP(2);
+    {
+      f4 acc[2][1];
+      acc2_zero(acc);
+      if (row0 < bs) {
+        const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
+        mma16<1>(acc, A, row0 + r, B1, nchx, lane, q);
+      }
+      acc2_fold(acc);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b >= bs) continue;
+        st_ho(a.dZ + (long)(o + b) * 2 * Hm + 16 * mem + r, acc[0][0][g] * (1.f - zpre[g] * zpre[g]), loc);
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(3);
+    // ---------------- P2: dh -> cell backward -> dG_t -> partials ----------------
+    float pg[4][4], pc[4], pcp[4], pdho[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      const bool live = b < bs;
+      const long rr = o + (live ? b : 0);
+      const float* Gr = a.Gst + rr * 4 * H;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pg[g][j] = live ? Gr[j * H + unit] : 0.f;
+      pc[g] = live ? a.Cst[rr * H + unit] : 0.f;
+      pcp[g] = live ? a.Cprev[rr * H + unit] : 0.f;
+      pdho[g] = live ? a.DHO[rr * H + unit] : 0.f;
+    }
+    group_wait(cnt, (unsigned)(M * (3 * i + 2)));
+    PSTAMP(4);
+    f4 acc[1] = {f4zero()};
+    if (row0 < bs) {
+      const BufKC Az{make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u), (uint32_t)2 * Hm * 4u};
+      wave_mma_x6<1, NZ, 8>(acc, Az, row0 + r, B2, NZ, lane, q);
+    }
+    PSTAMP(7);
+    float dgh[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dgh[g][j] = 0.f;
+      if (b >= bs) continue;
+      const bool fin = b >= succ_valid;
+      const float dh = acc[0][g] + (fin ? 0.f : dhr[g]) + pdho[g];
+      const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
+      const float tc = ftanh(pc[g]);
+      const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
+      dgh[g][0] = dc * g_ * i_ * (1.f - i_);
+      dgh[g][1] = dc * pcp[g] * f_ * (1.f - f_);
+      dgh[g][2] = dc * i_ * (1.f - g_ * g_);
+      dgh[g][3] = dh * tc * o_ * (1.f - o_);
+      carry[g] = dc * f_;
+      if (t == 0 && lo) a.DC0[(long)b * H + unit] = dc * f_;
+    }
+    // partials of this step's dG columns: the dx subtiles (read by the next
+    // step's P0, on the critical path) are drained by this phase's publish;
+    // the dh subtiles (read by the next step's P2, after its P1 wait) go out
+    // after it and are drained by the next P0 publish
+    const bool mk = i + 1 < T && row0 < bs;
+    bf8 a0, a1, a2;
+    if (mk) {
+      if (lo) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Ast[(4 * q + g) * DSK_PITCH + 8 * j + r] = dgh[g][j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const float* ar = Ast + r * DSK_PITCH + 8 * q;
+      split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
+    }
+    const __amdgpu_buffer_rsrc_t pw = (i & 1) ? pr1 : pr0;
+    auto partial = [&](int s) {
+      const f4* bp = SK + (s * 3) * 64 + lane;
+      const f4 v = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                          __builtin_bit_cast(bf8, bp[128]));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
+                                             blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+    };
+    if (mk) {
+#pragma unroll
+      for (int s = 0; s < NXS; ++s) partial(s);
+    }
+    group_publish(cnt);
+    PSTAMP(5);
+    if (mk) {
+#pragma unroll
+      for (int s = NXS; s < NS; ++s) partial(s);
+    }
+    // stash for the weight-gradient GEMMs and the initial-state gradient (plain stores, after the publish)
+    if (lo) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b >= bs) continue;
+        float* dg = a.dG + (long)(o + b) * GH;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dg[j * H + unit] = dgh[g][j];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 bool persist_enabled() {
@@ -1140,7 +1410,7 @@ static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
 // the grid never looks evenly spread and every workgroup takes the fallback
 // roles with sc1 hand-off stores.
 static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
-  hipError_t e = hipMemsetAsync(sync, 0, (size_t)(ngroups + PERSIST_REG_LINES) * PERSIST_SYNC_STRIDE * sizeof(unsigned), s);
+  hipError_t e = hipMemsetAsync(sync, 0, (size_t)(2 * ngroups + PERSIST_REG_LINES) * PERSIST_SYNC_STRIDE * sizeof(unsigned), s);
   const char* v = getenv("ABCD_XCD");
   if (e == hipSuccess && !(v && v[0] == '1')) e = hipMemsetAsync(sync + (size_t)ngroups * PERSIST_SYNC_STRIDE, 1, 1, s);
   return e;
@@ -1311,9 +1581,36 @@ int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launch
 }
 
 
+template <int NXS, int NHS, int NZ>
+static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+  constexpr int NS = NXS + NHS, M = NHS * 2;
+  const size_t lds = (size_t)(NS + NZ) * 3 * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * 16 * DSK_PITCH * 4;
+  const int grid = a.nrt * M;
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_sk<NXS, NHS, NZ>, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(zero_sync(s, a.sync, a.nrt));
+  PDecBwdArgs b = a;
+  b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
+  {
+    TimedScope ts(s, TK_DEC_BWD);
+    dec_bwd_sk<NXS, NHS, NZ><<<grid, 256, lds, s>>>(b);
+  }
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled() || G != 4 || a.H % 8) return 0;
+  // split-K form: H = 256 (32 members), 2Hm/16 == members, Fp/16 <= members
+  if (a.part && x6_enabled(a.H) && splitk_enabled() && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8) {
+    const int nxs = a.feedback ? a.Fp / 16 : 0;
+    if (nxs == 9) return launch_dec_bwd_sk<9, 16, 16>(s, a, launched);
+    if (nxs == 5) return launch_dec_bwd_sk<5, 16, 16>(s, a, launched);
+    if (nxs == 0) return launch_dec_bwd_sk<0, 16, 16>(s, a, launched);
+  }
   const int M = a.H / 8, nchg = 4 * a.H / 16, nchx = a.Fp / 16, nchz = 2 * a.Hm / 16;
   const int n0 = cdiv(a.Fp / 16 + a.H / 16, M), n1 = cdiv(2 * a.Hm / 16, M);
   const size_t lds = (size_t)64 * 16 * (n0 * nchg + n1 * nchx + nchz);
