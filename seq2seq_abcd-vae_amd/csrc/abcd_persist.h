@@ -23,6 +23,8 @@ struct PFwdDir {
   float *Hprev, *Cprev;          // stashes (Hprev is also the in-launch hand-off)
   float* out; long ldo; int hcol, ccol;  // final state (last_hidden), or null
   int rev;
+  // fused input projection (layer 0, NXC > 0): gates += X W_ih^T + b, X rows x ldx
+  const float *X, *Wih, *bih; long ldx;   // Wih: G*H x ldx (zero-padded), bih: b_ih (+ b_hh for LSTM)
 };
 struct PFwdArgs {
   PFwdDir d[2];
@@ -110,6 +112,8 @@ int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst);
 // (*launched = true); otherwise leave *launched = false (caller runs the
 // per-step kernels).  Returns 0 or a hipError_t.
 int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched);
+// the same with the input projection fused (PFwdDir::X/Wih/bih set; layer 0)
+int persist_encoder_fwd_fused(hipStream_t s, int G, const PFwdArgs& a, bool* launched);
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched);
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched);
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched);

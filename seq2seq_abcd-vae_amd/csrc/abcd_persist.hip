@@ -225,8 +225,13 @@ DEV void st_ho(float* p, float v, bool local) {
 // ---------------------------------------------------------------------------
 // encoder forward: one launch per layer, both directions
 // ---------------------------------------------------------------------------
-// X6 > 0: split-fp32 recurrent MMA with X6 = H / 32 chunks (abcd_x6.h)
-template <int G, int PD, int X6>
+// X6 > 0: split-fp32 recurrent MMA with X6 = H / 32 chunks (abcd_x6.h).
+// NXC > 0 (with X6): the input projection x_t W_ih^T + b is fused too, over
+// NXC 32-deep chunks of the padded input row: W_ih's slice sits in LDS next
+// to W_hh's, the x rows of the NEXT step are prefetched into registers at the
+// end of each step, and the x6 MMA runs before the hand-off wait (it does not
+// depend on the recurrence) -- no L x 8H projection GEMM, no GX round trip.
+template <int G, int PD, int X6, int NXC = 0>
 __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, nut = H / 16, nch = H / 16, T = a.T;
@@ -242,12 +247,50 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
   unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
   if (X6) stage_x6(smem, D.Whh, H, H, G, H / 32, 0, H / 32, [&](int j, int rr) { return j * H + u0 + rr; });
   else stage_b_frag(smem, D.Whh, H, G, nch, [&](int j) { return j * H + u0; });
-  float bh[G];
+  f4* Bx = smem + (size_t)G * (X6 > 0 ? X6 : 1) * 3 * 64;  // W_ih slice (NXC > 0)
+  if (NXC) stage_x6(Bx, D.Wih, D.ldx, (int)D.ldx, G, NXC, 0, NXC, [&](int j, int rr) { return j * H + u0 + rr; });
+  float bh[G], bx[G];
 #pragma unroll
-  for (int j = 0; j < G; ++j) bh[j] = (G == 3) ? D.bhh[j * H + unit] : 0.f;
+  for (int j = 0; j < G; ++j) {
+    bh[j] = (G == 3) ? D.bhh[j * H + unit] : 0.f;
+    bx[j] = NXC ? D.bih[j * H + unit] : 0.f;
+  }
   __syncthreads();
   float st[4] = {0.f, 0.f, 0.f, 0.f};  // c (LSTM) / h (GRU) of the lane's 4 cells
   const int* off = a.off;
+  // x rows of a step for the fused projection: lane (r, q) holds k = 32c + 8q + 0..7 of row row0 + r
+  f4 xa[NXC > 0 ? NXC : 1][2];
+  auto load_x = [&](int ii) {
+    const int tt = D.rev ? T - 1 - ii : ii;
+    const int oo = off[tt], bb = off[tt + 1] - oo;
+    const BufKC X{make_rsrc(D.X + (size_t)oo * D.ldx, (uint32_t)(bb * D.ldx * 4)), (uint32_t)(D.ldx * 4)};
+#pragma unroll
+    for (int c = 0; c < (NXC > 0 ? NXC : 1); ++c) X.frag8(row0 + r, c, q, xa[c][0], xa[c][1]);
+  };
+  f4 ax[G];  // x projection of the current step (NXC > 0)
+  auto project_x = [&](int ii) {
+    const int tt = D.rev ? T - 1 - ii : ii;
+    const int bb = off[tt + 1] - off[tt];
+#pragma unroll
+    for (int j = 0; j < G; ++j) ax[j] = f4zero();
+    if (row0 < bb) {
+#pragma unroll
+      for (int c = 0; c < (NXC > 0 ? NXC : 1); ++c) {
+        bf8 a0, a1, a2;
+        split8(xa[c][0], xa[c][1], a0, a1, a2);
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const f4* bp = Bx + ((j * NXC + c) * 3) * 64 + lane;
+          ax[j] = mma_x6(ax[j], a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                         __builtin_bit_cast(bf8, bp[128]));
+        }
+      }
+    }
+  };
+  if (NXC) {
+    load_x(0);
+    project_x(0);
+  }
   for (int i = 0; i < T; ++i) {
     const int t = D.rev ? T - 1 - i : i;
     const int o = off[t], bs = off[t + 1] - o;
@@ -265,13 +308,23 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
     // input projection of this step (independent of the recurrence: issued
     // before the wait so its latency hides behind it)
     float gxp[4][G];
+    if (NXC) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-      const bool live = b < bs;
-      const long rr = o + (live ? b : 0);
+      for (int g = 0; g < 4; ++g) {
+        const bool live = row0 + 4 * q + g < bs;
 #pragma unroll
-      for (int j = 0; j < G; ++j) gxp[g][j] = live ? D.GX[rr * D.ldgx + j * H + unit] : 0.f;
+        for (int j = 0; j < G; ++j) gxp[g][j] = live ? ax[j][g] + bx[j] : 0.f;
+      }
+      if (i + 1 < T) load_x(i + 1);  // next step's x rows: in flight across this step's wait and MMA
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        const bool live = b < bs;
+        const long rr = o + (live ? b : 0);
+#pragma unroll
+        for (int j = 0; j < G; ++j) gxp[g][j] = live ? D.GX[rr * D.ldgx + j * H + unit] : 0.f;
+      }
     }
     if (i > 0) group_wait(cnt, (unsigned)(nut * i));
     PSTAMP(1);
@@ -317,6 +370,7 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
     }
     PSTAMP(3);
     group_publish(cnt);
+    if (NXC && i + 1 < T) project_x(i + 1);  // next step's projection, off the hand-off path
     // pass 2: stashes for the backward pass and the outputs (plain stores,
     // drained while the next step waits for its operand)
 #pragma unroll
@@ -911,6 +965,194 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 
 
 // ---------------------------------------------------------------------------
+// decoder forward, all-x6 form.  The three phases of dec_fwd_persist<NCC>
+// (cell / mlp / emit) with every product on the bf16 matrix cores (x6):
+//   cell: as dec_fwd_persist<NCC>;
+//   mlp : the member's 16-column tile of Aact (K = H, NH32 chunks);
+//   emit: 2 * Fp/16 members, each owning one 16-column tile of [mu | lv] for
+//         32 of the group's 64 rows: waves 0-1 compute mu, waves 2-3 lv
+//         (K = Hm, NM32 chunks), so each wave gathers only its half of the
+//         Aact row (16 KiB instead of 32) and runs one tile instead of two;
+//         the lv waves hand lv to the mu waves through LDS, and those draw the
+//         noise and store the self-feedback sample.
+// ---------------------------------------------------------------------------
+template <int NCC, int NH32, int NM32>
+__global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
+  const int M = H / 8;
+  const int nx32 = a.feedback ? (Fp + 31) / 32 : 0;
+  const int n1t = 2 * Hm / 16, n2t = Fp / 16;
+  const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
+  const int grp = role.grp, mem = role.mem;
+  const bool loc = role.local;
+  const int rt = grp;
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row0 = rt * PERSIST_ROWS + w * 16;
+  const int u0 = mem * 8, unit = u0 + (r & 7);
+  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  // emit roles: tile j2 of [mu | lv] columns, row half `half`; wave part 0 = mu, 1 = lv
+  const int j2 = mem >> 1, half = mem & 1, part = w >> 1;
+  const int erow0 = rt * PERSIST_ROWS + 32 * half + 16 * (w & 1);
+  const bool has1 = mem < n1t, has2 = j2 < n2t;
+  // LDS images
+  f4* BC = smem;                        // cell [x | h]: [2][NCC][3][64]
+  f4* B1 = BC + 2 * NCC * 3 * 64;       // mlp tile: [NH32][3][64]
+  f4* B2 = B1 + NH32 * 3 * 64;          // emit: mu tile, lv tile: [2][NM32][3][64]
+  float* LVX = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [2][16][16]
+  if (nx32) stage_x6(BC, a.Wih, Fp, Fp, 2, nx32, 0, NCC, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+  stage_x6(BC, a.Whh, H, H, 2, H / 32, nx32, NCC, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+  if (has1) stage_x6(B1, a.W1, H, H, 1, NH32, 0, NH32, [&](int, int rr) { return 16 * mem + rr; });
+  if (has2) {
+    stage_x6(B2, a.W2m, Hm, Hm, 1, NM32, 0, NM32, [&](int, int rr) { return 16 * j2 + rr; });
+    stage_x6(B2 + NM32 * 3 * 64, a.W2l, Hm, Hm, 1, NM32, 0, NM32, [&](int, int rr) { return 16 * j2 + rr; });
+  }
+  const float bias0 = a.bias[dec_cell_row(H, u0, 0, r)], bias1 = a.bias[dec_cell_row(H, u0, 1, r)];
+  const float b1v = has1 ? a.b1[16 * mem + r] : 0.f;
+  const int col2 = 16 * j2 + r;
+  const float b2v = has2 ? (part ? a.b2l[col2] : a.b2m[col2]) : 0.f;
+  const bool lo = r < 8;
+  __syncthreads();
+  float cst[4] = {0.f, 0.f, 0.f, 0.f};
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = i;
+    const int o = off[t], bs = off[t + 1] - o;
+    const int next_off = off[t + 1];
+    const int next_bs = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+    // ---------------- cell ----------------
+    if (i == 0) {  // c_0 from feature2hidden (dec_init wrote it to the stash rows of step 0)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        cst[g] = b < bs ? a.Cprev[(long)(o + b) * H + unit] : 0.f;
+      }
+    }
+    if (i > 0) group_wait(cnt, (unsigned)(M * 3 * i));
+    PSTAMP(0);
+    f4 acc[2];
+    acc[0] = acc[1] = f4zero();
+    if (row0 < bs) {
+      // [x_t | h_{t-1}] in one ring (x is zero at t = 0: empty descriptor)
+      const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.Xin + (size_t)o * Fp, t > 0 ? (uint32_t)bs * Fp * 4u : 0u);
+      const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.Hprev + (size_t)o * H, (uint32_t)bs * H * 4u);
+      const BufKC2x A{rx, rh, (uint32_t)Fp * 4u, (uint32_t)H * 4u, nx32, Fp};
+      wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q);
+    }
+    PSTAMP(7);
+    float gi[4], gf[4], gg[4], go[4], hv[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float v0 = acc[0][g] + bias0, v1 = acc[1][g] + bias1;
+      const float w0 = __shfl_xor(v0, 8, 64), w1 = __shfl_xor(v1, 8, 64);
+      gi[g] = fsigmoid(lo ? v0 : w0);
+      gf[g] = fsigmoid(lo ? w0 : v0);
+      gg[g] = ftanh(lo ? v1 : w1);
+      go[g] = fsigmoid(lo ? w1 : v1);
+      cst[g] = gf[g] * cst[g] + gi[g] * gg[g];
+      hv[g] = go[g] * ftanh(cst[g]);
+      const int b = row0 + 4 * q + g;
+      if (b < bs) {
+        if (lo) st_ho(a.Hs + (long)(o + b) * H + unit, hv[g], loc);                       // -> mlp
+        else if (b < next_bs) st_ho(a.Hprev + (long)(next_off + b) * H + unit, hv[g], loc);  // -> next cell
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      if (b >= bs) continue;
+      const long rr = o + b;
+      float* Gr = a.Gst + rr * 4 * H;
+      if (lo) {
+        Gr[unit] = gi[g]; Gr[H + unit] = gf[g];
+        a.Cst[rr * H + unit] = cst[g];
+      } else {
+        Gr[2 * H + unit] = gg[g]; Gr[3 * H + unit] = go[g];
+        if (b < next_bs) a.Cprev[(long)(next_off + b) * H + unit] = cst[g];
+      }
+    }
+    // ---------------- mlp ----------------
+    group_wait(cnt, (unsigned)(M * (3 * i + 1)));
+    PSTAMP(2);
+    if (has1) {
+      f4 a1[1] = {f4zero()};
+      if (row0 < bs) {
+        const BufKC Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
+        wave_mma_x6<1, NH32, 8>(a1, Hs, row0 + r, B1, NH32, lane, q);
+      }
+      PSTAMP(6);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = row0 + 4 * q + g;
+        if (b < bs) st_ho(a.Aact + (long)(o + b) * 2 * Hm + 16 * mem + r, ftanh(a1[0][g] + b1v), loc);
+      }
+    }
+    group_publish(cnt);
+    PSTAMP(3);
+    // ---------------- emit ----------------
+    // the mu waves' noise, drawn before the wait (independent of the recurrence)
+    float epre[4] = {0.f, 0.f, 0.f, 0.f};
+    if (has2 && part == 0 && col2 < F) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = erow0 + 4 * q + g;
+        if (b < bs) {
+          const long rr = o + b;
+          epre[g] = a.eps ? a.eps[rr * F + col2] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col2);
+        }
+      }
+    }
+    group_wait(cnt, (unsigned)(M * (3 * i + 2)));
+    PSTAMP(4);
+    float ev[4] = {0.f, 0.f, 0.f, 0.f};  // mu (part 0) / lv (part 1); sample x kept in epre
+    if (has2) {
+      f4 ae[1] = {f4zero()};
+      if (erow0 < bs) {
+        const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
+                       (uint32_t)2 * Hm * 4u};
+        wave_mma_x6<1, NM32, 8>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) ev[g] = col2 < F ? ae[0][g] + b2v : 0.f;
+      if (part == 1) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) LVX[((w & 1) * 16 + 4 * q + g) * 16 + r] = ev[g];
+      }
+    }
+    __syncthreads();
+    if (has2 && part == 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = erow0 + 4 * q + g;
+        const float lv = LVX[((w & 1) * 16 + 4 * q + g) * 16 + r];
+        const float x = col2 < F ? ev[g] + __expf(0.5f * lv) * epre[g] : 0.f;
+        epre[g] = x;
+        if (b < bs && a.feedback && b < next_bs) st_ho(a.Xin + (long)(next_off + b) * Fp + col2, x, loc);
+      }
+    }
+    group_publish(cnt);
+    if (has2) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = erow0 + 4 * q + g;
+        if (b >= bs) continue;
+        const long rr = o + b;
+        if (part == 0) {
+          a.MU[rr * Fp + col2] = ev[g];
+          a.OUT[rr * Fp + col2] = epre[g];
+        } else {
+          a.LV[rr * Fp + col2] = ev[g];
+        }
+      }
+    }
+    PSTAMP(5);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // decoder backward (LSTM): one launch for the whole BPTT loop
 // ---------------------------------------------------------------------------
 // Group = 64-row tile, M = H/8 members (as the forward).  Tiles of 16 columns
@@ -1426,12 +1668,12 @@ static bool x6_enabled(int K) {
   return (K == 64 || K == 128 || K == 256) && !(v && v[0] == '0');
 }
 
-template <int G, int PD, int X6>
+template <int G, int PD, int X6, int NXC = 0>
 static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * (a.H / 16);
-  const size_t lds = (size_t)G * 16 * a.H * (X6 ? 6 : 4);
+  const size_t lds = (size_t)G * 16 * a.H * (X6 ? 6 : 4) + (size_t)G * NXC * 3 * 64 * 16;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD, X6>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD, X6, NXC>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PFwdArgs b = a;
@@ -1440,7 +1682,7 @@ static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   b.exp = ex ? atoi(ex) : 0;
   {
     TimedScope ts(s, TK_ENC_FWD);
-    enc_fwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
+    enc_fwd_persist<G, PD, X6, NXC><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
   *launched = true;
@@ -1470,6 +1712,26 @@ static int launch_fwd_x6(hipStream_t s, const PFwdArgs& a, bool* launched) {
   if (a.H == 64) return launch_fwd<G, 16, 2>(s, a, launched);
   if (a.H == 128) return launch_fwd<G, 16, 4>(s, a, launched);
   return launch_fwd<G, 16, 8>(s, a, launched);
+}
+
+// fused input projection (layer 0): H = 256, x6, padded input width <= 160.
+// Opt-in (ABCD_FUSEX=1): measured on MI355X at c2 the fused launch takes
+// ~0.68 ms longer than the unfused one (W_ih's slice fills the LDS next to
+// W_hh's and the extra x6 work sits on the step's critical path), about what
+// the 0.6 ms projection GEMM it replaces costs.
+int persist_encoder_fwd_fused(hipStream_t s, int G, const PFwdArgs& a, bool* launched) {
+  *launched = false;
+  const char* v = getenv("ABCD_FUSEX");
+  if (!persist_enabled() || !(v && v[0] == '1') || !x6_enabled(a.H) || a.H != 256 || !a.d[0].X) return 0;
+  const int nxc = (int)((a.d[0].ldx + 31) / 32);
+  if (G == 4) {
+    if (nxc == 5) return launch_fwd<4, 16, 8, 5>(s, a, launched);
+    if (nxc == 3) return launch_fwd<4, 16, 8, 3>(s, a, launched);
+  } else {
+    if (nxc == 5) return launch_fwd<3, 16, 8, 5>(s, a, launched);
+    if (nxc == 3) return launch_fwd<3, 16, 8, 3>(s, a, launched);
+  }
+  return 0;
 }
 
 int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched) {
@@ -1569,9 +1831,37 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
+template <int NCC, int NH32, int NM32>
+static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
+  const int M = a.H / 8;
+  const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4;
+  const int grid = a.nrt * M;
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32>, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(zero_sync(s, a.sync, a.nrt));
+  PDecFwdArgs b = a;
+  b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
+  {
+    TimedScope ts(s, TK_DEC_FWD);
+    dec_fwd_x6<NCC, NH32, NM32><<<grid, 256, lds, s>>>(b);
+  }
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled() || G != 4 || a.H % 8) return 0;
+  // all-x6 form: H = Hm = 256 (one mlp tile per member), 2 Fp/16 emit members
+  const char* v6 = getenv("ABCD_DECX6");
+  if (x6_enabled(a.H) && a.H == 256 && a.Hm == 256 && 2 * (a.Fp / 16) <= a.H / 8 && !(v6 && v6[0] == '0')) {
+    const int ncc = (a.feedback ? cdiv(a.Fp, 32) : 0) + a.H / 32;
+    if (ncc == 13) return launch_dec_fwd_x6<13, 8, 8>(s, a, launched);
+    if (ncc == 11) return launch_dec_fwd_x6<11, 8, 8>(s, a, launched);
+    if (ncc == 8) return launch_dec_fwd_x6<8, 8, 8>(s, a, launched);
+  }
   if (x6_enabled(a.H) && a.H == 256) {
     const int ncc = (a.feedback ? cdiv(a.Fp, 32) : 0) + a.H / 32;
     if (ncc == 13) return launch_dec_fwd<13>(s, a, launched);

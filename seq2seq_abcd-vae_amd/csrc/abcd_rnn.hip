@@ -398,8 +398,6 @@ extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encode
         ABCD_TRY((hipError_t)pack2d(s, W.b_ih, G * H, 1, G * H, false, w.bcat[l] + d * G * H, G * H, 1, G * H));
     }
     const float* X = l == 0 ? w.Xp : w.Y[l - 1];
-    ABCD_TRY((hipError_t)gemm(s, L, D * G * H, Inp, opKC(X, Inp, L), opKC(w.Wihp[l], Inp, D * G * H), w.GX,
-                              (long)D * G * H, 1.f, 0.f, w.bcat[l], ACT_NONE, w.scratch, w.scratch_floats));
     bool done = false;
     {
       PFwdArgs pa{};
@@ -417,9 +415,17 @@ extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encode
         const int base = (l * D + d) * (G == 4 ? 2 * H : H);
         f.hcol = base; f.ccol = G == 4 ? base + H : -1;
         f.rev = d == 1;
+        f.X = X; f.ldx = Inp; f.Wih = w.Wihp[l] + (size_t)d * G * H * Inp; f.bih = w.bcat[l] + d * G * H;
       }
       if (l == 0 && persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
-      ABCD_TRY((hipError_t)persist_encoder_fwd(s, G, pa, &done));
+      // layer 0: input projection fused into the persistent kernel when it fits;
+      // otherwise the L x D*G*H projection GEMM feeds the recurrence
+      if (l == 0) ABCD_TRY((hipError_t)persist_encoder_fwd_fused(s, G, pa, &done));
+      if (!done) {
+        ABCD_TRY((hipError_t)gemm(s, L, D * G * H, Inp, opKC(X, Inp, L), opKC(w.Wihp[l], Inp, D * G * H), w.GX,
+                                  (long)D * G * H, 1.f, 0.f, w.bcat[l], ACT_NONE, w.scratch, w.scratch_floats));
+        ABCD_TRY((hipError_t)persist_encoder_fwd(s, G, pa, &done));
+      }
     }
     for (int i = 0; i < T && !done && !(diag_mask() & 8); ++i) {
       FwdArgs a{};

@@ -144,3 +144,28 @@ def test_fused_step_persist_vs_stepwise_bench_size(cfg_name):
     for k in range(4):
         assert abs(sc_p[k] - sc_s[k]) <= 1e-5 * abs(sc_s[k]) + 1e-6, (k, sc_p[k].item(), sc_s[k].item())
     assert _rel(g_p, g_s) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knob", ["ABCD_FUSEX", "ABCD_X6GEMM"])
+def test_opt_in_paths_match_default(knob):
+    """The opt-in variants -- input projection fused into the persistent
+    encoder kernel (ABCD_FUSEX=1), split-fp32 weight-gradient GEMMs
+    (ABCD_X6GEMM=1) -- give the default path's losses and gradients at c2."""
+    import bench
+    cfg = bench.CONFIGS["c2"]
+    step = bench.build(cfg, "cuda")
+    batch = bench.make_batch(cfg, 0, "cuda")
+    sc_d, g_d = _fused_run(step, batch, True)
+    old = os.environ.get(knob)
+    os.environ[knob] = "1"
+    try:
+        sc_o, g_o = _fused_run(step, batch, True)
+    finally:
+        if old is None:
+            os.environ.pop(knob, None)
+        else:
+            os.environ[knob] = old
+    for k in range(4):
+        assert abs(sc_o[k] - sc_d[k]) <= 1e-5 * abs(sc_d[k]) + 1e-6, (k, sc_o[k].item(), sc_d[k].item())
+    assert _rel(g_o, g_d) < 1e-4
