@@ -192,6 +192,25 @@ int abcd_decoder_backward_overlap(const abcd_decoder_cfg* cfg, const abcd_decode
                                   void* wgrad_stream);
 
 /* ------------------------------------------------------------------------
+ * Featurisation + packing on the device: replaces the per-item host path
+ * Dataset.__getitem__ -> STFT.__call__ -> log_and_normalize -> pack_sequence
+ * (data_utils.py:88-103, 124-139, 165-182; learning.py:466-470) for a whole
+ * batch.  wave: concatenated fp32 samples (DEVICE); seg_off / seg_len: HOST,
+ * one entry per segment in packed (length-descending) order; window: n_fft
+ * floats (DEVICE, e.g. torch.hann_window); batch_sizes: HOST, T entries,
+ * consistent with the per-segment frame counts.  out: L x (n_fft/2 + 1)
+ * packed log-amplitudes log(|STFT| + eps) / norm; is_offset: L (may be NULL),
+ * 1 at each segment's last frame.
+ * ---------------------------------------------------------------------- */
+/* frames torch.stft produces for `length` samples (0 if none) */
+int abcd_stft_frames(long long length, int n_fft, int hop, int center);
+size_t abcd_featurize_workspace_bytes(int B, int T);
+int abcd_featurize_packed(const float* wave, const long long* seg_off, const long long* seg_len, int B, int n_fft,
+                          int hop, int center, const float* window, float eps, float norm,
+                          const int64_t* batch_sizes, int T, int L, float* out, float* is_offset, void* ws,
+                          size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
  * Optimiser: torch.nn.utils.clip_grad_norm_ + torch.optim.SGD
  * (learning.py:161-163, 256) over one flat fp32 parameter/gradient buffer.
  * ---------------------------------------------------------------------- */

@@ -244,10 +244,12 @@ class Learner(object):
         return mean_loss
 
     def learn(self, train_dataset, valid_dataset, num_epochs, batch_size_train, batch_size_valid, pretrain_epochs=0,
-              learning_rate=0.1, momentum=0.9, gradient_clip=0.25, patience=0):
-        """learning.py:245-290"""
-        train_dataloader = data_utils.DataLoader(train_dataset, batch_size=batch_size_train, shuffle=True)
-        valid_dataloader = data_utils.DataLoader(valid_dataset, batch_size=batch_size_valid)
+              learning_rate=0.1, momentum=0.9, gradient_clip=0.25, patience=0, featurizer=None):
+        """learning.py:245-290.  featurizer: a data_utils.DeviceFeaturizer when the
+        datasets return raw samples (--gpu_featurize)."""
+        train_dataloader = data_utils.DataLoader(train_dataset, batch_size=batch_size_train, shuffle=True,
+                                                 featurizer=featurizer)
+        valid_dataloader = data_utils.DataLoader(valid_dataset, batch_size=batch_size_valid, featurizer=featurizer)
         self.optimizer = torch.optim.SGD(self.parameters(), lr=learning_rate, momentum=momentum)
         if self.retrieval:
             initial_epoch = self.last_epoch + 1
@@ -397,6 +399,9 @@ def get_parameters(argv=None):
     p.add_argument("--noise", type=str, default="philox", choices=["philox", "reference"],
                    help="philox: in-kernel noise (default); reference: host torch CPU generator in the "
                         "reference's order (bit-identical noise to a reference CPU run).")
+    p.add_argument("--gpu_featurize", action="store_true",
+                   help="STFT + log + packing of each batch on the GPU (libabcd_hip) instead of per item on the "
+                        "host; same batches, features within fp32 FFT noise.")
     return p.parse_args(argv)
 
 
@@ -462,16 +467,22 @@ def main(argv=None):
     logger.info("STFT window type: {w}".format(w=parameters.fft_window_type))
     logger.info("STFT frame lengths: {v} sec".format(v=parameters.fft_frame_length))
     logger.info("STFT step size: {v} sec".format(v=parameters.fft_step_size))
-    train_dataset = data_parser.get_data(data_type="train", transform=Compose([to_tensor, stft, log_and_normalize]),
-                                         channel=parameters.channel)
-    valid_dataset = data_parser.get_data(data_type="valid", transform=Compose([to_tensor, stft, log_and_normalize]),
-                                         channel=parameters.channel)
+    featurizer = None
+    transform = Compose([to_tensor, stft, log_and_normalize])
+    if parameters.gpu_featurize:
+        featurizer = data_utils.DeviceFeaturizer(fft_frame_length, fft_step_size, window=parameters.fft_window_type,
+                                                 centering=not parameters.fft_no_centering, eps=eps, normalizer=norm,
+                                                 device=parameters.device)
+        transform = None
+        logger.info("STFT featurisation and packing on the GPU.")
+    train_dataset = data_parser.get_data(data_type="train", transform=transform, channel=parameters.channel)
+    valid_dataset = data_parser.get_data(data_type="valid", transform=transform, channel=parameters.channel)
     if parameters.validation_batch_size is None:
         parameters.validation_batch_size = parameters.batch_size
     learner.learn(train_dataset, valid_dataset, parameters.epochs, parameters.batch_size,
                   parameters.validation_batch_size, pretrain_epochs=parameters.pretrain_epochs,
                   learning_rate=parameters.learning_rate, momentum=parameters.momentum,
-                  gradient_clip=parameters.clip, patience=parameters.patience)
+                  gradient_clip=parameters.clip, patience=parameters.patience, featurizer=featurizer)
     return learner
 
 

@@ -150,11 +150,64 @@ class Compose(object):
         return data
 
 
-class DataLoader(object):
-    """data_utils.py:150-185: yields (PackedSequence, packed is_offset, speakers, ixs)."""
+class DeviceFeaturizer(object):
+    """STFT -> |.| -> log(x + eps) / norm -> pack_sequence for a whole batch on the
+    GPU (libabcd_hip: abcd_featurize_packed), replacing the per-item host chain
+    ``Compose([ToTensor(), STFT(...), log_and_normalize])`` + ``pack_sequence``
+    (data_utils.py:124-139, 165-182; learning.py:456-466).  Takes the RAW
+    per-item float32 samples (a Dataset built with transform=None) in packed
+    (length-descending) order; returns (packed data L x F on `device`,
+    batch_sizes (CPU int64), packed is_offset on `device`)."""
 
-    def __init__(self, dataset, batch_size=1, shuffle=False):
+    def __init__(self, frame_length, step_size, window="hann_window", centering=True, eps=2 ** (-15),
+                 normalizer=1.0, device="cuda"):
+        self.n_fft, self.hop, self.center = int(frame_length), int(step_size), bool(centering)
+        self.eps, self.norm = float(eps), float(normalizer)
+        self.device = torch.device(device)
+        self.window = getattr(torch, window)(self.n_fft).to(self.device, torch.float32).contiguous()
+        self._ws = None
+
+    def num_frames(self, length):
+        from . import _native as N
+        return int(N.lib().abcd_stft_frames(int(length), self.n_fft, self.hop, int(self.center)))
+
+    def __call__(self, waves):
+        from . import _native as N
+        lib = N.lib()
+        lens = [int(len(w)) for w in waves]
+        frames = [self.num_frames(n) for n in lens]
+        if any(f <= 0 for f in frames) or any(a < b for a, b in zip(frames, frames[1:])):
+            raise ValueError("segments must be in length-descending order and long enough for one frame")
+        T, B = frames[0], len(waves)
+        batch_sizes = torch.tensor([sum(f > t for f in frames) for t in range(T)], dtype=torch.int64)
+        L = int(batch_sizes.sum())
+        F = self.n_fft // 2 + 1
+        host = torch.from_numpy(np.concatenate([np.asarray(w, dtype=np.float32) for w in waves]))
+        wave = host.pin_memory().to(self.device, non_blocking=True) if self.device.type == "cuda" else host
+        seg_off = np.cumsum([0] + lens[:-1]).astype(np.int64)
+        seg_len = np.asarray(lens, dtype=np.int64)
+        out = torch.empty(L, F, device=self.device)
+        is_off = torch.empty(L, device=self.device)
+        nbytes = lib.abcd_featurize_workspace_bytes(B, T)
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = N.workspace(2 * nbytes, self.device)
+        N.check(lib.abcd_featurize_packed(N.ptr(wave), seg_off.ctypes.data, seg_len.ctypes.data, B, self.n_fft,
+                                          self.hop, int(self.center), N.ptr(self.window), self.eps, self.norm,
+                                          batch_sizes.data_ptr(), T, L, N.ptr(out), N.ptr(is_off), N.ptr(self._ws),
+                                          self._ws.numel(), N.stream()), "featurize")
+        return out, batch_sizes, is_off
+
+
+class DataLoader(object):
+    """data_utils.py:150-185: yields (PackedSequence, packed is_offset, speakers, ixs).
+
+    With ``featurizer`` (a DeviceFeaturizer) the dataset must return raw
+    samples (transform=None) and the whole batch is featurised and packed on
+    the GPU; batch order, in-batch sort and outputs are those of the host path."""
+
+    def __init__(self, dataset, batch_size=1, shuffle=False, featurizer=None):
         self.dataset = dataset
+        self.featurizer = featurizer
         self.shuffle = shuffle
         if shuffle:
             sampler = torch.utils.data.RandomSampler(self.dataset, replacement=False)
@@ -171,6 +224,15 @@ class DataLoader(object):
             raise StopIteration
         ixs = self.batches.pop()
         ixs = self.dataset.sort_indices_by_length(ixs)
+        if self.featurizer is not None:
+            waves, speakers = [], []
+            for ix in ixs:
+                w, spk = self.dataset[ix]
+                waves.append(w)
+                speakers.append(spk)
+            data, batch_sizes, is_off = self.featurizer(waves)
+            packed = torch.nn.utils.rnn.PackedSequence(data, batch_sizes)
+            return packed, torch.nn.utils.rnn.PackedSequence(is_off, batch_sizes), torch.tensor(speakers), ixs
         batched_input, speakers, is_offset = [], [], []
         for ix in ixs:
             seq, spk = self.dataset[ix]

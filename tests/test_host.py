@@ -109,3 +109,17 @@ def test_compute_refuses_cpu_tensors():
     x = torch.nn.utils.rnn.pack_sequence([torch.randn(5, 33), torch.randn(3, 33)])
     with pytest.raises(RuntimeError):
         enc(x)
+
+
+@pytest.mark.parametrize("n_fft,hop,center", [(128, 64, True), (256, 128, True), (128, 64, False), (100, 33, True)])
+def test_stft_frame_count_matches_torch(n_fft, hop, center):
+    """abcd_stft_frames (host function of the C ABI, no GPU) agrees with
+    torch.stft's frame count -- the featuriser's batch_sizes depend on it."""
+    from modules import _native as N
+    lib = N.lib()
+    for length in (n_fft // 2 + 1, n_fft, n_fft + 1, 1000, 4097):
+        if not center and length < n_fft:
+            continue
+        z = torch.stft(torch.zeros(length), n_fft, hop_length=hop, window=torch.hann_window(n_fft), center=center,
+                       return_complex=True)
+        assert lib.abcd_stft_frames(length, n_fft, hop, int(center)) == z.shape[1], length
