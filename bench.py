@@ -68,7 +68,11 @@ def flops_per_step(cfg, L, B):
 
 
 # persistent recurrent kernels: id (abcd_timing_read_kernel), rocprof symbol
-KERNELS = {1: "enc_fwd_persist", 2: "enc_bwd_persist", 3: "dec_fwd_persist", 4: "dec_bwd_persist"}
+# timing ids of the persistent-kernel roles (abcd_timing_*); at c2 the library
+# dispatches them to the kernels named in ROLE_KERNELS
+KERNELS = {1: "enc_fwd", 2: "enc_bwd", 3: "dec_fwd", 4: "dec_bwd"}
+ROLE_KERNELS = {"enc_fwd": "abcd::enc_fwd_persist<4,16,8>", "enc_bwd": "abcd::enc_bwd_sk<4,16>",
+                "dec_fwd": "abcd::dec_fwd_x6<13,8,8>", "dec_bwd": "abcd::dec_bwd_sk<9,16,16>"}
 
 
 def kernel_flops_per_frame(cfg, kid):
@@ -278,7 +282,8 @@ def kernel_roofline(step, batches, cfg, run):
     d = per[dom]
     achieved = d["tflops"]
     traffic = load_traffic(dom)
-    return {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS,
+    return {"bound": "mfma", "kernel": dom, "kernel_symbol": ROLE_KERNELS.get(dom), "achieved": achieved,
+            "peak": PEAK_FP32_MFMA_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
             "avg_launch_us": d["avg_launch_us"], "launches": d["launches"],
             "flops_per_launch": d["flops_per_launch"], "all_kernels": per}

@@ -458,7 +458,11 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
       ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0)
     return gemm_x6(s, M, N, K, A.p, A.ld, std::min(A.nrows, M), B.p, B.ld, std::min(B.nrows, N), e,
                                scratch, scratch_floats);
-  if (K >= 512 && A.nrows >= M && B.nrows >= N && tn_ok(A, M) && tn_ok(B, N))
+  // gemm_tn for the frame-reduction shapes (K = packed frames); short K (the
+  // batch-reduction weight gradients, K = B = 512) goes to gemm_ks, whose
+  // 32 x 64 tiles and grid split-K fill the chip (gemm_tn's 128 x 256 tiles
+  // leave ~16 workgroups: ~100-170 us per GEMM measured, vs ~10)
+  if (K >= 4096 && A.nrows >= M && B.nrows >= N && tn_ok(A, M) && tn_ok(B, N))
     return gemm_tn(s, M, N, K, A, B, e, scratch, scratch_floats);
   return gemm_launch(s, M, N, K, KM{A.p, A.ld, std::min(A.nrows, M), K}, KM{B.p, B.ld, std::min(B.nrows, N), K},
                      e, scratch, scratch_floats);
