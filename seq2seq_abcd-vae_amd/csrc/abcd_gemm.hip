@@ -558,6 +558,41 @@ int pack2d(hipStream_t s, const float* src, long lds, int sr, int sc, bool trans
   return 0;
 }
 
+// several pack2d / add_vec jobs in ONE launch (blockIdx.y = job): the
+// per-step weight re-layouts of a module are ~10 tiny kernels otherwise,
+// each paying a ~5 us launch slot on the step's critical path
+__global__ void pack_many_kernel(PackList pl) {
+  const PackJob& j = pl.j[blockIdx.y];
+  const long n = (long)j.dr * j.dc;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / j.dc), c = (int)(i % j.dc);
+    float v = 0.f;
+    if (r < j.sr && c < j.sc) {
+      const long o = j.trans ? (long)c * j.lds + r : (long)r * j.lds + c;
+      v = j.src[o];
+      if (j.src2) v += j.src2[o];
+    }
+    j.dst[(long)r * j.ldd + c] = v;
+  }
+}
+int Packs::add(const float* src, long lds, int sr, int sc, bool trans, float* dst, long ldd, int dr, int dc,
+               const float* src2) {
+  if ((long)dr * dc <= 0) return 0;
+  if (pl.n == ABCD_PACK_MAX) ABCD_TRY((hipError_t)flush());
+  pl.j[pl.n++] = PackJob{src, src2, lds, dst, ldd, sr, sc, dr, dc, trans ? 1 : 0};
+  maxn = std::max(maxn, (long)dr * dc);
+  return 0;
+}
+int Packs::flush() {
+  if (pl.n == 0) return 0;
+  const int gx = (int)std::min<long>(1024, cdiv(maxn, 256));
+  pack_many_kernel<<<dim3(gx, pl.n), 256, 0, s>>>(pl);
+  ABCD_CHECK_LAUNCH();
+  pl.n = 0;
+  maxn = 0;
+  return 0;
+}
+
 __global__ void add_vec_kernel(const float* a, const float* b, float* y, int n) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n) y[i] = a[i] + b[i];

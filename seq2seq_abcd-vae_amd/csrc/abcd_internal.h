@@ -50,6 +50,30 @@ int pack2d(hipStream_t s, const float* src, long lds, int sr, int sc, bool trans
 // y = a + b elementwise (n floats)
 int add_vec(hipStream_t s, const float* a, const float* b, float* y, int n);
 
+// A queue of pack2d jobs (optionally dst = src + src2, same layout) issued as
+// one launch by flush() -- or earlier, when the queue is full.
+constexpr int ABCD_PACK_MAX = 12;
+struct PackJob {
+  const float *src, *src2;
+  long lds;
+  float* dst;
+  long ldd;
+  int sr, sc, dr, dc, trans;
+};
+struct PackList {
+  PackJob j[ABCD_PACK_MAX];
+  int n;
+};
+struct Packs {
+  hipStream_t s;
+  PackList pl;
+  long maxn;
+  explicit Packs(hipStream_t st) : s(st), pl{}, maxn(0) {}
+  int add(const float* src, long lds, int sr, int sc, bool trans, float* dst, long ldd, int dr, int dc,
+          const float* src2 = nullptr);
+  int flush();
+};
+
 // Sum of n doubles/floats -> out (device), deterministic two-pass.
 int reduce_sum(hipStream_t s, const float* x, long n, double* partials, float* out, double* out64);
 

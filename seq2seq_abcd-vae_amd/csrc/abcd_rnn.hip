@@ -384,19 +384,19 @@ extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encode
   const int E = abcd_encoder_out_size(c);
   const std::vector<int> off = step_offsets(x->batch_sizes, T);
   const int64_t* bs = x->batch_sizes;
-  ABCD_TRY((hipError_t)pack2d(s, x->data, F, L, F, false, w.Xp, Fp, L, Fp));
+  Packs pk(s);
+  ABCD_TRY((hipError_t)pk.add(x->data, F, L, F, false, w.Xp, Fp, L, Fp));
   for (int l = 0; l < c->layers; ++l) {
     const int In = l == 0 ? F : D * H, Inp = l == 0 ? Fp : D * H;
     for (int d = 0; d < D; ++d) {
       const abcd_rnn_w& W = p->w[l][d];
       ABCD_REQUIRE(W.w_ih && W.w_hh && W.b_ih && W.b_hh);
-      ABCD_TRY((hipError_t)pack2d(s, W.w_ih, In, G * H, In, false, w.Wihp[l] + (size_t)d * G * H * Inp, Inp,
-                                  G * H, Inp));
-      if (G == 4)
-        ABCD_TRY((hipError_t)add_vec(s, W.b_ih, W.b_hh, w.bcat[l] + d * G * H, G * H));
-      else
-        ABCD_TRY((hipError_t)pack2d(s, W.b_ih, G * H, 1, G * H, false, w.bcat[l] + d * G * H, G * H, 1, G * H));
+      ABCD_TRY((hipError_t)pk.add(W.w_ih, In, G * H, In, false, w.Wihp[l] + (size_t)d * G * H * Inp, Inp, G * H,
+                                  Inp));
+      ABCD_TRY((hipError_t)pk.add(W.b_ih, G * H, 1, G * H, false, w.bcat[l] + d * G * H, G * H, 1, G * H,
+                                  G == 4 ? W.b_hh : nullptr));
     }
+    ABCD_TRY((hipError_t)pk.flush());
     const float* X = l == 0 ? w.Xp : w.Y[l - 1];
     bool done = false;
     {
@@ -927,17 +927,21 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
   const std::vector<int> off = step_offsets(bs, T);
   const abcd_rnn_w& cw = p->cell;
   // ---- derived (compute-layout) weights ----
-  ABCD_TRY((hipError_t)pack2d(s, cw.w_ih, F, GH, F, false, w.Wihp, Fp, GH, Fp));
-  if (G == 4) ABCD_TRY((hipError_t)add_vec(s, cw.b_ih, cw.b_hh, w.bcomb, GH));
-  else ABCD_TRY((hipError_t)pack2d(s, cw.b_ih, GH, 1, GH, false, w.bcomb, GH, 1, GH));
-  ABCD_TRY((hipError_t)pack2d(s, p->mu.w1, H, Hm, H, false, w.W1cat, H, Hm, H));
-  ABCD_TRY((hipError_t)pack2d(s, p->lv.w1, H, Hm, H, false, w.W1cat + (size_t)Hm * H, H, Hm, H));
-  ABCD_TRY((hipError_t)pack2d(s, p->mu.b1, Hm, 1, Hm, false, w.b1cat, Hm, 1, Hm));
-  ABCD_TRY((hipError_t)pack2d(s, p->lv.b1, Hm, 1, Hm, false, w.b1cat + Hm, Hm, 1, Hm));
-  ABCD_TRY((hipError_t)pack2d(s, p->mu.w2, Hm, F, Hm, false, w.W2mp, Hm, Fp, Hm));
-  ABCD_TRY((hipError_t)pack2d(s, p->lv.w2, Hm, F, Hm, false, w.W2lp, Hm, Fp, Hm));
-  ABCD_TRY((hipError_t)pack2d(s, p->mu.b2, F, 1, F, false, w.b2mp, Fp, 1, Fp));
-  ABCD_TRY((hipError_t)pack2d(s, p->lv.b2, F, 1, F, false, w.b2lp, Fp, 1, Fp));
+  {
+    Packs pk(s);
+    ABCD_TRY((hipError_t)pk.add(cw.w_ih, F, GH, F, false, w.Wihp, Fp, GH, Fp));
+    if (G == 4) ABCD_TRY((hipError_t)pk.add(cw.b_ih, GH, 1, GH, false, w.bcomb, GH, 1, GH, cw.b_hh));
+    else ABCD_TRY((hipError_t)pk.add(cw.b_ih, GH, 1, GH, false, w.bcomb, GH, 1, GH));
+    ABCD_TRY((hipError_t)pk.add(p->mu.w1, H, Hm, H, false, w.W1cat, H, Hm, H));
+    ABCD_TRY((hipError_t)pk.add(p->lv.w1, H, Hm, H, false, w.W1cat + (size_t)Hm * H, H, Hm, H));
+    ABCD_TRY((hipError_t)pk.add(p->mu.b1, Hm, 1, Hm, false, w.b1cat, Hm, 1, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->lv.b1, Hm, 1, Hm, false, w.b1cat + Hm, Hm, 1, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->mu.w2, Hm, F, Hm, false, w.W2mp, Hm, Fp, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->lv.w2, Hm, F, Hm, false, w.W2lp, Hm, Fp, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->mu.b2, F, 1, F, false, w.b2mp, Fp, 1, Fp));
+    ABCD_TRY((hipError_t)pk.add(p->lv.b2, F, 1, F, false, w.b2lp, Fp, 1, Fp));
+    ABCD_TRY((hipError_t)pk.flush());
+  }
   // ---- feature2hidden -> initial state ----
   const float* FS = features;
   if (S > 0) {
@@ -1064,14 +1068,18 @@ extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const ab
   float* sc = w.scratch;
   const size_t scf = w.scratch_floats;
   // ---- derived transposed weights for the backward GEMMs ----
-  ABCD_TRY((hipError_t)pack2d(s, cw.w_ih, F, F, GH, true, w.WihTp, GH, Fp, GH));  // rows >= F zero
-  ABCD_TRY((hipError_t)pack2d(s, cw.w_hh, H, H, GH, true, w.WhhT, GH, H, GH));
-  ABCD_TRY((hipError_t)pack2d(s, p->mu.w2, Hm, Hm, F, true, w.W2mT, Fp, Hm, Fp));
-  ABCD_TRY((hipError_t)pack2d(s, p->lv.w2, Hm, Hm, F, true, w.W2lT, Fp, Hm, Fp));
-  ABCD_TRY((hipError_t)pack2d(s, p->mu.w1, H, H, Hm, true, w.W1catT, 2 * Hm, H, Hm));
-  ABCD_TRY((hipError_t)pack2d(s, p->lv.w1, H, H, Hm, true, w.W1catT + Hm, 2 * Hm, H, Hm));
-  ABCD_TRY((hipError_t)pack2d(s, p->offset.w1, H, H, Hm, true, w.W1oT, Hm, H, Hm));
-  ABCD_TRY((hipError_t)pack2d(s, p->f2h_w, DS, DS, Htot, true, w.Wf2hT, Htot, DS, Htot));
+  {
+    Packs pk(s);
+    ABCD_TRY((hipError_t)pk.add(cw.w_ih, F, F, GH, true, w.WihTp, GH, Fp, GH));  // rows >= F zero
+    ABCD_TRY((hipError_t)pk.add(cw.w_hh, H, H, GH, true, w.WhhT, GH, H, GH));
+    ABCD_TRY((hipError_t)pk.add(p->mu.w2, Hm, Hm, F, true, w.W2mT, Fp, Hm, Fp));
+    ABCD_TRY((hipError_t)pk.add(p->lv.w2, Hm, Hm, F, true, w.W2lT, Fp, Hm, Fp));
+    ABCD_TRY((hipError_t)pk.add(p->mu.w1, H, H, Hm, true, w.W1catT, 2 * Hm, H, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->lv.w1, H, H, Hm, true, w.W1catT + Hm, 2 * Hm, H, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->offset.w1, H, H, Hm, true, w.W1oT, Hm, H, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->f2h_w, DS, DS, Htot, true, w.Wf2hT, Htot, DS, Htot));
+    ABCD_TRY((hipError_t)pk.flush());
+  }
   // ---- offset head backward (batched over all frames) ----
   dec_offset_bwd<<<launch_grid((long)L * Hm), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, w.dlog_raw, d_off, w.dZo,
                                                            w.dlog_s);

@@ -580,6 +580,7 @@ extern "C" int abcd_sampler_backward(const abcd_sampler_cfg* c, const abcd_sampl
 // One wave per row (rows dealt round-robin over the waves); each wave keeps
 // its own column-sum row in LDS (no atomics, deterministic), summed over the
 // waves at the end.
+template <int KPL>
 __global__ __launch_bounds__(1024) void perplex_kernel(const float* logits, int B, int K, const float* psl,
                                                        float* out) {
   extern __shared__ __attribute__((aligned(16))) float colsum_sh[];  // nw x K floats
@@ -589,24 +590,44 @@ __global__ __launch_bounds__(1024) void perplex_kernel(const float* logits, int 
   float* mine = colsum_sh + (long)wv * K;
   for (int k = lane; k < K; k += 64) mine[k] = 0.f;
   double ent = 0.0;
-  for (int b = wv; b < B; b += nw) {
-    const float* l = logits + (long)b * K;
-    float m = -INFINITY;
-    for (int k = lane; k < K; k += 64) m = fmaxf(m, l[k]);
-    m = wave_max(m);
-    float s = 0.f;
-    for (int k = lane; k < K; k += 64) s += __expf(l[k] - m);
-    s = wave_sum(s);
-    const float ls = __logf(s), inv = 1.0f / s;
-    float e = 0.f;
-    for (int k = lane; k < K; k += 64) {
-      const float z = l[k] - m;
-      const float q = __expf(z) * inv;
-      e += -q * (z - ls);
-      mine[k] += q;
+  // PR rows per wave in flight: every row's K values (KPL per lane) are loaded
+  // before any is reduced, so the wave pays one memory latency per PR rows
+  constexpr int PR = 4;
+  for (int b0 = wv * PR; b0 < B; b0 += nw * PR) {
+    float v[PR][KPL];
+#pragma unroll
+    for (int rr = 0; rr < PR; ++rr)
+#pragma unroll
+      for (int u = 0; u < KPL; ++u) {
+        const int k = lane + 64 * u;
+        v[rr][u] = (b0 + rr < B && k < K) ? logits[(long)(b0 + rr) * K + k] : -INFINITY;
+      }
+#pragma unroll
+    for (int rr = 0; rr < PR; ++rr) {
+      if (b0 + rr >= B) break;
+      float m = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < KPL; ++u) m = fmaxf(m, v[rr][u]);
+      m = wave_max(m);
+      float sm = 0.f;
+#pragma unroll
+      for (int u = 0; u < KPL; ++u) sm += lane + 64 * u < K ? __expf(v[rr][u] - m) : 0.f;
+      sm = wave_sum(sm);
+      const float ls = __logf(sm), inv = 1.0f / sm;
+      float e = 0.f;
+#pragma unroll
+      for (int u = 0; u < KPL; ++u) {
+        const int k = lane + 64 * u;
+        if (k < K) {
+          const float z = v[rr][u] - m;
+          const float qq = __expf(z) * inv;
+          e += -qq * (z - ls);
+          mine[k] += qq;
+        }
+      }
+      e = wave_sum(e);
+      ent += e;
     }
-    e = wave_sum(e);
-    ent += e;
   }
   if (lane == 0) sh[wv] = ent;
   __syncthreads();
@@ -673,7 +694,12 @@ extern "C" int abcd_perplexities(const float* logits, int B, int K, const float*
   int nw = 16;
   while (nw > 1 && (size_t)nw * K * sizeof(float) > 65536) nw >>= 1;
   if ((size_t)nw * K * sizeof(float) > 160 * 1024) return ABCD_EINVAL;
-  perplex_kernel<<<1, 64 * nw, (size_t)nw * K * sizeof(float), s>>>(logits, B, K, psl, out);
+  const size_t lds = (size_t)nw * K * sizeof(float);
+  if (K <= 64) perplex_kernel<1><<<1, 64 * nw, lds, s>>>(logits, B, K, psl, out);
+  else if (K <= 128) perplex_kernel<2><<<1, 64 * nw, lds, s>>>(logits, B, K, psl, out);
+  else if (K <= 256) perplex_kernel<4><<<1, 64 * nw, lds, s>>>(logits, B, K, psl, out);
+  else if (K <= 1024) perplex_kernel<16><<<1, 64 * nw, lds, s>>>(logits, B, K, psl, out);
+  else return ABCD_EINVAL;
   ABCD_CHECK_LAUNCH();
   return 0;
 }
