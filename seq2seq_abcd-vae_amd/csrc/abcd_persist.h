@@ -114,7 +114,12 @@ int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst);
 int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched);
 // the same with the input projection fused (PFwdDir::X/Wih/bih set; layer 0)
 int persist_encoder_fwd_fused(hipStream_t s, int G, const PFwdArgs& a, bool* launched);
-int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched);
+// zeroed (may be null): recorded on s between the counter reset and the launch
+// (split-K form only; with it set the gather form declines, *launched = false)
+int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched, hipEvent_t zeroed = nullptr);
+// on stream s: wait until the first ngroups group counters of a running
+// persistent launch reach target (call after waiting on its `zeroed` event)
+int gate_persist(hipStream_t s, const unsigned* sync, int ngroups, unsigned target);
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched);
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched);
 

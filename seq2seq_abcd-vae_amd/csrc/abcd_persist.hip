@@ -690,7 +690,10 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
     }
     PSTAMP(3);
     group_publish(cnt);
-    // stashes for the weight-gradient GEMMs (plain stores, after the publish)
+    // stashes for the weight-gradient GEMMs, after the publish; write-through
+    // (sc1) so that a gated GEMM running beside this launch (abcd_encoder_
+    // backward_overlap) reads them from memory once the NEXT publish -- whose
+    // vmcnt(0) drains them -- has been counted
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int b = row0 + 4 * q + g;
@@ -698,11 +701,11 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
       const long rr = o + b;
       float* dx = D.dGX + rr * GH;
 #pragma unroll
-      for (int j = 0; j < G; ++j) dx[j * H + unit] = dgx[g][j];
+      for (int j = 0; j < G; ++j) st_sc1(dx + j * H + unit, dgx[g][j]);
       if (G == 3) {
         float* dhh = D.dGH + rr * GH;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) dhh[j * H + unit] = dgh[g][j];
+        for (int j = 0; j < 3; ++j) st_sc1(dhh + j * H + unit, dgh[g][j]);
       }
     }
     PSTAMP(4);
@@ -1750,13 +1753,14 @@ int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched)
 }
 
 template <int G, int NSUB>
-static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
+static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched, hipEvent_t zeroed) {
   const int grid = a.nd * a.nrt * NSUB;
   const size_t lds = (size_t)NSUB * 2 * 3 * 64 * 16 + (size_t)4 * 16 * SK_PITCH * 4;
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(enc_bwd_sk<G, NSUB>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
+  if (zeroed) ABCD_TRY(hipEventRecord(zeroed, s));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
@@ -1774,19 +1778,44 @@ static bool splitk_enabled() {
   return !(v && v[0] == '0');
 }
 
-int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
+// gate for work queued beside a persistent launch: one wave polls the first
+// `ngroups` group counters (sc1 loads) until each reaches `target` (bounded)
+__global__ void gate_counters(const unsigned* sync, int ngroups, unsigned target) {
+  const int lane = threadIdx.x;
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
+    if (lane < ngroups)
+      ok = __hip_atomic_load(sync + lane * PERSIST_SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(8);
+    if (++spins > (1u << 22)) {
+      if (lane == 0) __hip_atomic_store(&g_persist_status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+}
+int gate_persist(hipStream_t s, const unsigned* sync, int ngroups, unsigned target) {
+  if (ngroups > 64) return (int)hipErrorInvalidValue;
+  gate_counters<<<1, 64, 0, s>>>(sync, ngroups, target);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched, hipEvent_t zeroed) {
   *launched = false;
   if (!persist_enabled()) return 0;
   if (x6_enabled(a.H) && a.part && splitk_enabled()) {
     if (G == 4) {
-      if (a.H == 64) return launch_bwd_sk<4, 4>(s, a, launched);
-      if (a.H == 128) return launch_bwd_sk<4, 8>(s, a, launched);
-      return launch_bwd_sk<4, 16>(s, a, launched);
+      if (a.H == 64) return launch_bwd_sk<4, 4>(s, a, launched, zeroed);
+      if (a.H == 128) return launch_bwd_sk<4, 8>(s, a, launched, zeroed);
+      return launch_bwd_sk<4, 16>(s, a, launched, zeroed);
     }
-    if (a.H == 64) return launch_bwd_sk<3, 4>(s, a, launched);
-    if (a.H == 128) return launch_bwd_sk<3, 8>(s, a, launched);
-    return launch_bwd_sk<3, 16>(s, a, launched);
+    if (a.H == 64) return launch_bwd_sk<3, 4>(s, a, launched, zeroed);
+    if (a.H == 128) return launch_bwd_sk<3, 8>(s, a, launched, zeroed);
+    return launch_bwd_sk<3, 16>(s, a, launched, zeroed);
   }
+  if (zeroed) return 0;  // the gather-form kernels keep plain stash stores: no gated overlap
   if (x6_enabled(a.H)) {
     if (G == 4) {
       if (a.H == 64) return launch_bwd<4, 16, 8>(s, a, launched);

@@ -469,9 +469,18 @@ extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encode
   return 0;
 }
 
+static int fork_event(hipEvent_t* ev, int slot);
+
 extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encoder_params* p, const abcd_packed* x,
                                      const float* d_last_hidden, const abcd_encoder_grads* g, void* ws,
                                      size_t ws_bytes, void* stream) {
+  return abcd_encoder_backward_overlap(c, p, x, d_last_hidden, g, ws, ws_bytes, stream, nullptr);
+}
+
+extern "C" int abcd_encoder_backward_overlap(const abcd_encoder_cfg* c, const abcd_encoder_params* p,
+                                             const abcd_packed* x, const float* d_last_hidden,
+                                             const abcd_encoder_grads* g, void* ws, size_t ws_bytes, void* stream,
+                                             void* wgrad_stream) {
   ABCD_REQUIRE(enc_check(c) == 0 && p && x && x->data && g && ws && d_last_hidden);
   ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
   hipStream_t s = (hipStream_t)stream;
@@ -484,6 +493,14 @@ extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encod
   const std::vector<int> off = step_offsets(x->batch_sizes, T);
   const int64_t* bs = x->batch_sizes;
   const int TN = bwd_tn(H);
+  const hipStream_t s2 = (hipStream_t)wgrad_stream;
+  // opt-in (ABCD_ENCGATE=1): measured at c2 it gains nothing -- the side stream
+  // is busy with the decoder's weight gradients until ~1.8 ms into the 2.2 ms
+  // encoder BPTT, and the extra co-running GEMMs slow the BPTT by about what
+  // they hide (14.59 vs 14.59 ms/step)
+  const bool gate_ok = s2 && s2 != s && c->layers == 1 && D == 2 && persist_enabled() && T >= 8 &&
+                       getenv("ABCD_ENCGATE") && getenv("ABCD_ENCGATE")[0] == '1';
+  bool gated = false;
   for (int l = c->layers - 1; l >= 0; --l) {
     const int In = l == 0 ? F : D * H;
     for (int d = 0; d < D; ++d)
@@ -506,7 +523,14 @@ extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encod
         b.rev = d == 1;
       }
       if (l == c->layers - 1 && persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
-      ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done));
+      // gated overlap (single layer, side stream given): the weight gradients
+      // of the rows the BPTT finishes in its first half run on wgrad_stream
+      // beside the second half (split-K kernel only: write-through stashes)
+      hipEvent_t zeroed = nullptr;
+      if (gate_ok) ABCD_TRY((hipError_t)fork_event(&zeroed, 1));
+      ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done, zeroed));
+      if (gate_ok && !done) ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done));  // gather form
+      else if (gate_ok && done) gated = true;
     }
     for (int i = 0; i < T && !done; ++i) {
       BwdArgs a{};
@@ -544,21 +568,48 @@ extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encod
       if (G == 4) ABCD_TRY((hipError_t)launch_bwd_step<4>(s, a, grid, H));
       else ABCD_TRY((hipError_t)launch_bwd_step<3>(s, a, grid, H));
     }
-    // weight gradients: reductions over all L packed frames (K = L, K-major operands)
-    for (int d = 0; d < D; ++d) {
+    // weight gradients: reductions over all L packed frames (K = L, K-major
+    // operands), over the row range [r0, r1) into the gradient with weight beta
+    auto wgrad = [&](hipStream_t st, int d, int r0, int r1, float beta, float* scratch, size_t scf) -> int {
       const abcd_rnn_g& gr = g->g[l][d];
       const float* X = l == 0 ? w.Xp : w.Y[l - 1];  // Xp: the padded copy made by the forward
       const long ldxx = l == 0 ? rup16(F) : (long)D * H;
+      const int K = r1 - r0;
+      const float* dGX = w.dGX[l][d] + (size_t)r0 * GH;
+      const float* dGH = w.dGH[l][d] + (size_t)r0 * GH;
       if (gr.w_ih)
-        ABCD_TRY((hipError_t)gemm(s, GH, In, L, opKM(w.dGX[l][d], GH, GH), opKM(X, ldxx, In), gr.w_ih, In, 1.f, 0.f,
-                                  nullptr, ACT_NONE, w.scratch, w.scratch_floats));
+        ABCD_TRY((hipError_t)gemm(st, GH, In, K, opKM(dGX, GH, GH), opKM(X + (size_t)r0 * ldxx, ldxx, In), gr.w_ih,
+                                  In, 1.f, beta, nullptr, ACT_NONE, scratch, scf));
       if (gr.w_hh)
-        ABCD_TRY((hipError_t)gemm(s, GH, H, L, opKM(w.dGH[l][d], GH, GH), opKM(w.Hprev[l][d], H, H), gr.w_hh, H,
-                                  1.f, 0.f, nullptr, ACT_NONE, w.scratch, w.scratch_floats));
-      if (gr.b_ih)
-        ABCD_TRY((hipError_t)colsum(s, w.dGX[l][d], GH, L, GH, nullptr, gr.b_ih, 0.f, w.scratch, w.scratch_floats));
-      if (gr.b_hh)
-        ABCD_TRY((hipError_t)colsum(s, w.dGH[l][d], GH, L, GH, nullptr, gr.b_hh, 0.f, w.scratch, w.scratch_floats));
+        ABCD_TRY((hipError_t)gemm(st, GH, H, K, opKM(dGH, GH, GH), opKM(w.Hprev[l][d] + (size_t)r0 * H, H, H),
+                                  gr.w_hh, H, 1.f, beta, nullptr, ACT_NONE, scratch, scf));
+      if (gr.b_ih) ABCD_TRY((hipError_t)colsum(st, dGX, GH, K, GH, nullptr, gr.b_ih, beta, scratch, scf));
+      if (gr.b_hh) ABCD_TRY((hipError_t)colsum(st, dGH, GH, K, GH, nullptr, gr.b_hh, beta, scratch, scf));
+      return 0;
+    };
+    if (gated) {
+      // rows finished by BPTT step im (both directions): the forward direction
+      // runs t = T-1 .. 0 (rows [off[T-1-im], L) done), the reverse t = 0 ..
+      // (rows [0, off[im+1]) done).  Their stashes are in memory once every
+      // group counter reached 16 * (im + 2) (the next publish drained them).
+      const int im = T / 2, nut = H / 16, ng = 2 * cdiv(x->B, PERSIST_ROWS);
+      const int f0 = off[T - 1 - im], r1 = off[im + 1];
+      hipEvent_t zeroed = nullptr, done_a = nullptr;
+      ABCD_TRY((hipError_t)fork_event(&zeroed, 1));
+      ABCD_TRY((hipError_t)fork_event(&done_a, 2));
+      ABCD_TRY(hipStreamWaitEvent(s2, zeroed, 0));
+      ABCD_TRY((hipError_t)gate_persist(s2, w.sync, ng, (unsigned)(nut * (im + 2))));
+      {
+        GemmSideScope side_tiles(true);
+        ABCD_TRY((hipError_t)wgrad(s2, 0, f0, L, 0.f, w.scratch, w.scratch_floats));
+        ABCD_TRY((hipError_t)wgrad(s2, 1, 0, r1, 0.f, w.scratch, w.scratch_floats));
+      }
+      ABCD_TRY(hipEventRecord(done_a, s2));
+      ABCD_TRY(hipStreamWaitEvent(s, done_a, 0));
+      ABCD_TRY((hipError_t)wgrad(s, 0, 0, f0, 1.f, w.scratch, w.scratch_floats));
+      ABCD_TRY((hipError_t)wgrad(s, 1, r1, L, 1.f, w.scratch, w.scratch_floats));
+    } else {
+      for (int d = 0; d < D; ++d) ABCD_TRY((hipError_t)wgrad(s, d, 0, L, 0.f, w.scratch, w.scratch_floats));
     }
     if (l > 0) {  // dX of this layer = dh of the layer below (both directions)
       for (int d = 0; d < D; ++d) {
@@ -1024,17 +1075,18 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
   return 0;
 }
 
-// one reusable "data-gradient path done" event per device (re-recorded each
-// call: hipStreamWaitEvent captures the record that precedes it)
-static int fork_event(hipEvent_t* ev) {
+// reusable cross-stream events per device and slot (re-recorded each call:
+// hipStreamWaitEvent captures the record that precedes it).  Slot 0: decoder
+// data-gradient path done; 1: encoder counters zeroed; 2: encoder chunk A done.
+static int fork_event(hipEvent_t* ev, int slot) {
   static std::mutex mu;
-  static hipEvent_t evs[64] = {};
+  static hipEvent_t evs[64][3] = {};
   int dev = 0;
   ABCD_TRY(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
+  if (dev < 0 || dev >= 64 || slot < 0 || slot >= 3) return (int)hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lk(mu);
-  if (!evs[dev]) ABCD_TRY(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming));
-  *ev = evs[dev];
+  if (!evs[dev][slot]) ABCD_TRY(hipEventCreateWithFlags(&evs[dev][slot], hipEventDisableTiming));
+  *ev = evs[dev][slot];
   return 0;
 }
 
@@ -1159,7 +1211,7 @@ extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const ab
   const bool side = wgrad_stream && wgrad_stream != stream;
   if (side) {
     hipEvent_t ev;
-    ABCD_TRY((hipError_t)fork_event(&ev));
+    ABCD_TRY((hipError_t)fork_event(&ev, 0));
     ABCD_TRY(hipEventRecord(ev, s));
     s = (hipStream_t)wgrad_stream;
     ABCD_TRY(hipStreamWaitEvent(s, ev, 0));

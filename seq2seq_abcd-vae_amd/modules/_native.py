@@ -84,6 +84,8 @@ _SIGS = {
                                      c_void_p]),
     "abcd_encoder_backward": (c_int, [_P(EncoderCfg), _P(EncoderParams), _P(Packed), c_void_p, _P(EncoderGrads),
                                       c_void_p, c_size_t, c_void_p]),
+    "abcd_encoder_backward_overlap": (c_int, [_P(EncoderCfg), _P(EncoderParams), _P(Packed), c_void_p,
+                                              _P(EncoderGrads), c_void_p, c_size_t, c_void_p, c_void_p]),
     "abcd_sampler_workspace_bytes": (c_size_t, [_P(SamplerCfg), c_int]),
     "abcd_sampler_forward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_void_p, c_void_p,
                                      c_size_t, c_void_p]),

@@ -180,8 +180,9 @@ class FusedStep:
         N.check(L_.abcd_sampler_backward(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, float(entire_data_size),
                                          N.ptr(d_feats), N.ptr(inv), N.ptr(d_h), self.samp_g, N.ptr(ws_s),
                                          ws_s.numel(), st), "sampler backward")
-        N.check(L_.abcd_encoder_backward(self.enc_cfg, self.enc_p, pk, N.ptr(d_h), self.enc_g, N.ptr(ws_e),
-                                         ws_e.numel(), st), "encoder backward")
+        N.check(L_.abcd_encoder_backward_overlap(self.enc_cfg, self.enc_p, pk, N.ptr(d_h), self.enc_g, N.ptr(ws_e),
+                                                 ws_e.numel(), st, N.c_void_p(side.cuda_stream)),
+                "encoder backward")
         torch.cuda.current_stream(dev).wait_stream(side)
         return sc, logits
 

@@ -147,11 +147,12 @@ def test_fused_step_persist_vs_stepwise_bench_size(cfg_name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", ["ABCD_FUSEX", "ABCD_X6GEMM"])
+@pytest.mark.parametrize("knob", ["ABCD_FUSEX", "ABCD_X6GEMM", "ABCD_ENCGATE"])
 def test_opt_in_paths_match_default(knob):
     """The opt-in variants -- input projection fused into the persistent
     encoder kernel (ABCD_FUSEX=1), split-fp32 weight-gradient GEMMs
-    (ABCD_X6GEMM=1) -- give the default path's losses and gradients at c2."""
+    (ABCD_X6GEMM=1), encoder weight gradients gated beside the BPTT
+    (ABCD_ENCGATE=1) -- give the default path's losses and gradients at c2."""
     import bench
     cfg = bench.CONFIGS["c2"]
     step = bench.build(cfg, "cuda")
