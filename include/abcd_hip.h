@@ -85,6 +85,19 @@ int abcd_encoder_backward_overlap(const abcd_encoder_cfg* cfg, const abcd_encode
                                   const float* d_last_hidden, const abcd_encoder_grads* g, void* ws, size_t ws_bytes,
                                   void* stream, void* wgrad_stream);
 
+/* Training-mode inter-layer dropout of nn.LSTM/GRU(dropout = p) (applied by
+ * ATen to the packed output of every layer but the last, model.py:53):
+ * noise is a HOST array of layers - 1 DEVICE pointers, noise[l] = L x dirs*H
+ * values bernoulli(1 - p) / (1 - p) drawn by the caller (in the reference's
+ * RNG order for parity, or abcd_fill_dropout); noise == NULL or noise[l] ==
+ * NULL: no dropout at that boundary.  The backward takes the same noise. */
+int abcd_encoder_forward_dropout(const abcd_encoder_cfg* cfg, const abcd_encoder_params* p, const abcd_packed* x,
+                                 const float* const* noise, float* last_hidden, void* ws, size_t ws_bytes,
+                                 void* stream);
+int abcd_encoder_backward_dropout(const abcd_encoder_cfg* cfg, const abcd_encoder_params* p, const abcd_packed* x,
+                                  const float* const* noise, const float* d_last_hidden, const abcd_encoder_grads* g,
+                                  void* ws, size_t ws_bytes, void* stream, void* wgrad_stream);
+
 /* ------------------------------------------------------------------------
  * ABCDSampler (model.py:538-639) and the plain Gaussian Sampler
  * (plain/modules/model.py:538-567, model.py:17-28)
@@ -254,6 +267,8 @@ int abcd_linear(int M, int N, int K, const float* x, long ldx, const float* W, l
                 float* y, long ldy, void* ws, size_t ws_bytes, void* stream);
 /* n standard normals from Philox-4x32-10(seed, offset + i) */
 int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offset, void* stream);
+/* dropout noise bernoulli(1 - p) / (1 - p) from the same Philox stream */
+int abcd_fill_dropout(float* out, long n, float p, uint64_t seed, uint64_t offset, void* stream);
 /* live device timing of the recurrent kernel family (encoder and decoder,
  * persistent or per-step): HIP events around every launch while enabled;
  * read: out[0] = summed device ms, out[1] = number of launches */

@@ -593,6 +593,26 @@ int Packs::flush() {
   return 0;
 }
 
+__global__ void mul_vec_kernel(const float* a, const float* b, float* y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) y[i] = a[i] * b[i];
+}
+int mul_vec(hipStream_t s, const float* a, const float* b, float* y, long n) {
+  if (n <= 0) return 0;
+  mul_vec_kernel<<<(int)std::min<long>(4096, cdiv(n, 256)), 256, 0, s>>>(a, b, y, n);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+// training-mode dropout noise (nn.Dropout / torch.nn.LSTM(dropout)): bernoulli(1 - p) / (1 - p)
+// from the Philox stream (seed, offset + i)
+__global__ void fill_dropout_kernel(float* out, long n, float keep, float scale, uint64_t seed, uint64_t offset) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    uint32_t o[4];
+    philox4x32(seed, offset + (uint64_t)i, o);
+    out[i] = u01(o[0]) <= keep ? scale : 0.f;
+  }
+}
+
 __global__ void add_vec_kernel(const float* a, const float* b, float* y, int n) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n) y[i] = a[i] + b[i];
@@ -698,4 +718,13 @@ extern "C" int abcd_linear(int M, int N, int K, const float* x, long ldx, const 
   ABCD_TRY((hipError_t)pack2d(s, W, ldw, N, K, false, wp, Kp, N, Kp));
   return gemm(s, M, N, Kp, opKC(xp, Kp, M), opKC(wp, Kp, N), y, ldy, 1.f, 0.f, b, act, wp + (size_t)N * Kp,
               ws_bytes / 4 - need);
+}
+
+extern "C" int abcd_fill_dropout(float* out, long n, float p, uint64_t seed, uint64_t offset, void* stream) {
+  if (!out || n < 0 || !(p >= 0.f && p < 1.f)) return ABCD_EINVAL;
+  if (n == 0) return 0;
+  const float keep = 1.0f - p;
+  abcd::fill_dropout_kernel<<<(int)std::min<long>(4096, abcd::cdiv(n, 256)), 256, 0, (hipStream_t)stream>>>(
+      out, n, keep, 1.0f / keep, seed, offset);
+  return (int)hipGetLastError();
 }

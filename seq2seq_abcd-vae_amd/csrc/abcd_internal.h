@@ -49,6 +49,8 @@ int pack2d(hipStream_t s, const float* src, long lds, int sr, int sc, bool trans
 
 // y = a + b elementwise (n floats)
 int add_vec(hipStream_t s, const float* a, const float* b, float* y, int n);
+// y = a * b elementwise (n floats; y may alias a)
+int mul_vec(hipStream_t s, const float* a, const float* b, float* y, long n);
 
 // A queue of pack2d jobs (optionally dst = src + src2, same layout) issued as
 // one launch by flush() -- or earlier, when the queue is full.

@@ -304,6 +304,7 @@ struct EncWS {
   float* dGH[ABCD_MAX_LAYERS][2];
   float* DC[ABCD_MAX_LAYERS][2];
   float* DHX[ABCD_MAX_LAYERS];
+  float* Ydrop[ABCD_MAX_LAYERS];  // layer output x dropout noise (input of layer l + 1)
   int* off;          // device copy of the step offsets (persistent kernels)
   unsigned* sync;    // persistent-kernel group counters
   float* skp;        // dec_bwd_sk split-K partials
@@ -342,6 +343,7 @@ static EncWS carve_encoder(Arena& A, const abcd_encoder_cfg* c, int T, int L, in
     }
     w.Y[l] = A.f((size_t)L * D * H);
     w.DHX[l] = l + 1 < c->layers ? A.f((size_t)L * D * H) : nullptr;
+    w.Ydrop[l] = l + 1 < c->layers ? A.f((size_t)L * D * H) : nullptr;
     maxMN = std::max(maxMN, (size_t)G * H * std::max(In, H));
   }
   w.GX = A.f((size_t)L * D * G * H);
@@ -372,6 +374,12 @@ extern "C" size_t abcd_encoder_workspace_bytes(const abcd_encoder_cfg* c, int T,
 
 extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encoder_params* p, const abcd_packed* x,
                                     float* last_hidden, void* ws, size_t ws_bytes, void* stream) {
+  return abcd_encoder_forward_dropout(c, p, x, nullptr, last_hidden, ws, ws_bytes, stream);
+}
+
+extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abcd_encoder_params* p,
+                                            const abcd_packed* x, const float* const* noise, float* last_hidden,
+                                            void* ws, size_t ws_bytes, void* stream) {
   ABCD_REQUIRE(enc_check(c) == 0 && p && x && x->data && last_hidden && ws);
   ABCD_REQUIRE(x->F == c->input_size);
   ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
@@ -398,6 +406,10 @@ extern "C" int abcd_encoder_forward(const abcd_encoder_cfg* c, const abcd_encode
     }
     ABCD_TRY((hipError_t)pk.flush());
     const float* X = l == 0 ? w.Xp : w.Y[l - 1];
+    if (l > 0 && noise && noise[l - 1]) {  // nn.LSTM(dropout=p): the layer below's packed output x noise
+      ABCD_TRY((hipError_t)mul_vec(s, w.Y[l - 1], noise[l - 1], w.Ydrop[l - 1], (long)L * D * H));
+      X = w.Ydrop[l - 1];
+    }
     bool done = false;
     {
       PFwdArgs pa{};
@@ -474,13 +486,20 @@ static int fork_event(hipEvent_t* ev, int slot);
 extern "C" int abcd_encoder_backward(const abcd_encoder_cfg* c, const abcd_encoder_params* p, const abcd_packed* x,
                                      const float* d_last_hidden, const abcd_encoder_grads* g, void* ws,
                                      size_t ws_bytes, void* stream) {
-  return abcd_encoder_backward_overlap(c, p, x, d_last_hidden, g, ws, ws_bytes, stream, nullptr);
+  return abcd_encoder_backward_dropout(c, p, x, nullptr, d_last_hidden, g, ws, ws_bytes, stream, nullptr);
 }
 
 extern "C" int abcd_encoder_backward_overlap(const abcd_encoder_cfg* c, const abcd_encoder_params* p,
                                              const abcd_packed* x, const float* d_last_hidden,
                                              const abcd_encoder_grads* g, void* ws, size_t ws_bytes, void* stream,
                                              void* wgrad_stream) {
+  return abcd_encoder_backward_dropout(c, p, x, nullptr, d_last_hidden, g, ws, ws_bytes, stream, wgrad_stream);
+}
+
+extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const abcd_encoder_params* p,
+                                             const abcd_packed* x, const float* const* noise,
+                                             const float* d_last_hidden, const abcd_encoder_grads* g, void* ws,
+                                             size_t ws_bytes, void* stream, void* wgrad_stream) {
   ABCD_REQUIRE(enc_check(c) == 0 && p && x && x->data && g && ws && d_last_hidden);
   ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
   hipStream_t s = (hipStream_t)stream;
@@ -572,7 +591,7 @@ extern "C" int abcd_encoder_backward_overlap(const abcd_encoder_cfg* c, const ab
     // operands), over the row range [r0, r1) into the gradient with weight beta
     auto wgrad = [&](hipStream_t st, int d, int r0, int r1, float beta, float* scratch, size_t scf) -> int {
       const abcd_rnn_g& gr = g->g[l][d];
-      const float* X = l == 0 ? w.Xp : w.Y[l - 1];  // Xp: the padded copy made by the forward
+      const float* X = l == 0 ? w.Xp : ((noise && noise[l - 1]) ? w.Ydrop[l - 1] : w.Y[l - 1]);  // Xp: padded copy
       const long ldxx = l == 0 ? rup16(F) : (long)D * H;
       const int K = r1 - r0;
       const float* dGX = w.dGX[l][d] + (size_t)r0 * GH;
@@ -617,6 +636,8 @@ extern "C" int abcd_encoder_backward_overlap(const abcd_encoder_cfg* c, const ab
         ABCD_TRY((hipError_t)gemm(s, L, In, GH, opKC(w.dGX[l][d], GH, L), opKC(w.WihT[l][d], GH, In), w.DHX[l - 1],
                                   In, 1.f, d == 0 ? 0.f : 1.f, nullptr, ACT_NONE, w.scratch, w.scratch_floats));
       }
+      if (noise && noise[l - 1])  // through the dropout: d(y * noise)/dy = noise
+        ABCD_TRY((hipError_t)mul_vec(s, w.DHX[l - 1], noise[l - 1], w.DHX[l - 1], (long)L * In));
     }
   }
   return 0;

@@ -86,6 +86,10 @@ _SIGS = {
                                       c_void_p, c_size_t, c_void_p]),
     "abcd_encoder_backward_overlap": (c_int, [_P(EncoderCfg), _P(EncoderParams), _P(Packed), c_void_p,
                                               _P(EncoderGrads), c_void_p, c_size_t, c_void_p, c_void_p]),
+    "abcd_encoder_forward_dropout": (c_int, [_P(EncoderCfg), _P(EncoderParams), _P(Packed), c_void_p, c_void_p,
+                                             c_void_p, c_size_t, c_void_p]),
+    "abcd_encoder_backward_dropout": (c_int, [_P(EncoderCfg), _P(EncoderParams), _P(Packed), c_void_p, c_void_p,
+                                              _P(EncoderGrads), c_void_p, c_size_t, c_void_p, c_void_p]),
     "abcd_sampler_workspace_bytes": (c_size_t, [_P(SamplerCfg), c_int]),
     "abcd_sampler_forward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_void_p, c_void_p,
                                      c_size_t, c_void_p]),
@@ -132,6 +136,7 @@ _SIGS = {
     "abcd_timing_read": (c_int, [ctypes.POINTER(c_double)]),
     "abcd_timing_read_kernel": (c_int, [c_int, ctypes.POINTER(c_double)]),
     "abcd_fill_normal": (c_int, [c_void_p, c_long, c_uint64, c_uint64, c_void_p]),
+    "abcd_fill_dropout": (c_int, [c_void_p, c_long, c_float, c_uint64, c_uint64, c_void_p]),
     "abcd_device_status": (c_int, []),
 }
 EXPORTED = sorted(_SIGS)
@@ -182,3 +187,11 @@ def stream():
 
 def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def ptr_array(tensors):
+    """HOST array of device pointers (None entries -> NULL), or None if all None."""
+    if tensors is None or all(t is None for t in tensors):
+        return None
+    arr = (c_void_p * len(tensors))(*[None if t is None else t.data_ptr() for t in tensors])
+    return arr

@@ -135,8 +135,10 @@ class FusedStep:
         dcfg = self.decoder._dcfg(None if train else 1)
         ws_d = self._workspace("dec", L_.abcd_decoder_workspace_bytes(dcfg, T, L, B))
         h = torch.empty(B, self.E, device=dev)
-        N.check(L_.abcd_encoder_forward(self.enc_cfg, self.enc_p, pk, N.ptr(h), N.ptr(ws_e), ws_e.numel(), st),
-                "encoder forward")
+        # inter-layer dropout noise: the step's first RNG draw, as in the reference
+        enc_noise = self.encoder.draw_dropout_noise(L, dev) if train else None
+        N.check(L_.abcd_encoder_forward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(h),
+                                                N.ptr(ws_e), ws_e.numel(), st), "encoder forward")
         W = self.sampler._logit_width()
         logits = torch.empty(B, W, device=dev)
         N.check(L_.abcd_sampler_forward(self.samp_cfg, self.samp_p, N.ptr(h), B, N.ptr(logits), N.ptr(ws_s),
@@ -180,9 +182,9 @@ class FusedStep:
         N.check(L_.abcd_sampler_backward(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, float(entire_data_size),
                                          N.ptr(d_feats), N.ptr(inv), N.ptr(d_h), self.samp_g, N.ptr(ws_s),
                                          ws_s.numel(), st), "sampler backward")
-        N.check(L_.abcd_encoder_backward_overlap(self.enc_cfg, self.enc_p, pk, N.ptr(d_h), self.enc_g, N.ptr(ws_e),
-                                                 ws_e.numel(), st, N.c_void_p(side.cuda_stream)),
-                "encoder backward")
+        N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
+                                                 self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
+                                                 N.c_void_p(side.cuda_stream)), "encoder backward")
         torch.cuda.current_stream(dev).wait_stream(side)
         return sc, logits
 

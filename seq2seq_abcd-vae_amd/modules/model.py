@@ -186,15 +186,16 @@ class RNN_Cell(torch.nn.Module):
 class _EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, enc, data, batch_sizes, *params):
-        out, ws, keep = enc._run_forward(data, batch_sizes)
-        ctx.enc, ctx.ws, ctx.keep = enc, ws, keep
+        noise = enc.draw_dropout_noise(int(data.shape[0]), data.device)
+        out, ws, keep = enc._run_forward(data, batch_sizes, noise=noise)
+        ctx.enc, ctx.ws, ctx.keep, ctx.noise = enc, ws, keep, noise
         ctx.data, ctx.batch_sizes = data, batch_sizes
         return out
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, d_out):
-        grads = ctx.enc._run_backward(ctx.data, ctx.batch_sizes, d_out.contiguous(), ctx.ws)
+        grads = ctx.enc._run_backward(ctx.data, ctx.batch_sizes, d_out.contiguous(), ctx.ws, noise=ctx.noise)
         return (None, None, None) + tuple(grads)
 
 
@@ -230,11 +231,18 @@ class RNN_Variational_Encoder(torch.nn.Module):
                     None if t is None else t.data_ptr() for t in ws]
         return st
 
-    def _check_dropout(self):
-        if self.training and self.rnn.dropout > 0 and self.rnn.num_layers > 1:
-            raise NotImplementedError("inter-layer encoder dropout > 0 in training is not on the HIP path yet")
+    def draw_dropout_noise(self, L, device):
+        """Training-mode inter-layer dropout noise (model.py:53: nn.LSTM/GRU with
+        dropout = hidden_dropout), one L x dirs*H tensor per layer boundary in
+        layer order -- the reference's RNG order within the step -- or None."""
+        p = self.rnn.dropout
+        if not (self.training and p > 0 and self.rnn.num_layers > 1):
+            return None
+        dirs = 2 if self.rnn.bidirectional else 1
+        return [_noise.dropout_noise((L, dirs * self.rnn.hidden_size), p, device)
+                for _ in range(self.rnn.num_layers - 1)]
 
-    def _run_forward(self, data, batch_sizes, ws=None):
+    def _run_forward(self, data, batch_sizes, ws=None, noise=None):
         data = _f32c(data)
         N.require_gpu(data)
         cfg = self._cfg()
@@ -246,11 +254,11 @@ class RNN_Variational_Encoder(torch.nn.Module):
         if ws is None or ws.numel() < nbytes:
             ws = N.workspace(nbytes, data.device)
         out = torch.empty(pk.B, self.hidden_size_total, device=data.device)
-        N.check(L.abcd_encoder_forward(cfg, self._params(), pk, N.ptr(out), N.ptr(ws), ws.numel(), N.stream()),
-                "encoder forward")
+        N.check(L.abcd_encoder_forward_dropout(cfg, self._params(), pk, N.ptr_array(noise), N.ptr(out), N.ptr(ws),
+                                               ws.numel(), N.stream()), "encoder forward")
         return out, ws, (bs, data)
 
-    def _run_backward(self, data, batch_sizes, d_out, ws, grad_views=None):
+    def _run_backward(self, data, batch_sizes, d_out, ws, grad_views=None, noise=None):
         cfg = self._cfg()
         pk, bs = _packed_struct(data, batch_sizes, cfg.input_size)
         dirs = 2 if self.rnn.bidirectional else 1
@@ -259,8 +267,9 @@ class RNN_Variational_Encoder(torch.nn.Module):
             for l in range(self.rnn.num_layers):
                 for d in range(dirs):
                     grad_views[(l, d)] = [torch.empty_like(p) for p in self.rnn.layer_weights(l, d)]
-        N.check(N.lib().abcd_encoder_backward(cfg, self._params(), pk, N.ptr(d_out), self._params(grad_views),
-                                              N.ptr(ws), ws.numel(), N.stream()), "encoder backward")
+        N.check(N.lib().abcd_encoder_backward_dropout(cfg, self._params(), pk, N.ptr_array(noise), N.ptr(d_out),
+                                                      self._params(grad_views), N.ptr(ws), ws.numel(), N.stream(),
+                                                      None), "encoder backward")
         out = []
         for l in range(self.rnn.num_layers):
             for d in range(dirs):
@@ -268,12 +277,11 @@ class RNN_Variational_Encoder(torch.nn.Module):
         return out
 
     def forward(self, packed_input):
-        self._check_dropout()
         data, bsz = packed_input.data, packed_input.batch_sizes
         params = list(self.rnn.parameters())
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
             return _EncoderFn.apply(self, data, bsz, *params)
-        return self._run_forward(data, bsz)[0]
+        return self._run_forward(data, bsz, noise=self.draw_dropout_noise(int(data.shape[0]), data.device))[0]
 
     def pack_init_parameters(self):
         return {"input_size": self.rnn.input_size, "rnn_hidden_size": self.rnn.hidden_size,

@@ -108,3 +108,19 @@ def decoder_eps(batch_sizes, F, device):
         return eps.to(device, non_blocking=True), 0, 0
     s, o = philox(L * F)
     return None, s, o
+
+
+def dropout_noise(shape, p, device):
+    """Training-mode dropout noise bernoulli(1 - p) / (1 - p) of `shape`
+    (ATen's _dropout_impl: ``empty_like(x).bernoulli_(1 - p).div_(1 - p)``):
+    drawn on the host from torch's CPU generator in reference mode (bit-exact
+    with a reference CPU run), from the Philox stream by abcd_fill_dropout
+    otherwise.  Returns a device tensor."""
+    if _state["mode"] == "reference":
+        return torch.empty(*shape).bernoulli_(1 - p).div_(1 - p).to(device, non_blocking=True)
+    from . import _native as N
+    out = torch.empty(*shape, device=device)
+    n = out.numel()
+    s, o = philox(n)
+    N.check(N.lib().abcd_fill_dropout(N.ptr(out), n, float(p), s, o, N.stream()), "dropout noise")
+    return out

@@ -322,6 +322,8 @@ CLI_RUNS = {
     "gru_softmax_e2": ("ABCD-VAE", ["-e", "2", "-b", "4", "-R", "GRU", "-K", "16"]),
     "greedy_e2": ("ABCD-VAE", ["-e", "2", "-b", "4", "-R", "LSTM", "-K", "16", "--greedy_decoder"]),
     "plain_e2": ("plain", ["-e", "2", "-b", "4"]),
+    "lstm2_drop_e2": ("ABCD-VAE", ["-e", "2", "-b", "4", "-R", "LSTM", "-K", "16", "--encoder_rnn_layers", "2",
+                                   "--encoder_hidden_dropout", "0.1"]),
 }
 
 LINE_PATTERNS = {
@@ -360,12 +362,18 @@ def cli_child(variant_dir, script, argv):
     runpy.run_path(os.path.join(REF, variant_dir, script), run_name="__main__")
 
 
-def run_cli():
+def run_cli(only=None):
     root = os.path.join(REF, "toy_data")
     ann = os.path.join(root, "annotation_20170806-080002_89.2-94.22.csv")
+    path = os.path.join(HERE, "toy_known_answers.json")
     results = {}
+    if only and os.path.isfile(path):  # refresh one case, keep the others
+        with open(path) as f:
+            results = json.load(f)
     with tempfile.TemporaryDirectory() as tmp:
         for name, (vdir, flags) in CLI_RUNS.items():
+            if only and name != only:
+                continue
             save_root = os.path.join(tmp, name)
             cmd = [sys.executable, __file__, "--child", vdir, "learning.py", "--",
                    root, ann, "-S", save_root, "-j", "run"] + flags
@@ -387,7 +395,6 @@ def run_cli():
                                                   zip(best["data_ix"], best["category_ix"])}
                 results[name]["encode_maxprob"] = {int(a): float(b) for a, b in
                                                    zip(best["data_ix"], best["prob"])}
-    path = os.path.join(HERE, "toy_known_answers.json")
     with open(path, "w") as f:
         json.dump(results, f, indent=1, sort_keys=True)
     print("wrote", path)
@@ -401,6 +408,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", choices=["small", "toy", "cli"], default=None)
     ap.add_argument("--variant", default=None)
+    ap.add_argument("--case", default=None, help="cli: regenerate only this trajectory")
     a = ap.parse_args()
     if not os.path.isdir(REF):
         sys.exit("reference not present; fixtures are committed, nothing to do")
@@ -418,7 +426,7 @@ def main():
                         "import sys; sys.path.insert(0, %r); import make_golden as m; m.run_toy_step()" % HERE],
                        check=True)
     if a.only in (None, "cli"):
-        run_cli()
+        run_cli(a.case)
 
 
 if __name__ == "__main__":
