@@ -60,6 +60,7 @@ struct PBwdArgs {
 //   emit : mu, lv = Aact W2^T + b2; x = mu + e^{lv/2} eps -> Xin_{t+1}
 struct PDecFwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
+  int flags;                       // hand-off form: 1 per-member flags, 0 group counter
   const int* off;
   unsigned* sync;
   unsigned long long* prof;
@@ -76,6 +77,7 @@ struct PDecFwdArgs {
 //   P2: dh = dZ W1cat + dh_rec + dh_offset -> LSTM cell backward -> dG_t
 struct PDecBwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
+  int flags;                       // hand-off form: 1 per-member flags, 0 group counter
   const int* off;
   unsigned* sync;
   unsigned long long* prof;
@@ -101,8 +103,9 @@ inline size_t persist_part_floats(int nd, int B, int H) {
   return 2 * (size_t)persist_groups(nd, B) * nut * 4 * nut * 256;
 }
 // group counters + the role registry (abcd_persist.hip: 8 XCD ticket lines + 1
-// arrival line) + a second counter per group (dec_bwd_sk: split-K partials drained)
-inline size_t persist_sync_uints(int nd, int B) { return (size_t)(2 * persist_groups(nd, B) + 9) * PERSIST_SYNC_STRIDE; }
+// arrival line) + a second counter per group (dec_bwd_sk: split-K partials
+// drained) + 64 per-member flag lines per group (flag-form hand-offs)
+inline size_t persist_sync_uints(int nd, int B) { return (size_t)(66 * persist_groups(nd, B) + 9) * PERSIST_SYNC_STRIDE; }
 
 // Copy off[0..T] to device memory `dst` on stream s through a pinned ring
 // (asynchronous, no host/device synchronisation).

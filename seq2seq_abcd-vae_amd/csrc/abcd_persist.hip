@@ -125,6 +125,54 @@ DEV void group_publish(unsigned* cnt) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Per-member flag form of the same hand-off (MI355X_MICROARCH.md visibility
+// table row 1 with a sharded counter): member m stores its publish count to
+// its own 128-B line (sc1 store by one lane after every wave's vmcnt(0) drain
+// and a barrier); a waiter's wave 0 polls the group's M lines with one sc1
+// load per lane.  Replaces the M serialized atomic adds on one counter line
+// (~12 ns each at the memory side) by parallel plain write-through stores.
+constexpr int PERSIST_FLAG_LINES = 64;  // flag lines per group (members <= 64)
+DEV void flags_publish(unsigned* fl, int mem, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(fl + mem * PERSIST_SYNC_STRIDE, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV void flags_wait(const unsigned* fl, int M, unsigned epoch) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+      if (lane < M)
+        ok = __hip_atomic_load(fl + lane * PERSIST_SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {
+        if (lane == 0) __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __syncthreads();
+}
+// a group's hand-off in either form (flags unless ABCD_FLAGS=0 at launch)
+struct GSync {
+  unsigned *cnt, *fl;
+  int M, mem, use_flags;
+  unsigned ep;  // publishes so far by this member
+  DEV void wait(unsigned publishes) {
+    if (use_flags) flags_wait(fl, M, publishes);
+    else group_wait(cnt, (unsigned)M * publishes);
+  }
+  DEV void publish() {
+    ++ep;
+    if (use_flags) flags_publish(fl, mem, ep);
+    else group_publish(cnt);
+  }
+};
+
 // diagnostics: thread 0 stamps s_memrealtime (100 MHz, one clock for the whole
 // device, so stamps of different workgroups compare) at the phase boundaries of step i
 #define PSTAMP(k)                                                                                   \
@@ -994,7 +1042,9 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int row0 = rt * PERSIST_ROWS + w * 16;
   const int u0 = mem * 8, unit = u0 + (r & 7);
-  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  GSync gs{a.sync + grp * PERSIST_SYNC_STRIDE,
+           a.sync + ((size_t)2 * a.nrt + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
+           M, mem, a.flags, 0u};
   // emit roles: tile j2 of [mu | lv] columns, row half `half`; wave part 0 = mu, 1 = lv
   const int j2 = mem >> 1, half = mem & 1, part = w >> 1;
   const int erow0 = rt * PERSIST_ROWS + 32 * half + 16 * (w & 1);
@@ -1032,7 +1082,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         cst[g] = b < bs ? a.Cprev[(long)(o + b) * H + unit] : 0.f;
       }
     }
-    if (i > 0) group_wait(cnt, (unsigned)(M * 3 * i));
+    if (i > 0) gs.wait(3u * i);
     PSTAMP(0);
     f4 acc[2];
     acc[0] = acc[1] = f4zero();
@@ -1061,7 +1111,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         else if (b < next_bs) st_ho(a.Hprev + (long)(next_off + b) * H + unit, hv[g], loc);  // -> next cell
       }
     }
-    group_publish(cnt);
+    gs.publish();
     PSTAMP(1);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -1078,7 +1128,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       }
     }
     // ---------------- mlp ----------------
-    group_wait(cnt, (unsigned)(M * (3 * i + 1)));
+    gs.wait(3u * i + 1);
     PSTAMP(2);
     if (has1) {
       f4 a1[1] = {f4zero()};
@@ -1093,7 +1143,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         if (b < bs) st_ho(a.Aact + (long)(o + b) * 2 * Hm + 16 * mem + r, ftanh(a1[0][g] + b1v), loc);
       }
     }
-    group_publish(cnt);
+    gs.publish();
     PSTAMP(3);
     // ---------------- emit ----------------
     // the mu waves' noise, drawn before the wait (independent of the recurrence)
@@ -1108,7 +1158,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         }
       }
     }
-    group_wait(cnt, (unsigned)(M * (3 * i + 2)));
+    gs.wait(3u * i + 2);
     PSTAMP(4);
     float ev[4] = {0.f, 0.f, 0.f, 0.f};  // mu (part 0) / lv (part 1); sample x kept in epre
     if (has2) {
@@ -1136,7 +1186,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         if (b < bs && a.feedback && b < next_bs) st_ho(a.Xin + (long)(next_off + b) * Fp + col2, x, loc);
       }
     }
-    group_publish(cnt);
+    gs.publish();
     if (has2) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1382,7 +1432,9 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int row0 = rt * PERSIST_ROWS + w * 16;
-  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  GSync gs{a.sync + grp * PERSIST_SYNC_STRIDE,
+           a.sync + ((size_t)2 * a.nrt + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
+           M, mem, a.flags, 0u};
   // second counter: +1 per member once its dh partials of the previous step are drained
   unsigned* cnt2 = a.sync + (a.nrt + PERSIST_REG_LINES + grp) * PERSIST_SYNC_STRIDE;
   const int u0 = mem * 8, unit = u0 + (r & 7);
@@ -1440,7 +1492,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       ey[g] = live ? a.Y[rr * F + col0] : 0.f;
     }
     if (i > 0) {
-      group_wait(cnt, (unsigned)(M * 3 * i));
+      gs.wait(3u * i);
       // the dh partials stored after the previous P2 publish have had a whole
       // hand-off to land: drain and announce them on the second counter
       group_publish(cnt2);
@@ -1465,7 +1517,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
         st_ho(a.dLV + rr * Fp + col0, dlv, loc);
       }
     }
-    group_publish(cnt);
+    gs.publish();
     PSTAMP(1);
     // dh_rec of the own units from step t+1's partials (lane takes column
     // (mem & 1) * 8 + (r & 7) of subtile NXS + mem / 2 from each producer):
@@ -1489,7 +1541,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       const int b = row0 + 4 * q + g;
       zpre[g] = b < bs ? a.Aact[(long)(o + b) * 2 * Hm + 16 * mem + r] : 0.f;
     }
-    group_wait(cnt, (unsigned)(M * (3 * i + 1)));
+    gs.wait(3u * i + 1);
     PSTAMP(2);
     {
       f4 acc[2][1];
@@ -1506,7 +1558,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
         st_ho(a.dZ + (long)(o + b) * 2 * Hm + 16 * mem + r, acc[0][0][g] * (1.f - zpre[g] * zpre[g]), loc);
       }
     }
-    group_publish(cnt);
+    gs.publish();
     PSTAMP(3);
     // ---------------- P2: dh -> cell backward -> dG_t -> partials ----------------
     float pg[4][4], pc[4], pcp[4], pdho[4];
@@ -1522,7 +1574,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       pcp[g] = live ? a.Cprev[rr * H + unit] : 0.f;
       pdho[g] = live ? a.DHO[rr * H + unit] : 0.f;
     }
-    group_wait(cnt, (unsigned)(M * (3 * i + 2)));
+    gs.wait(3u * i + 2);
     PSTAMP(4);
     f4 acc[1] = {f4zero()};
     if (row0 < bs) {
@@ -1579,7 +1631,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
 #pragma unroll
       for (int s = 0; s < NXS; ++s) partial(s);
     }
-    group_publish(cnt);
+    gs.publish();
     PSTAMP(5);
     if (mk) {
 #pragma unroll
@@ -1655,10 +1707,17 @@ static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
 // the grid never looks evenly spread and every workgroup takes the fallback
 // roles with sc1 hand-off stores.
 static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
-  hipError_t e = hipMemsetAsync(sync, 0, (size_t)(2 * ngroups + PERSIST_REG_LINES) * PERSIST_SYNC_STRIDE * sizeof(unsigned), s);
+  hipError_t e = hipMemsetAsync(
+      sync, 0, (size_t)(2 * ngroups + PERSIST_REG_LINES + PERSIST_FLAG_LINES * ngroups) * PERSIST_SYNC_STRIDE * 4, s);
   const char* v = getenv("ABCD_XCD");
   if (e == hipSuccess && !(v && v[0] == '1')) e = hipMemsetAsync(sync + (size_t)ngroups * PERSIST_SYNC_STRIDE, 1, 1, s);
   return e;
+}
+
+// per-member flag hand-offs unless ABCD_FLAGS=0 (then the group counter)
+static int flags_enabled() {
+  const char* v = getenv("ABCD_FLAGS");
+  return (v && v[0] == '0') ? 0 : 1;
 }
 
 // ring depth: the largest of 16 / 4 / 1 dividing the chunk count
@@ -1850,6 +1909,7 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
+  b.flags = flags_enabled();
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
@@ -1870,6 +1930,7 @@ static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
+  b.flags = flags_enabled();
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
@@ -1910,6 +1971,7 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
+  b.flags = flags_enabled();
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
@@ -1939,6 +2001,7 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
+  b.flags = flags_enabled();
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
