@@ -128,12 +128,13 @@ ODD = dict(workload="odd shapes", F=33, H=48, Hm=32, D=32, K=16, rnn="LSTM", pla
            N=1000, spk=0, sdim=None)
 
 
-@pytest.mark.parametrize("cfg_name", ["c2", "c4", "odd"])
+@pytest.mark.parametrize("cfg_name", ["c2", "c4", "c5", "c5gru", "odd"])
 def test_fused_step_persist_vs_stepwise_bench_size(cfg_name):
     """Whole training step (encoder + sampler + decoder, forward + backward) at
     the benchmark configuration: persistent kernels vs the per-step kernels;
-    "odd": K-chunk counts that are not multiples of the ring depth (H = 48,
-    Fp = 48), two row tiles with a ragged one."""
+    c5 / c5gru: the stress configuration of BASELINE.json (K = 1024, speaker
+    embedding 256, T_max = 512); "odd": K-chunk counts that are not multiples
+    of the ring depth (H = 48, Fp = 48), two row tiles with a ragged one."""
     import bench
     cfg = ODD if cfg_name == "odd" else bench.CONFIGS[cfg_name]
     step = bench.build(cfg, "cuda")
