@@ -224,6 +224,11 @@ __global__ __launch_bounds__(256) void gemm_x6_kernel(const float* __restrict__ 
 // (M = 4H, N = H or Fp, K = L ~ 64k) it is not faster than gemm_tn's fp32
 // MFMA path (300-335 us vs 305 / 200 us): one 120-KiB workgroup per CU leaves
 // too little latency hiding for the staged loads
+static bool lds_nt_disabled() {
+  const char* v = getenv("ABCD_LDSNT");
+  return v && v[0] == '0';
+}
+
 static bool x6_gemm_enabled() {
   const char* v = getenv("ABCD_X6GEMM");
   return v && v[0] == '1';
@@ -307,45 +312,72 @@ static int gemm_launch(hipStream_t s, int M, int N, int K, OA A, OB B, EpiArgs e
 // are demoted to scratch by the compiler).  The grid splits K into fp32 slabs
 // (slab_reduce_kernel).
 // ---------------------------------------------------------------------------
-template <int MR, int NR>
+// AKC / BKC: the operand is K-contiguous instead (element (row, k) at
+// p[row*ld + k], e.g. frames x features): a thread loads 4 consecutive k of
+// one row and stores them transposed into the same [k][row] LDS slab (4
+// conflict-free 4-B writes), so the MFMA loop is shared.  This is the
+// frame-parallel GEMM path (input projection, offset head).
+template <int MR, int NR, bool AKC = false, bool BKC = false>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict__ A, long lda,
                                                       const float* __restrict__ B, long ldb, int K, int kps,
                                                       EpiArgs e) {
   constexpr int BM = 32 * MR, BN = 32 * NR, BK = 16, LA = BM + 4, LB = BN + 4;
   constexpr int AVT = BK * BM / 4, BVT = BK * BN / 4;   // f4 per slab
   constexpr int AV = (AVT + 255) / 256, BV = (BVT + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float As[2][BK * LA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK * LB];
+  __shared__ __attribute__((aligned(16))) float smab[2 * BK * LA + 2 * BK * LB];
+  float* const As = smab;                  // [2][BK * LA]
+  float* const Bs = smab + 2 * BK * LA;    // [2][BK * LB]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
   const int wm = w >> 1, wn = w & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int kb = blockIdx.z * kps, ke = min(K, kb + kps);
   const int M = e.M, N = e.N;
   f4 ra[AV], rb[BV];
+  // slab element -> (k, row) of f4 x: K-major: 4 rows at one k; K-contiguous: 4 k of one row
+  auto gload1 = [&](const float* P, long ld, int R, int r0, int k0, int x, int BR, bool kc) -> f4 {
+    if (kc) {
+      const int row = x / 4, k = 4 * (x % 4);
+      if (r0 + row < R && k0 + k + 4 <= ke) return *reinterpret_cast<const f4*>(P + (long)(r0 + row) * ld + k0 + k);
+      f4 v = f4zero();
+      if (r0 + row < R)
+        for (int s = 0; s < 4; ++s) v[s] = k0 + k + s < ke ? P[(long)(r0 + row) * ld + k0 + k + s] : 0.f;
+      return v;
+    }
+    const int k = x / (BR / 4), row = (x % (BR / 4)) * 4;
+    return (k0 + k < ke && r0 + row < R) ? *reinterpret_cast<const f4*>(P + (long)(k0 + k) * ld + r0 + row) : f4zero();
+  };
   auto gload = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
-      const int x = threadIdx.x + 256 * u, k = x / (BM / 4), m = (x % (BM / 4)) * 4;
-      ra[u] = (x < AVT && k0 + k < ke && m0 + m < M) ? *reinterpret_cast<const f4*>(A + (long)(k0 + k) * lda + m0 + m)
-                                                      : f4zero();
+      const int x = threadIdx.x + 256 * u;
+      ra[u] = x < AVT ? gload1(A, lda, M, m0, k0, x, BM, AKC) : f4zero();
     }
 #pragma unroll
     for (int u = 0; u < BV; ++u) {
-      const int x = threadIdx.x + 256 * u, k = x / (BN / 4), n = (x % (BN / 4)) * 4;
-      rb[u] = (x < BVT && k0 + k < ke && n0 + n < N) ? *reinterpret_cast<const f4*>(B + (long)(k0 + k) * ldb + n0 + n)
-                                                      : f4zero();
+      const int x = threadIdx.x + 256 * u;
+      rb[u] = x < BVT ? gload1(B, ldb, N, n0, k0, x, BN, BKC) : f4zero();
+    }
+  };
+  auto lstore1 = [&](float* S, int LD, int BR, int x, const f4& v, bool kc) {
+    if (kc) {
+      const int row = x / 4, k = 4 * (x % 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) S[(k + s) * LD + row] = v[s];
+    } else {
+      const int k = x / (BR / 4), row = (x % (BR / 4)) * 4;
+      *reinterpret_cast<f4*>(&S[k * LD + row]) = v;
     }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
-      const int x = threadIdx.x + 256 * u, k = x / (BM / 4), m = (x % (BM / 4)) * 4;
-      if (x < AVT) *reinterpret_cast<f4*>(&As[buf][k * LA + m]) = ra[u];
+      const int x = threadIdx.x + 256 * u;
+      if (x < AVT) lstore1(As + buf * BK * LA, LA, BM, x, ra[u], AKC);
     }
 #pragma unroll
     for (int u = 0; u < BV; ++u) {
-      const int x = threadIdx.x + 256 * u, k = x / (BN / 4), n = (x % (BN / 4)) * 4;
-      if (x < BVT) *reinterpret_cast<f4*>(&Bs[buf][k * LB + n]) = rb[u];
+      const int x = threadIdx.x + 256 * u;
+      if (x < BVT) lstore1(Bs + buf * BK * LB, LB, BN, x, rb[u], BKC);
     }
   };
   f4 acc[MR][NR];
@@ -357,8 +389,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict
   for (int k0 = kb; k0 < ke; k0 += BK) {
     const bool more = k0 + BK < ke;
     if (more) gload(k0 + BK);
-    const float* as = As[cur] + wm * 16 * MR + r;
-    const float* bs = Bs[cur] + wn * 16 * NR + r;
+    const float* as = As + cur * BK * LA + wm * 16 * MR + r;
+    const float* bs = Bs + cur * BK * LB + wn * 16 * NR + r;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int k = 4 * q + s;
@@ -376,23 +408,49 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict
     __syncthreads();
     cur ^= 1;
   }
+  // epilogue through a wave-private LDS transpose (the operand slabs are free
+  // after the loop's last barrier): each 16-row strip of the wave's tile goes
+  // out as whole rows of 16-B stores (4 x NR lanes per row) instead of 64-B
+  // row pieces from the accumulator layout
+  constexpr int SW = 16 * NR, SP = SW + 4;  // strip width, pitch (16 x SW floats = 64 NR f4 per strip)
+  float* stg = smab + w * 16 * SP;
+  float* const dst = e.slab ? e.slab + (long)blockIdx.z * M * N : e.C;
+  const long ldd = e.slab ? (long)N : e.ldc;
+  const bool vec = (ldd % 4 == 0) && (((uintptr_t)dst & 15) == 0);
 #pragma unroll
-  for (int i = 0; i < MR; ++i)
+  for (int i = 0; i < MR; ++i) {
 #pragma unroll
     for (int j = 0; j < NR; ++j)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int row = m0 + wm * 16 * MR + 16 * i + 4 * q + g, col = n0 + wn * 16 * NR + 16 * j + r;
-        if (row < M && col < N) {
-          if (e.slab)
-            e.slab[(long)blockIdx.z * M * N + (long)row * N + col] = acc[i][j][g];
-          else
-            e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, acc[i][j][g]);
+      for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < NR; ++p) {
+      const int lr = (lane + 64 * p) / (4 * NR), c4 = (lane + 64 * p) % (4 * NR);
+      const int gcol = n0 + wn * SW + 4 * c4;
+      const int row = m0 + wm * 16 * MR + 16 * i + lr;
+      f4 v = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
+      if (row < M) {
+        if (!e.slab) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (gcol + t < N) v[t] = apply_epi(e, row, gcol + t, v[t]);
         }
+        float* d = dst + (long)row * ldd + gcol;
+        if (vec && gcol + 4 <= N) *reinterpret_cast<f4*>(d) = v;
+        else
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (gcol + t < N) d[t] = v[t];
       }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
-template <int MR, int NR>
+template <int MR, int NR, bool AKC = false, bool BKC = false>
 static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
                           EpiArgs e, float* scratch, size_t scratch_floats) {
   const int BM = 32 * MR, BN = 32 * NR;
@@ -405,7 +463,7 @@ static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, lo
   Z = cdiv(K, kps);
   EpiArgs ek = e;
   if (Z > 1) ek.slab = scratch;
-  gemm_tn_kernel<MR, NR><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek);
+  gemm_tn_kernel<MR, NR, AKC, BKC><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek);
   ABCD_CHECK_LAUNCH();
   if (Z > 1) {
     const long n = (long)M * N;
@@ -443,9 +501,17 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
   }
   if (!A.kmajor) ABCD_REQUIRE(K % 16 == 0 && A.ld % 4 == 0 && ((uintptr_t)A.p % 16) == 0);
   if (!B.kmajor) ABCD_REQUIRE(K % 16 == 0 && B.ld % 4 == 0 && ((uintptr_t)B.p % 16) == 0);
-  if (!A.kmajor && !B.kmajor)
+  if (!A.kmajor && !B.kmajor) {
+    // frame-parallel GEMMs (M = packed frames): LDS-staged tiles, 128 x 256 (measured
+    // ~1.6x the direct-fragment gemm_big at the input-projection shape)
+    if (cdiv(M, 128) * cdiv(N, 128) >= 240 && A.nrows >= M && B.nrows >= N && A.ld % 4 == 0 && B.ld % 4 == 0 &&
+        ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0 && !lds_nt_disabled()) {
+      if (N >= 256) return gemm_tn_launch<4, 8, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
+      return gemm_tn_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
+    }
     return gemm_launch(s, M, N, K, KC{A.p, A.ld, std::min(A.nrows, M)}, KC{B.p, B.ld, std::min(B.nrows, N)}, e,
                        scratch, scratch_floats);
+  }
   if (A.kmajor && !B.kmajor)
     return gemm_launch(s, M, N, K, KM{A.p, A.ld, std::min(A.nrows, M), K}, KC{B.p, B.ld, std::min(B.nrows, N)}, e,
                        scratch, scratch_floats);
