@@ -214,6 +214,23 @@ int abcd_decoder_backward_overlap(const abcd_decoder_cfg* cfg, const abcd_decode
                                   const float* d_em, const float* d_off, float* d_features,
                                   const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream,
                                   void* wgrad_stream);
+/* Training-mode decoder input dropout (RNN_Cell's nn.Dropout, model.py:289,297):
+ * xmask is L x F (DEVICE, packed order) holding bernoulli(1-p)/(1-p) -- the
+ * noise the dropout applies to step t's cell input at rows off[t] .. off[t]+bs_t
+ * (row block 0 multiplies the zero initial input and only keeps the RNG
+ * order).  The sample fed back is mask * x; flatten_out keeps x.  The
+ * backward needs the same xmask.  xmask == NULL: no dropout (eval mode,
+ * p = 0); cfg->feedback must be 1 when xmask is given. */
+int abcd_decoder_forward_dropout(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
+                                 const float* features, const int64_t* speakers, const float* gt_offset,
+                                 const float* eps, const float* xmask, uint64_t seed, uint64_t offset,
+                                 float* flatten_out, float* mu, float* log_var, float* offset_logits, float* losses,
+                                 void* ws, size_t ws_bytes, void* stream);
+int abcd_decoder_backward_dropout(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
+                                  const float* features, const int64_t* speakers, const float* gt_offset,
+                                  const float* xmask, const float* d_em, const float* d_off, float* d_features,
+                                  const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream,
+                                  void* wgrad_stream);
 
 /* ------------------------------------------------------------------------
  * Featurisation + packing on the device: replaces the per-item host path

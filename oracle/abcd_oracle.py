@@ -268,7 +268,7 @@ def gaussian_kl(mu, lv):
 # ----------------------------------------------------------------------------
 # decoder (model.py:147-196)
 # ----------------------------------------------------------------------------
-def decoder_forward(P, feats, batch_sizes, cfg, eps, speakers=None, gt=None, gt_off=None, train=True):
+def decoder_forward(P, feats, batch_sizes, cfg, eps, speakers=None, gt=None, gt_off=None, train=True, xmask=None):
     bsz = [int(b) for b in batch_sizes]
     Hd = cfg["Hdec"]
     F = cfg["F"]
@@ -288,6 +288,8 @@ def decoder_forward(P, feats, batch_sizes, cfg, eps, speakers=None, gt=None, gt_
     hs, mus, lvs, outs = [], [], [], []
     for t, bs in enumerate(bsz):
         xin = x[:bs] if feedback else x[:bs] * 0.0
+        if xmask is not None and train:  # RNN_Cell input dropout, model.py:297 (noise bernoulli(1-p)/(1-p))
+            xin = xin * xmask[off[t]:off[t] + bs]
         if lstm:
             h, c = lstm_cell(xin, h[:bs], c[:bs], *w)
         else:
@@ -324,7 +326,7 @@ def forward_losses(P, batch, cfg, noise, N, pretrain=False, tau=1.0, train=True)
         kl = digamma_kl(P, logits, N)
     em, off, out, (mu, lv), off_logits = decoder_forward(
         P, feats, batch_sizes, cfg, noise["eps"], speakers=batch.get("speakers"),
-        gt=data, gt_off=batch["is_offset"], train=train)
+        gt=data, gt_off=batch["is_offset"], train=train, xmask=noise.get("xmask"))
     B = int(batch_sizes[0])
     loss = (em + off + kl) / B
     return dict(loss=loss, em=em, off=off, kl=kl, last_hidden=last_hidden, logits=logits, feats=feats,

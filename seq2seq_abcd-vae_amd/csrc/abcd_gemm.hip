@@ -565,7 +565,7 @@ __global__ __launch_bounds__(256) void colsum_pass1(const float* Z, long ldz, in
 // pass 2: 64 columns x 4 slice groups per block, 4 independent accumulators
 // per thread (the slice count reaches 256: keep many loads in flight)
 __global__ __launch_bounds__(256) void colsum_pass2(const float* part, int nslices, int ncols, float* out,
-                                                    float beta) {
+                                                    float beta, float* out2) {
   __shared__ float sh[4][64];
   const int cg = threadIdx.x & 63, sg = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + cg;
@@ -582,12 +582,15 @@ __global__ __launch_bounds__(256) void colsum_pass2(const float* part, int nslic
   }
   sh[sg][cg] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (sg == 0 && j < ncols)
-    out[j] = (beta != 0.f ? beta * out[j] : 0.f) + ((sh[0][cg] + sh[1][cg]) + (sh[2][cg] + sh[3][cg]));
+  if (sg == 0 && j < ncols) {
+    const float v = (sh[0][cg] + sh[1][cg]) + (sh[2][cg] + sh[3][cg]);
+    out[j] = (beta != 0.f ? beta * out[j] : 0.f) + v;
+    if (out2) out2[j] = (beta != 0.f ? beta * out2[j] : 0.f) + v;
+  }
 }
 
 int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const float* w, float* out,
-           float beta, float* scratch, size_t scratch_floats) {
+           float beta, float* scratch, size_t scratch_floats, float* out2) {
   if (ncols <= 0) return 0;
   const int cblocks = cdiv(ncols, 64);
   int slices = std::max(1, std::min(cdiv(std::max(nrows, 1), 256), std::max(1, 1024 / cblocks)));
@@ -597,7 +600,7 @@ int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const 
   slices = std::max(1, cdiv(std::max(nrows, 1), rows_per));
   colsum_pass1<<<dim3(cblocks, slices), 256, 0, s>>>(Z, ldz, nrows, ncols, w, rows_per, scratch);
   ABCD_CHECK_LAUNCH();
-  colsum_pass2<<<cdiv(ncols, 64), 256, 0, s>>>(scratch, slices, ncols, out, beta);
+  colsum_pass2<<<cdiv(ncols, 64), 256, 0, s>>>(scratch, slices, ncols, out, beta, out2);
   ABCD_CHECK_LAUNCH();
   return 0;
 }

@@ -39,8 +39,9 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
          float beta, const float* bias, int act, float* scratch, size_t scratch_floats);
 
 // out[j] (+)= sum_r w[r] * Z[r*ldz + j]  (w == null -> 1), j < ncols, r < nrows; deterministic.
+// out2 (optional) receives the same sum with the same beta (e.g. b_ih and b_hh of an LSTM).
 int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const float* w, float* out,
-           float beta, float* scratch, size_t scratch_floats);
+           float beta, float* scratch, size_t scratch_floats, float* out2 = nullptr);
 
 // dst[r*ldd + c] = (r < sr && c < sc) ? src(r, c) : 0 for r < dr, c < dc;
 // src(r,c) = trans ? src[c*lds + r] : src[r*lds + c]

@@ -68,6 +68,7 @@ struct PDecFwdArgs {
   const float *W1, *b1;            // 2Hm x H, 2Hm  ([mu; lv] first layers)
   const float *W2m, *W2l, *b2m, *b2l;  // Fp x Hm (padded rows), Fp
   const float* eps; uint64_t seed, offset;  // explicit noise (rows x F) or Philox stream
+  const float* xmask;              // input-dropout noise of the cell input (rows x F, 0 or 1/(1-p)); null: none
   float *Xin, *Hprev, *Cprev, *Gst, *Cst, *Hs, *Aact, *MU, *LV, *OUT;
 };
 
@@ -87,6 +88,7 @@ struct PDecBwdArgs {
   const float *Gst, *Cst, *Cprev, *MU, *LV, *OUT, *Aact, *DHO;
   const float* Y;                  // target frames (rows x F)
   const float* s_em;               // device scalar: d loss / d emission NLL
+  const float* xmask;              // input-dropout noise (rows x F) of the cell inputs; null: none
   float *dG, *dMU, *dLV, *dZ, *DHR, *DC0;
   float* part;  // split-K partials (dec_bwd_sk): 2 parity slots x groups x (Fp+H)/16 subtiles x 4 waves x H/8 x 256
 };

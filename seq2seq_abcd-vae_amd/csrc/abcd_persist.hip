@@ -944,7 +944,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
     // ---------------- emit ----------------
     // noise of the first owned tile, drawn before the wait (independent of
     // the recurrence); its stash stores go out after the hand-off publish
-    float epre[4] = {0.f, 0.f, 0.f, 0.f}, mu0[4], lv0[4], x0[4];
+    float epre[4] = {0.f, 0.f, 0.f, 0.f}, mpre[4] = {1.f, 1.f, 1.f, 1.f}, mu0[4], lv0[4], x0[4];
     if (n2 > 0) {
       const int col = 16 * mem + r;
 #pragma unroll
@@ -953,6 +953,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
         if (b < bs && col < F) {
           const long rr = o + b;
           epre[g] = a.eps ? a.eps[rr * F + col] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col);
+          if (a.xmask && b < next_bs) mpre[g] = a.xmask[(long)(next_off + b) * F + col];
         }
       }
     }
@@ -987,7 +988,10 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
                                           : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col));
           x = mu + __expf(0.5f * lv) * e;
         }
-        if (b < bs && a.feedback && b < next_bs) st_ho(a.Xin + (long)(next_off + b) * Fp + col, x, loc);
+        if (b < bs && a.feedback && b < next_bs) {
+          const float m = k == 0 ? mpre[g] : ((a.xmask && col < F) ? a.xmask[(long)(next_off + b) * F + col] : 1.f);
+          st_ho(a.Xin + (long)(next_off + b) * Fp + col, x * m, loc);
+        }
         if (k == 0) {
           mu0[g] = mu; lv0[g] = lv; x0[g] = x;
         } else if (b < bs) {
@@ -1147,7 +1151,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     PSTAMP(3);
     // ---------------- emit ----------------
     // the mu waves' noise, drawn before the wait (independent of the recurrence)
-    float epre[4] = {0.f, 0.f, 0.f, 0.f};
+    float epre[4] = {0.f, 0.f, 0.f, 0.f}, mpre[4] = {1.f, 1.f, 1.f, 1.f};
     if (has2 && part == 0 && col2 < F) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1155,6 +1159,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         if (b < bs) {
           const long rr = o + b;
           epre[g] = a.eps ? a.eps[rr * F + col2] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col2);
+          if (a.xmask && b < next_bs) mpre[g] = a.xmask[(long)(next_off + b) * F + col2];
         }
       }
     }
@@ -1183,7 +1188,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         const float lv = LVX[((w & 1) * 16 + 4 * q + g) * 16 + r];
         const float x = col2 < F ? ev[g] + __expf(0.5f * lv) * epre[g] : 0.f;
         epre[g] = x;
-        if (b < bs && a.feedback && b < next_bs) st_ho(a.Xin + (long)(next_off + b) * Fp + col2, x, loc);
+        if (b < bs && a.feedback && b < next_bs) st_ho(a.Xin + (long)(next_off + b) * Fp + col2, x * mpre[g], loc);
       }
     }
     gs.publish();
@@ -1274,7 +1279,8 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
           const int col = 16 * j0 + r;
           float dmu = 0.f, dlv = 0.f;
           if (col < F) {
-            const float dx = acc[0][0][g];
+            float dx = acc[0][0][g];
+            if (a.xmask && b < succ_valid) dx *= a.xmask[(long)(succ_off + b) * F + col];
             const float mu = a.MU[rr * Fp + col], lv = a.LV[rr * Fp + col], ox = a.OUT[rr * Fp + col];
             const float y = a.Y[rr * F + col];
             const float iv = __expf(-lv), d = y - mu;
@@ -1480,7 +1486,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     // ---------------- P0: dx_{t+1} tile -> dMU, dLV ----------------
     // emission operands of the tile: independent of the hand-off, loaded before the wait
     const int col0 = 16 * mem + r;
-    float emu[4], elv[4], eox[4], ey[4];
+    float emu[4], elv[4], eox[4], ey[4], emk[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int b = row0 + 4 * q + g;
@@ -1490,6 +1496,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       elv[g] = live ? a.LV[rr * Fp + col0] : 0.f;
       eox[g] = live ? a.OUT[rr * Fp + col0] : 0.f;
       ey[g] = live ? a.Y[rr * F + col0] : 0.f;
+      emk[g] = (a.xmask && live && b < succ_valid) ? a.xmask[(long)(o + bs + b) * F + col0] : 1.f;
     }
     if (i > 0) {
       gs.wait(3u * i);
@@ -1508,7 +1515,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
         const long rr = o + b;
         float dmu = 0.f, dlv = 0.f;
         if (col0 < F) {
-          const float dxv = dx[g], mu = emu[g], lv = elv[g];
+          const float dxv = dx[g] * emk[g], mu = emu[g], lv = elv[g];
           const float iv = __expf(-lv), d = ey[g] - mu;
           dmu = dxv + s_em * (-d) * iv;
           dlv = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);

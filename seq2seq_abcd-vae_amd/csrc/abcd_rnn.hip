@@ -602,6 +602,11 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       if (gr.w_hh)
         ABCD_TRY((hipError_t)gemm(st, GH, H, K, opKM(dGH, GH, GH), opKM(w.Hprev[l][d] + (size_t)r0 * H, H, H),
                                   gr.w_hh, H, 1.f, beta, nullptr, ACT_NONE, scratch, scf));
+      // LSTM: b_ih and b_hh receive the same sum over dG (one pass, two outputs)
+      if (dGX == dGH && gr.b_ih) {
+        ABCD_TRY((hipError_t)colsum(st, dGX, GH, K, GH, nullptr, gr.b_ih, beta, scratch, scf, gr.b_hh));
+        return 0;
+      }
       if (gr.b_ih) ABCD_TRY((hipError_t)colsum(st, dGX, GH, K, GH, nullptr, gr.b_ih, beta, scratch, scf));
       if (gr.b_hh) ABCD_TRY((hipError_t)colsum(st, dGH, GH, K, GH, nullptr, gr.b_hh, beta, scratch, scf));
       return 0;
@@ -660,6 +665,7 @@ struct EmitFwd {
   const float* Aact; long lda; int Hm, nch;
   const float *W2m, *W2l, *b2m, *b2l;  // padded Fp x Hm, Fp
   const float* eps; uint64_t seed, offset;
+  const float* xmask;  // input dropout of step t+1's cell input (rows x F) or null
   float *MU, *LV, *OUT, *Xin; int F, Fp;
   int off, bs, next_off, next_bs, feedback;
 };
@@ -695,7 +701,10 @@ __global__ __launch_bounds__(256) void dec_emit_fwd(EmitFwd a) {
   a.MU[rr * a.Fp + j] = mu;
   a.LV[rr * a.Fp + j] = lv;
   a.OUT[rr * a.Fp + j] = x;
-  if (a.feedback && b < a.next_bs) a.Xin[(long)(a.next_off + b) * a.Fp + j] = x;
+  if (a.feedback && b < a.next_bs) {
+    const long nr = a.next_off + b;
+    a.Xin[nr * a.Fp + j] = (a.xmask && j < a.F) ? x * a.xmask[nr * a.F + j] : x;
+  }
 }
 
 struct EmitBwdX {
@@ -703,6 +712,7 @@ struct EmitBwdX {
   const float* WihT;                                  // Fp x G*H
   const float *MU, *LV, *OUT, *Y;                     // stash (ld Fp), gt (ld F)
   const float* s_em;                                  // device scalar
+  const float* xmask; int succ_off;                   // input dropout of step t+1's rows (or null)
   float *dMU, *dLV; int F, Fp; int off, bs;
 };
 
@@ -725,7 +735,8 @@ __global__ __launch_bounds__(256) void dec_emit_bwd_x(EmitBwdX a) {
   const long rr = a.off + b;
   float dmu = 0.f, dlv = 0.f;
   if (j < a.F) {
-    const float dx = lds[row * LD + cc];
+    float dx = lds[row * LD + cc];
+    if (a.xmask && b < a.succ_valid) dx *= a.xmask[(long)(a.succ_off + b) * a.F + j];
     const float mu = a.MU[rr * a.Fp + j], lv = a.LV[rr * a.Fp + j], o = a.OUT[rr * a.Fp + j];
     const float y = a.Y[rr * a.F + j];
     const float s = *a.s_em;
@@ -983,7 +994,18 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
                                     const float* eps, uint64_t seed, uint64_t offset, float* flatten_out,
                                     float* mu_out, float* lv_out, float* offset_logits, float* losses, void* ws,
                                     size_t ws_bytes, void* stream) {
+  return abcd_decoder_forward_dropout(c, p, x, features, speakers, gt_offset, eps, nullptr, seed, offset,
+                                      flatten_out, mu_out, lv_out, offset_logits, losses, ws, ws_bytes, stream);
+}
+
+extern "C" int abcd_decoder_forward_dropout(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
+                                            const abcd_packed* x, const float* features, const int64_t* speakers,
+                                            const float* gt_offset, const float* eps, const float* xmask,
+                                            uint64_t seed, uint64_t offset, float* flatten_out, float* mu_out,
+                                            float* lv_out, float* offset_logits, float* losses, void* ws,
+                                            size_t ws_bytes, void* stream) {
   ABCD_REQUIRE(dec_check(c) == 0 && p && x && features && ws);
+  ABCD_REQUIRE(!xmask || c->feedback);
   ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
   ABCD_REQUIRE(c->num_speakers == 0 || (speakers && p->embed_speaker));
   hipStream_t s = (hipStream_t)stream;
@@ -1035,7 +1057,7 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
     pa.Wih = w.Wihp; pa.Whh = cw.w_hh; pa.bias = w.bcomb;
     pa.W1 = w.W1cat; pa.b1 = w.b1cat;
     pa.W2m = w.W2mp; pa.W2l = w.W2lp; pa.b2m = w.b2mp; pa.b2l = w.b2lp;
-    pa.eps = eps; pa.seed = seed; pa.offset = offset;
+    pa.eps = eps; pa.seed = seed; pa.offset = offset; pa.xmask = xmask;
     pa.Xin = w.Xin; pa.Hprev = w.Hprev; pa.Cprev = w.Cprev; pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Hs = w.Hs;
     pa.Aact = w.Aact; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
     if (persist_enabled() && G == 4) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
@@ -1067,7 +1089,7 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
     EmitFwd e{};
     e.Aact = w.Aact; e.lda = 2 * Hm; e.Hm = Hm; e.nch = Hm / 16;
     e.W2m = w.W2mp; e.W2l = w.W2lp; e.b2m = w.b2mp; e.b2l = w.b2lp;
-    e.eps = eps; e.seed = seed; e.offset = offset;
+    e.eps = eps; e.seed = seed; e.offset = offset; e.xmask = xmask;
     e.MU = w.MU; e.LV = w.LV; e.OUT = w.OUT; e.Xin = w.Xin; e.F = F; e.Fp = Fp;
     e.off = off[t]; e.bs = b_t; e.next_off = off[t + 1]; e.next_bs = nb; e.feedback = c->feedback;
     dec_emit_fwd<<<cdiv(b_t, 16) * (Fp / 16), 256, 0, s>>>(e);
@@ -1115,8 +1137,8 @@ extern "C" int abcd_decoder_backward(const abcd_decoder_cfg* c, const abcd_decod
                                      const float* features, const int64_t* speakers, const float* gt_offset,
                                      const float* d_em, const float* d_off, float* d_features,
                                      const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream) {
-  return abcd_decoder_backward_overlap(c, p, x, features, speakers, gt_offset, d_em, d_off, d_features, g, ws,
-                                       ws_bytes, stream, nullptr);
+  return abcd_decoder_backward_dropout(c, p, x, features, speakers, gt_offset, nullptr, d_em, d_off, d_features, g,
+                                       ws, ws_bytes, stream, nullptr);
 }
 
 extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
@@ -1124,7 +1146,17 @@ extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const ab
                                              const float* gt_offset, const float* d_em, const float* d_off,
                                              float* d_features, const abcd_decoder_grads* g, void* ws,
                                              size_t ws_bytes, void* stream, void* wgrad_stream) {
+  return abcd_decoder_backward_dropout(c, p, x, features, speakers, gt_offset, nullptr, d_em, d_off, d_features, g,
+                                       ws, ws_bytes, stream, wgrad_stream);
+}
+
+extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
+                                             const abcd_packed* x, const float* features, const int64_t* speakers,
+                                             const float* gt_offset, const float* xmask, const float* d_em,
+                                             const float* d_off, float* d_features, const abcd_decoder_grads* g,
+                                             void* ws, size_t ws_bytes, void* stream, void* wgrad_stream) {
   ABCD_REQUIRE(dec_check(c) == 0 && p && x && x->data && features && g && ws && d_em && d_off && gt_offset);
+  ABCD_REQUIRE(!xmask || c->feedback);
   ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
   hipStream_t s = (hipStream_t)stream;
   Arena A(ws, ws_bytes);
@@ -1168,7 +1200,7 @@ extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const ab
     pa.off = w.off; pa.sync = w.sync;
     pa.WihT = w.WihTp; pa.WhhT = w.WhhT; pa.W2mT = w.W2mT; pa.W2lT = w.W2lT; pa.W1T = w.W1catT;
     pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Cprev = w.Cprev; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
-    pa.Aact = w.Aact; pa.DHO = w.DHO; pa.Y = x->data; pa.s_em = d_em;
+    pa.Aact = w.Aact; pa.DHO = w.DHO; pa.Y = x->data; pa.s_em = d_em; pa.xmask = xmask;
     pa.dG = w.dGX; pa.dMU = w.dMU; pa.dLV = w.dLV; pa.dZ = w.dZ; pa.DHR = w.DC; pa.DC0 = w.DC0;
     pa.part = w.skp;
     if (persist_enabled() && G == 4) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
@@ -1181,6 +1213,7 @@ extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const ab
     EmitBwdX e{};
     e.Ag = w.dGX + (size_t)off[t + 1] * GH; e.ldg = GH; e.succ_valid = c->feedback ? nb : 0; e.nch = GH / 16;
     e.WihT = w.WihTp; e.MU = w.MU; e.LV = w.LV; e.OUT = w.OUT; e.Y = x->data; e.s_em = d_em;
+    e.xmask = xmask; e.succ_off = t + 1 < T ? off[t + 1] : 0;
     e.dMU = w.dMU; e.dLV = w.dLV; e.F = F; e.Fp = Fp; e.off = off[t]; e.bs = b_t;
     dec_emit_bwd_x<<<cdiv(b_t, 16) * (Fp / 16), 256, 0, s>>>(e);
     ABCD_CHECK_LAUNCH();
@@ -1249,8 +1282,12 @@ extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const ab
   if (cg.w_hh)
     ABCD_TRY((hipError_t)gemm(s, GH, H, L, opKM(w.dGH, GH, GH), opKM(w.Hprev, H, H), cg.w_hh, H, 1.f, 0.f, nullptr,
                               ACT_NONE, sc, scf));
-  if (cg.b_ih) ABCD_TRY((hipError_t)colsum(s, w.dGX, GH, L, GH, nullptr, cg.b_ih, 0.f, sc, scf));
-  if (cg.b_hh) ABCD_TRY((hipError_t)colsum(s, w.dGH, GH, L, GH, nullptr, cg.b_hh, 0.f, sc, scf));
+  if (w.dGX == w.dGH && cg.b_ih) {  // LSTM: one pass for both bias gradients
+    ABCD_TRY((hipError_t)colsum(s, w.dGX, GH, L, GH, nullptr, cg.b_ih, 0.f, sc, scf, cg.b_hh));
+  } else {
+    if (cg.b_ih) ABCD_TRY((hipError_t)colsum(s, w.dGX, GH, L, GH, nullptr, cg.b_ih, 0.f, sc, scf));
+    if (cg.b_hh) ABCD_TRY((hipError_t)colsum(s, w.dGH, GH, L, GH, nullptr, cg.b_hh, 0.f, sc, scf));
+  }
   const abcd_mlp_g* em[2] = {&g->mu, &g->lv};
   const float* dout[2] = {w.dMU, w.dLV};
   for (int k = 0; k < 2; ++k) {

@@ -157,14 +157,16 @@ class FusedStep:
         N.check(L_.abcd_sampler_kl(self.samp_cfg, self.samp_p, N.ptr(logits), B, float(entire_data_size),
                                    N.ptr(sc[KL:KL + 1]), N.ptr(ws_s), ws_s.numel(), st), "sampler kl")
         F = self.decoder.rnn_cell.cell.input_size
-        eps, eseed, eoff = _noise.decoder_eps(bs_keep, F, dev)
+        pdrop = self.decoder._input_dropout_p() if train else 0.0
+        eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
         spk = None
         if self.decoder.embed_speaker is not None:
             spk = speakers.to(dev, torch.int64).contiguous()
         gt_off = is_offset.contiguous()
-        N.check(L_.abcd_decoder_forward(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off), N.ptr(eps),
-                                        eseed, eoff, None, None, None, None, N.ptr(sc[EM:EM + 2]), N.ptr(ws_d),
-                                        ws_d.numel(), st), "decoder forward")
+        N.check(L_.abcd_decoder_forward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
+                                                N.ptr(eps), N.ptr(xmask), eseed, eoff, None, None, None, None,
+                                                N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st),
+                "decoder forward")
         N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), B, N.ptr(sc[LOSS:LOSS + 1]), st),
                 "total loss")
         if not train:
@@ -174,9 +176,9 @@ class FusedStep:
         # the decoder's weight-gradient reductions run on a side stream beside
         # the sampler + encoder backward (joined below, before clip + SGD)
         side = self._side_stream()
-        N.check(L_.abcd_decoder_backward_overlap(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
-                                                 N.ptr(inv), N.ptr(inv), N.ptr(d_feats), self.dec_g, N.ptr(ws_d),
-                                                 ws_d.numel(), st, N.c_void_p(side.cuda_stream)),
+        N.check(L_.abcd_decoder_backward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
+                                                 N.ptr(xmask), N.ptr(inv), N.ptr(inv), N.ptr(d_feats), self.dec_g,
+                                                 N.ptr(ws_d), ws_d.numel(), st, N.c_void_p(side.cuda_stream)),
                 "decoder backward")
         d_h = torch.empty(B, self.E, device=dev)
         N.check(L_.abcd_sampler_backward(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, float(entire_data_size),

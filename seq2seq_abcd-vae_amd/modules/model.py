@@ -646,11 +646,11 @@ class Sampler(_SamplerBase):
 # ----------------------------------------------------------------------------
 class _DecoderFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, dec, features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, *params):
-        res = dec._run_forward(features, batch_sizes, speaker, gt, gt_off, eps, seed, offset)
+    def forward(ctx, dec, features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, xmask, *params):
+        res = dec._run_forward(features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, xmask=xmask)
         em, off, flat, mu, lv, offl, ws = res
         ctx.dec, ctx.ws = dec, ws
-        ctx.saved = (features, batch_sizes, speaker, gt, gt_off)
+        ctx.saved = (features, batch_sizes, speaker, gt, gt_off, xmask)
         ctx.feedback = dec._feedback()
         ctx.mark_non_differentiable(flat, mu, lv, offl)
         ctx.set_materialize_grads(False)
@@ -661,14 +661,14 @@ class _DecoderFn(torch.autograd.Function):
     def backward(ctx, d_em, d_off, d_flat, d_mu, d_lv, d_offl):
         if any(g is not None for g in (d_flat, d_mu, d_lv, d_offl)):
             raise NotImplementedError("decoder backward supports gradients of the emission and offset losses only")
-        features, batch_sizes, speaker, gt, gt_off = ctx.saved
+        features, batch_sizes, speaker, gt, gt_off, xmask = ctx.saved
         dev = features.device
         z = torch.zeros((), device=dev)
         d_em = z if d_em is None else d_em.reshape(()).contiguous()
         d_off = z if d_off is None else d_off.reshape(()).contiguous()
         d_feat, grads = ctx.dec._run_backward(features, batch_sizes, speaker, gt, gt_off, d_em, d_off, ctx.ws,
-                                              feedback=ctx.feedback)
-        return (None, d_feat, None, None, None, None, None, None, None) + tuple(grads)
+                                              feedback=ctx.feedback, xmask=xmask)
+        return (None, d_feat, None, None, None, None, None, None, None, None) + tuple(grads)
 
 
 class RNN_Variational_Decoder(torch.nn.Module):
@@ -707,12 +707,13 @@ class RNN_Variational_Decoder(torch.nn.Module):
 
     # -- native plumbing --
     def _feedback(self):
+        """1: the sample is fed back (eval mode, p < 1); 0: greedy / p = 1 in training (zero input)."""
+        return 0 if (self.training and self.rnn_cell.drop.p >= 1.0) else 1
+
+    def _input_dropout_p(self):
+        """p of the training-mode input dropout that needs noise (0 < p < 1), else 0."""
         p = self.rnn_cell.drop.p
-        if not self.training or p == 0.0:
-            return 1
-        if p == 1.0:
-            return 0
-        raise NotImplementedError("decoder input dropout with 0 < p < 1 in training is not on the HIP path yet")
+        return p if (self.training and 0.0 < p < 1.0) else 0.0
 
     def _dcfg(self, feedback=None):
         c = N.DecoderCfg()
@@ -756,7 +757,7 @@ class RNN_Variational_Decoder(torch.nn.Module):
         return N.lib().abcd_decoder_workspace_bytes(self._dcfg(1), T, L, B)
 
     def _run_forward(self, features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, ws=None,
-                     want_outputs=True):
+                     want_outputs=True, xmask=None):
         features = _f32c(features)
         N.require_gpu(features)
         cfg = self._dcfg()
@@ -779,16 +780,17 @@ class RNN_Variational_Decoder(torch.nn.Module):
             lv = torch.empty(pk.L, F, device=dev)
         offl = torch.empty(pk.L, device=dev)
         losses = torch.zeros(2, device=dev)
-        N.check(L.abcd_decoder_forward(cfg, self._dparams(), pk, N.ptr(features), N.ptr(spk),
-                                       N.ptr(None if gt_off is None else _f32c(gt_off)), N.ptr(eps), seed, offset,
-                                       N.ptr(flat), N.ptr(mu), N.ptr(lv), N.ptr(offl), N.ptr(losses), N.ptr(ws),
-                                       ws.numel(), N.stream()), "decoder forward")
+        N.check(L.abcd_decoder_forward_dropout(cfg, self._dparams(), pk, N.ptr(features), N.ptr(spk),
+                                               N.ptr(None if gt_off is None else _f32c(gt_off)), N.ptr(eps),
+                                               N.ptr(xmask), seed, offset, N.ptr(flat), N.ptr(mu), N.ptr(lv),
+                                               N.ptr(offl), N.ptr(losses), N.ptr(ws), ws.numel(), N.stream()),
+                "decoder forward")
         em = losses[0] if gt is not None else None
         off = losses[1] if gt_off is not None else None
         return em, off, flat, mu, lv, offl, ws
 
     def _run_backward(self, features, batch_sizes, speaker, gt, gt_off, d_em, d_off, ws, grad_tensors=None,
-                      feedback=None, d_features=None):
+                      feedback=None, d_features=None, xmask=None):
         cfg = self._dcfg(feedback)
         pk, bs = _packed_struct(gt, batch_sizes, cfg.output_size)
         dev = features.device
@@ -797,9 +799,10 @@ class RNN_Variational_Decoder(torch.nn.Module):
             grad_tensors = [torch.empty_like(p) for p in self._param_list()]
         if d_features is None:
             d_features = torch.empty_like(features)
-        N.check(N.lib().abcd_decoder_backward(cfg, self._dparams(), pk, N.ptr(features), N.ptr(spk),
-                                              N.ptr(_f32c(gt_off)), N.ptr(d_em), N.ptr(d_off), N.ptr(d_features),
-                                              self._dparams(grad_tensors), N.ptr(ws), ws.numel(), N.stream()),
+        N.check(N.lib().abcd_decoder_backward_dropout(cfg, self._dparams(), pk, N.ptr(features), N.ptr(spk),
+                                                      N.ptr(_f32c(gt_off)), N.ptr(xmask), N.ptr(d_em), N.ptr(d_off),
+                                                      N.ptr(d_features), self._dparams(grad_tensors), N.ptr(ws),
+                                                      ws.numel(), N.stream(), None),
                 "decoder backward")
         return d_features, grad_tensors
 
@@ -812,18 +815,18 @@ class RNN_Variational_Decoder(torch.nn.Module):
         if not torch.is_tensor(batch_sizes):
             batch_sizes = torch.tensor([int(b) for b in batch_sizes], dtype=torch.int64)
         F = self.rnn_cell.cell.input_size
-        eps, seed, offset = _noise.decoder_eps(batch_sizes, F, features.device)
+        eps, seed, offset, xmask = _noise.decoder_noise(batch_sizes, F, self._input_dropout_p(), features.device)
         params = self._param_list()
         gt = ground_truth_out
         gt_off = ground_truth_offset
         if (gt is not None and gt_off is not None and torch.is_grad_enabled()
                 and (features.requires_grad or any(p.requires_grad for p in params))):
             em, off, flat, mu, lv, offl = _DecoderFn.apply(self, features, batch_sizes, speaker, _f32c(gt),
-                                                           gt_off, eps, seed, offset, *params)
+                                                           gt_off, eps, seed, offset, xmask, *params)
         else:
             em, off, flat, mu, lv, offl, _ = self._run_forward(features, batch_sizes, speaker,
                                                                None if gt is None else _f32c(gt), gt_off, eps,
-                                                               seed, offset)
+                                                               seed, offset, xmask=xmask)
         return em, off, flat, (mu, lv), offl
 
     def _length_to_batch_sizes(self, lengths):

@@ -110,6 +110,32 @@ def decoder_eps(batch_sizes, F, device):
     return None, s, o
 
 
+def decoder_noise(batch_sizes, F, p, device):
+    """Noise of one training-mode decoder pass with input dropout p:
+    (eps, seed, offset, xmask).  0 < p < 1 adds the RNN_Cell dropout noise of
+    every step's cell input (model.py:297, ``nn.Dropout(p)`` on
+    ``batched_input[:bs_t]``), an L x F tensor in packed order.  In reference
+    mode the two draws interleave per step exactly as the reference loop makes
+    them (dropout of step t's input, then the sampler's ``randn(bs_t, F)``,
+    model.py:186-188, 19); otherwise eps is a Philox block and the mask comes
+    from abcd_fill_dropout.  Replays pop eps then the mask."""
+    if not (0.0 < p < 1.0):
+        return decoder_eps(batch_sizes, F, device) + (None,)
+    L = int(sum(int(b) for b in batch_sizes))
+    if _replay:
+        eps = _pop((L, F), device)
+        return eps + (_pop((L, F), device)[0],)
+    if _state["mode"] == "reference":
+        masks, eps = [], []
+        for bs in batch_sizes:
+            masks.append(torch.empty(int(bs), F).bernoulli_(1 - p).div_(1 - p))
+            eps.append(torch.randn(int(bs), F))
+        return (torch.cat(eps, 0).to(device, non_blocking=True), 0, 0,
+                torch.cat(masks, 0).to(device, non_blocking=True))
+    eps, s, o = decoder_eps(batch_sizes, F, device)
+    return eps, s, o, dropout_noise((L, F), p, device)
+
+
 def dropout_noise(shape, p, device):
     """Training-mode dropout noise bernoulli(1 - p) / (1 - p) of `shape`
     (ATen's _dropout_impl: ``empty_like(x).bernoulli_(1 - p).div_(1 - p)``):

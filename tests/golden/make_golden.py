@@ -122,6 +122,7 @@ SMALL_VARIANTS = {
     "lstm_2layer": dict(rnn="LSTM", layers=2),
     "lstm_uni": dict(rnn="LSTM", bidirectional=False),
     "lstm_greedy": dict(rnn="LSTM", greedy=True),
+    "lstm_ddrop": dict(rnn="LSTM", input_dropout=0.3),
     "gru_speaker_pretrain": dict(rnn="GRU", speaker=True, pretrain=True),
     "plain_lstm": dict(rnn="LSTM", plain=True),
     "plain_gru": dict(rnn="GRU", plain=True),
@@ -143,6 +144,7 @@ def run_small(name, cfg):
     speaker = cfg.get("speaker", False)
     greedy = cfg.get("greedy", False)
     pretrain = cfg.get("pretrain", False)
+    p_in = cfg.get("input_dropout", 0.0)
     nspk = d["NSPK"] if speaker else None
     sdim = d["S"] if speaker else None
     N_total = 50  # entire_data_size
@@ -170,7 +172,7 @@ def run_small(name, cfg):
         if "tau" in cfg:
             samp.temperature = cfg["tau"]
     dec = model.RNN_Variational_Decoder(F, H, Hm, feat_dim, rnn_type=rnn,
-                                        self_feedback=not greedy,
+                                        self_feedback=not greedy, input_dropout=p_in,
                                         num_speakers=nspk, speaker_embed_dim=sdim)
     modules = [("encoder", enc), ("feature_sampler", samp), ("decoder", dec)]
     out = {}
@@ -186,7 +188,16 @@ def run_small(name, cfg):
         feat_noise = -torch.empty(B, K).exponential_().log()
     else:
         feat_noise = torch.zeros(0)
-    eps = torch.cat([torch.randn(int(bs), F) for bs in batch_sizes], 0)
+    if p_in > 0.0:
+        # RNN_Cell's dropout of step t's input (model.py:297), then the
+        # sampler's randn (model.py:19), per step
+        masks, epss = [], []
+        for bs in batch_sizes:
+            masks.append(torch.empty(int(bs), F).bernoulli_(1 - p_in).div_(1 - p_in))
+            epss.append(torch.randn(int(bs), F))
+        xmask, eps = torch.cat(masks, 0), torch.cat(epss, 0)
+    else:
+        xmask, eps = None, torch.cat([torch.randn(int(bs), F) for bs in batch_sizes], 0)
     torch.set_rng_state(state)
 
     # -------- the Learner.train step body (learning.py:147-163) --------
@@ -237,6 +248,8 @@ def run_small(name, cfg):
         "mu": mu, "lv": lv, "offset_logits": off_logits,
         "total_norm": torch.tensor(total_norm),
     })
+    if xmask is not None:
+        out["xmask"] = xmask
     out.update(grads)
     meta = dict(cfg, name=name, dims=d, N=N_total, lengths=SMALL_LENGTHS, lr=1.0, clip=1.0,
                 temperature=(None if plain else samp.temperature))
@@ -324,6 +337,7 @@ CLI_RUNS = {
     "plain_e2": ("plain", ["-e", "2", "-b", "4"]),
     "lstm2_drop_e2": ("ABCD-VAE", ["-e", "2", "-b", "4", "-R", "LSTM", "-K", "16", "--encoder_rnn_layers", "2",
                                    "--encoder_hidden_dropout", "0.1"]),
+    "ddrop_e2": ("ABCD-VAE", ["-e", "2", "-b", "4", "-R", "LSTM", "-K", "16", "--decoder_input_dropout", "0.3"]),
 }
 
 LINE_PATTERNS = {

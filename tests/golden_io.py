@@ -41,7 +41,7 @@ def noise_from(meta, arr):
     feat = arr["feat_noise"]
     if not meta.get("plain") and meta.get("pretrain"):
         feat = None
-    return dict(feat=feat, eps=arr["eps"])
+    return dict(feat=feat, eps=arr["eps"], xmask=arr.get("xmask"))
 
 
 def known_answers():

@@ -28,6 +28,7 @@ def build_from_meta(meta, arr=None, device="cuda", cfg_override=None):
         if meta.get("temperature"):
             samp.temperature = meta["temperature"]
     dec = M.RNN_Variational_Decoder(F, H, Hm, fdim, rnn_type=rnn, self_feedback=not meta.get("greedy", False),
+                                    input_dropout=meta.get("input_dropout", 0.0),
                                     num_speakers=d["NSPK"] if speaker else None,
                                     speaker_embed_dim=d["S"] if speaker else None)
     if arr is not None:

@@ -21,6 +21,8 @@ def _noise_list(meta, arr):
     if meta.get("plain") or not meta.get("pretrain", False):
         q.append(arr["feat_noise"])
     q.append(arr["eps"])
+    if "xmask" in arr:  # decoder input dropout: replayed after eps (noise.decoder_noise)
+        q.append(arr["xmask"])
     return q
 
 
@@ -58,7 +60,8 @@ def test_fused_step_vs_reference(name, modules_pkg):
         assert rel_err(p, arr["q/" + k]) < 1e-5, k
 
 
-@pytest.mark.parametrize("name", ["lstm_gumbel", "gru_gumbel", "lstm_speaker", "plain_lstm", "lstm_2layer"])
+@pytest.mark.parametrize("name", ["lstm_gumbel", "gru_gumbel", "lstm_speaker", "plain_lstm", "lstm_2layer",
+                                  "lstm_ddrop"])
 def test_module_autograd_vs_reference(name, modules_pkg):
     """The nn.Module surface (encoder(packed) -> sampler -> sample -> kl ->
     decoder -> loss.backward()) on the HIP autograd Functions."""

@@ -171,3 +171,24 @@ def test_opt_in_paths_match_default(knob):
     for k in range(4):
         assert abs(sc_o[k] - sc_d[k]) <= 1e-5 * abs(sc_d[k]) + 1e-6, (k, sc_o[k].item(), sc_d[k].item())
     assert _rel(g_o, g_d) < 1e-4
+
+
+@pytest.mark.parametrize("rnn", ["LSTM", "GRU"])
+def test_decoder_input_dropout_persist_vs_stepwise(rnn):
+    """Decoder input dropout 0 < p < 1 in training (RNN_Cell's nn.Dropout,
+    ABCD-VAE/modules/model.py:289,297) at c2 widths: the persistent decoder
+    kernels (mask applied to the fed-back sample before the hand-off, and to
+    dx in the BPTT's emission epilogue) agree with the per-step kernels, and
+    the mask changes the result (it is applied at all)."""
+    import bench
+    cfg = dict(bench.CONFIGS["c2"], rnn=rnn)
+    step = bench.build(cfg, "cuda")
+    batch = bench.make_batch(cfg, 0, "cuda")
+    sc_0, g_0 = _fused_run(step, batch, True)
+    step.decoder.rnn_cell.drop.p = 0.3
+    sc_p, g_p = _fused_run(step, batch, True)
+    sc_s, g_s = _fused_run(step, batch, False)
+    for k in range(4):
+        assert abs(sc_p[k] - sc_s[k]) <= 1e-5 * abs(sc_s[k]) + 1e-6, (k, sc_p[k].item(), sc_s[k].item())
+    assert _rel(g_p, g_s) < 1e-4
+    assert sc_p[0] != sc_0[0] and _rel(g_p, g_0) > 1e-3
