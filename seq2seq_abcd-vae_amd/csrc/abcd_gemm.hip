@@ -317,10 +317,31 @@ static int gemm_launch(hipStream_t s, int M, int N, int K, OA A, OB B, EpiArgs e
 // one row and stores them transposed into the same [k][row] LDS slab (4
 // conflict-free 4-B writes), so the MFMA loop is shared.  This is the
 // frame-parallel GEMM path (input projection, offset head).
+// XCD-aware tile order: the hardware deals workgroup ids round-robin over
+// the 8 XCDs (id % 8), so tiles that share an operand slab (the M tiles of
+// one K split, the N tiles of one row block) would sit on 8 different L2s and
+// each fetch the slab from HBM.  Remapped, XCD x runs the contiguous logical
+// range [x n/8, (x+1) n/8): neighbours in (x fastest, y, z) order share its L2.
+DEV dim3 xcd_tile(bool remap) {
+  const unsigned gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+  unsigned i = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if (remap && n % 8 == 0) i = (i % 8) * (n / 8) + i / 8;
+  return dim3(i % gx, (i / gx) % gy, i / (gx * gy));
+}
+
+static int gxcd_remap() {
+  static const int v = [] {
+    const char* s = getenv("ABCD_GXCD");
+    return (s && s[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
 template <int MR, int NR, bool AKC = false, bool BKC = false>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict__ A, long lda,
                                                       const float* __restrict__ B, long ldb, int K, int kps,
-                                                      EpiArgs e) {
+                                                      EpiArgs e, int remap) {
+  const dim3 bid = xcd_tile(remap != 0);
   constexpr int BM = 32 * MR, BN = 32 * NR, BK = 16, LA = BM + 4, LB = BN + 4;
   constexpr int AVT = BK * BM / 4, BVT = BK * BN / 4;   // f4 per slab
   constexpr int AV = (AVT + 255) / 256, BV = (BVT + 255) / 256;
@@ -329,8 +350,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict
   float* const Bs = smab + 2 * BK * LA;    // [2][BK * LB]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
   const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kb = blockIdx.z * kps, ke = min(K, kb + kps);
+  const int m0 = bid.y * BM, n0 = bid.x * BN;
+  const int kb = bid.z * kps, ke = min(K, kb + kps);
   const int M = e.M, N = e.N;
   f4 ra[AV], rb[BV];
   // slab element -> (k, row) of f4 x: K-major: 4 rows at one k; K-contiguous: 4 k of one row
@@ -414,7 +435,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict
   // row pieces from the accumulator layout
   constexpr int SW = 16 * NR, SP = SW + 4;  // strip width, pitch (16 x SW floats = 64 NR f4 per strip)
   float* stg = smab + w * 16 * SP;
-  float* const dst = e.slab ? e.slab + (long)blockIdx.z * M * N : e.C;
+  float* const dst = e.slab ? e.slab + (long)bid.z * M * N : e.C;
   const long ldd = e.slab ? (long)N : e.ldc;
   const bool vec = (ldd % 4 == 0) && (((uintptr_t)dst & 15) == 0);
 #pragma unroll
@@ -463,7 +484,8 @@ static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, lo
   Z = cdiv(K, kps);
   EpiArgs ek = e;
   if (Z > 1) ek.slab = scratch;
-  gemm_tn_kernel<MR, NR, AKC, BKC><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek);
+  gemm_tn_kernel<MR, NR, AKC, BKC><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek,
+                                                                                   gxcd_remap());
   ABCD_CHECK_LAUNCH();
   if (Z > 1) {
     const long n = (long)M * N;
@@ -471,6 +493,203 @@ static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, lo
     ABCD_CHECK_LAUNCH();
   }
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// gemm_x6s: the gemm_tn structure (fp32 [k][row] LDS slabs, double-buffered,
+// K-major or K-contiguous operands, split-K over the grid, XCD-aware order,
+// LDS-transposed epilogue) with the contraction on the bf16 matrix cores in
+// split-fp32 form (abcd_x6.h: six bf16 MFMAs per 16x16x32 block, fp32-exact
+// to one rounding).  The operands stay fp32 in LDS (32 KB per stage at
+// 128 x 128, so two workgroups share a CU and hide each other's staging);
+// each wave splits its own fragments -- one split per fragment and chunk,
+// reused across the NR (A) or MR (B) blocks it multiplies.  Per 32-deep chunk
+// a wave issues 6 MR NR MFMAs of 16 cycles against 16 (MR + NR) plain VALU
+// ops of the splits: the f32-MFMA form of the same chunk costs 8 MR NR
+// MFMAs of 32 cycles.
+// ---------------------------------------------------------------------------
+template <int MR, int NR, bool AKC, bool BKC>
+__global__ __launch_bounds__(256, 2) void gemm_x6s_kernel(const float* __restrict__ A, long lda,
+                                                       const float* __restrict__ B, long ldb, int K, int kps,
+                                                       EpiArgs e, int remap) {
+  const dim3 bid = xcd_tile(remap != 0);
+  constexpr int BM = 32 * MR, BN = 32 * NR, BK = 32, LA = BM + 4, LB = BN + 4;
+  constexpr int AVT = BK * BM / 4, BVT = BK * BN / 4;  // f4 per slab
+  constexpr int AV = (AVT + 255) / 256, BV = (BVT + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float smab[2 * BK * LA + 2 * BK * LB];
+  float* const As = smab;
+  float* const Bs = smab + 2 * BK * LA;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = bid.y * BM, n0 = bid.x * BN;
+  const int kb = bid.z * kps, ke = min(K, kb + kps);
+  const int M = e.M, N = e.N;
+  // slab element x -> K-major: 4 rows at one k; K-contiguous: 4 k of one row (BK / 4 per row)
+  auto gload1 = [&](const float* P, long ld, int R, int r0, int k0, int x, int BR, bool kc) -> f4 {
+    if (kc) {
+      const int row = x / (BK / 4), k = 4 * (x % (BK / 4));
+      if (r0 + row < R && k0 + k + 4 <= ke) return *reinterpret_cast<const f4*>(P + (long)(r0 + row) * ld + k0 + k);
+      f4 v = f4zero();
+      if (r0 + row < R)
+        for (int t = 0; t < 4; ++t) v[t] = k0 + k + t < ke ? P[(long)(r0 + row) * ld + k0 + k + t] : 0.f;
+      return v;
+    }
+    const int k = x / (BR / 4), row = (x % (BR / 4)) * 4;
+    return (k0 + k < ke && r0 + row < R) ? *reinterpret_cast<const f4*>(P + (long)(k0 + k) * ld + r0 + row) : f4zero();
+  };
+  auto lstore1 = [&](float* S, int LD, int BR, int x, const f4& v, bool kc) {
+    if (kc) {
+      const int row = x / (BK / 4), k = 4 * (x % (BK / 4));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) S[(k + t) * LD + row] = v[t];
+    } else {
+      const int k = x / (BR / 4), row = (x % (BR / 4)) * 4;
+      *reinterpret_cast<f4*>(&S[k * LD + row]) = v;
+    }
+  };
+  auto gload = [&](int k0, f4 (&xa)[AV], f4 (&xb)[BV]) {
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int x = threadIdx.x + 256 * u;
+      xa[u] = x < AVT ? gload1(A, lda, M, m0, k0, x, BM, AKC) : f4zero();
+    }
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      const int x = threadIdx.x + 256 * u;
+      xb[u] = x < BVT ? gload1(B, ldb, N, n0, k0, x, BN, BKC) : f4zero();
+    }
+  };
+  auto lstore = [&](int buf, const f4 (&xa)[AV], const f4 (&xb)[BV]) {
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int x = threadIdx.x + 256 * u;
+      if (x < AVT) lstore1(As + buf * BK * LA, LA, BM, x, xa[u], AKC);
+    }
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      const int x = threadIdx.x + 256 * u;
+      if (x < BVT) lstore1(Bs + buf * BK * LB, LB, BN, x, xb[u], BKC);
+    }
+  };
+  f4 acc[MR][NR];
+  acc_zero(acc);
+  auto compute = [&](int cur) {
+    // fragment of lane (r, q): row r of the block, k = 8q .. 8q+7 of the chunk
+    const float* as = As + cur * BK * LA + 8 * q * LA + wm * 16 * MR + r;
+    const float* bs = Bs + cur * BK * LB + 8 * q * LB + wn * 16 * NR + r;
+    bf8 bp[3][NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      f4 x0, x1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        x0[t] = bs[t * LB + 16 * j];
+        x1[t] = bs[(4 + t) * LB + 16 * j];
+      }
+      split8(x0, x1, bp[0][j], bp[1][j], bp[2][j]);
+    }
+    // per A block: its split, then the six terms (smallest first), each over
+    // the NR blocks -- consecutive MFMAs write different accumulators
+    constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      f4 x0, x1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        x0[t] = as[t * LA + 16 * i];
+        x1[t] = as[(4 + t) * LA + 16 * i];
+      }
+      bf8 ap[3];
+      split8(x0, x1, ap[0], ap[1], ap[2]);
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = mfma_bf(ap[TA[t]], bp[TB[t]][j], acc[i][j]);
+    }
+  };
+  f4 ra[AV], rb[BV];
+  gload(kb, ra, rb);
+  lstore(0, ra, rb);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) gload(k0 + BK, ra, rb);
+    compute(cur);
+    if (more) lstore(cur ^ 1, ra, rb);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // epilogue: wave-private LDS transpose, whole-row 16-B stores (as gemm_tn_kernel)
+  constexpr int SW = 16 * NR, SP = SW + 4;
+  float* stg = smab + w * 16 * SP;
+  float* const dst = e.slab ? e.slab + (long)bid.z * M * N : e.C;
+  const long ldd = e.slab ? (long)N : e.ldc;
+  const bool vec = (ldd % 4 == 0) && (((uintptr_t)dst & 15) == 0);
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < NR; ++p) {
+      const int lr = (lane + 64 * p) / (4 * NR), c4 = (lane + 64 * p) % (4 * NR);
+      const int gcol = n0 + wn * SW + 4 * c4;
+      const int row = m0 + wm * 16 * MR + 16 * i + lr;
+      f4 v = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
+      if (row < M) {
+        if (!e.slab) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (gcol + t < N) v[t] = apply_epi(e, row, gcol + t, v[t]);
+        }
+        float* d = dst + (long)row * ldd + gcol;
+        if (vec && gcol + 4 <= N) *reinterpret_cast<f4*>(d) = v;
+        else
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (gcol + t < N) d[t] = v[t];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int MR, int NR, bool AKC, bool BKC>
+static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                           EpiArgs e, float* scratch, size_t scratch_floats) {
+  const int BM = 32 * MR, BN = 32 * NR;
+  const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  int Z = std::max(1, std::min(cdiv(tl_side ? 256 : 512, tiles), cdiv(K, 32 * 16)));
+  if (scratch) Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)M * N)));
+  else Z = 1;
+  Z = std::max(Z, 1);
+  const int kps = ((cdiv(K, Z) + 31) / 32) * 32;
+  Z = cdiv(K, kps);
+  EpiArgs ek = e;
+  if (Z > 1) ek.slab = scratch;
+  gemm_x6s_kernel<MR, NR, AKC, BKC><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek,
+                                                                                     gxcd_remap());
+  ABCD_CHECK_LAUNCH();
+  if (Z > 1) {
+    const long n = (long)M * N;
+    slab_reduce_kernel<<<std::min<long>(2048, cdiv(n, 256)), 256, 0, s>>>(scratch, Z, e);
+    ABCD_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// split-fp32 GEMM routing (default on; ABCD_X6S=0 keeps the f32-MFMA kernels)
+static bool x6s_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("ABCD_X6S");
+    return !(v && v[0] == '0');
+  }();
+  return on;
 }
 
 // both operands K-major with 16-B aligned rows covering roundup(M|N, 4).
@@ -506,6 +725,7 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
     // ~1.6x the direct-fragment gemm_big at the input-projection shape)
     if (cdiv(M, 128) * cdiv(N, 128) >= 240 && A.nrows >= M && B.nrows >= N && A.ld % 4 == 0 && B.ld % 4 == 0 &&
         ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0 && !lds_nt_disabled()) {
+      if (x6s_enabled() && !tl_side) return gemm_x6s_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
       if (N >= 256) return gemm_tn_launch<4, 8, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
       return gemm_tn_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
     }
@@ -528,8 +748,14 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
   // batch-reduction weight gradients, K = B = 512) goes to gemm_ks, whose
   // 32 x 64 tiles and grid split-K fill the chip (gemm_tn's 128 x 256 tiles
   // leave ~16 workgroups: ~100-170 us per GEMM measured, vs ~10)
-  if (K >= 4096 && A.nrows >= M && B.nrows >= N && tn_ok(A, M) && tn_ok(B, N))
+  if (K >= 4096 && A.nrows >= M && B.nrows >= N && tn_ok(A, M) && tn_ok(B, N)) {
+    if (x6s_enabled() && !tl_side) {  // 66-76 KB of LDS: not beside a persistent kernel
+      if (N > 128 && N <= 160)  // one 160-wide tile (e.g. dW_ih, N = F = 129)
+        return gemm_x6s_launch<4, 5, false, false>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+      return gemm_x6s_launch<4, 4, false, false>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+    }
     return gemm_tn(s, M, N, K, A, B, e, scratch, scratch_floats);
+  }
   return gemm_launch(s, M, N, K, KM{A.p, A.ld, std::min(A.nrows, M), K}, KM{B.p, B.ld, std::min(B.nrows, N), K},
                      e, scratch, scratch_floats);
 }

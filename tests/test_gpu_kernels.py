@@ -7,8 +7,11 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 16, 16), (33, 70, 48), (512, 1024, 256), (65, 2048, 144), (7, 5, 3),
-                                   (1000, 129, 385), (300, 512, 1024)])
+                                   (1000, 129, 385), (300, 512, 1024), (8001, 520, 144), (7000, 256, 256)])
 def test_gemm_nt_vs_torch(M, N, K):
+    """C = A B^T + bias; the last two shapes take the frame-parallel LDS route
+    (>= 240 128-wide tiles: split-fp32 gemm_x6s with K-contiguous operands,
+    ragged M / N / K)."""
     from modules import _native as Nn
     g = torch.Generator(device="cuda").manual_seed(M * 1000 + N + K)
     A = torch.randn(M, K, device="cuda", generator=g)
