@@ -513,12 +513,16 @@ __global__ __launch_bounds__(256, 2) void gemm_x6s_kernel(const float* __restric
                                                        const float* __restrict__ B, long ldb, int K, int kps,
                                                        EpiArgs e, int remap) {
   const dim3 bid = xcd_tile(remap != 0);
+  // slab row k at k * L + 16 (k / 8): the four 8-k groups a fragment read
+  // spans land on different bank quarters (a plain pitch of BM + 4 maps
+  // groups 0 / 2 and 1 / 3 onto the same banks)
   constexpr int BM = 32 * MR, BN = 32 * NR, BK = 32, LA = BM + 4, LB = BN + 4;
+  constexpr int SA = BK * LA + 16 * (BK / 8), SB = BK * LB + 16 * (BK / 8);  // one stage
   constexpr int AVT = BK * BM / 4, BVT = BK * BN / 4;  // f4 per slab
   constexpr int AV = (AVT + 255) / 256, BV = (BVT + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float smab[2 * BK * LA + 2 * BK * LB];
+  __shared__ __attribute__((aligned(16))) float smab[2 * SA + 2 * SB];
   float* const As = smab;
-  float* const Bs = smab + 2 * BK * LA;
+  float* const Bs = smab + 2 * SA;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
   const int wm = w >> 1, wn = w & 1;
   const int m0 = bid.y * BM, n0 = bid.x * BN;
@@ -541,10 +545,10 @@ __global__ __launch_bounds__(256, 2) void gemm_x6s_kernel(const float* __restric
     if (kc) {
       const int row = x / (BK / 4), k = 4 * (x % (BK / 4));
 #pragma unroll
-      for (int t = 0; t < 4; ++t) S[(k + t) * LD + row] = v[t];
+      for (int t = 0; t < 4; ++t) S[(k + t) * LD + 16 * ((k + t) >> 3) + row] = v[t];
     } else {
       const int k = x / (BR / 4), row = (x % (BR / 4)) * 4;
-      *reinterpret_cast<f4*>(&S[k * LD + row]) = v;
+      *reinterpret_cast<f4*>(&S[k * LD + 16 * (k >> 3) + row]) = v;
     }
   };
   auto gload = [&](int k0, f4 (&xa)[AV], f4 (&xb)[BV]) {
@@ -563,20 +567,20 @@ __global__ __launch_bounds__(256, 2) void gemm_x6s_kernel(const float* __restric
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
       const int x = threadIdx.x + 256 * u;
-      if (x < AVT) lstore1(As + buf * BK * LA, LA, BM, x, xa[u], AKC);
+      if (x < AVT) lstore1(As + buf * SA, LA, BM, x, xa[u], AKC);
     }
 #pragma unroll
     for (int u = 0; u < BV; ++u) {
       const int x = threadIdx.x + 256 * u;
-      if (x < BVT) lstore1(Bs + buf * BK * LB, LB, BN, x, xb[u], BKC);
+      if (x < BVT) lstore1(Bs + buf * SB, LB, BN, x, xb[u], BKC);
     }
   };
   f4 acc[MR][NR];
   acc_zero(acc);
   auto compute = [&](int cur) {
     // fragment of lane (r, q): row r of the block, k = 8q .. 8q+7 of the chunk
-    const float* as = As + cur * BK * LA + 8 * q * LA + wm * 16 * MR + r;
-    const float* bs = Bs + cur * BK * LB + 8 * q * LB + wn * 16 * NR + r;
+    const float* as = As + cur * SA + 8 * q * LA + 16 * q + wm * 16 * MR + r;
+    const float* bs = Bs + cur * SB + 8 * q * LB + 16 * q + wn * 16 * NR + r;
     bf8 bp[3][NR];
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
