@@ -806,6 +806,17 @@ DEV void mma16(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, i
 // Phase hand-offs use the group counter: every member adds 1 after each of
 // the three phases; phase p of step i waits for M * (3i + p).
 __device__ __forceinline__ int dec_cell_row(int H, int u0, int j, int r) { return (2 * j + (r >> 3)) * H + u0 + (r & 7); }
+// GRU cell columns of a member (the same 2 x 16 subtile shape): subtile 0 =
+// [r | z] (x and h parts), subtile 1 = [n_x | n_h] -- the candidate's input
+// and recurrent projections stay apart (n = tanh(n_x + b_in + r (n_h + b_hn)),
+// torch GRUCell), so n_x has a zero h part and n_h a zero x part.
+// Row of W_ih (xpart) or W_hh for column (j, r); -1 = zero row.
+__device__ __forceinline__ int dec_gru_row(int H, int u0, int j, int r, bool xpart) {
+  const int g = 2 * j + (r >> 3), u = u0 + (r & 7);
+  if (g < 2) return g * H + u;
+  if (g == 2) return xpart ? 2 * H + u : -1;
+  return xpart ? -1 : 2 * H + u;
+}
 
 // NCC > 0: the cell GEMM in split-fp32 (abcd_x6.h) over NCC 32-deep chunks
 // (cdiv(Fp, 32) for x when self-feeding, + H / 32 for h)
@@ -1031,7 +1042,10 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 //         the lv waves hand lv to the mu waves through LDS, and those draw the
 //         noise and store the self-feedback sample.
 // ---------------------------------------------------------------------------
-template <int NCC, int NH32, int NM32>
+// GRU: the cell columns are dec_gru_row's, a.bias is [b_r | b_z | b_in | b_hn]
+// (4H, r and z with b_ih + b_hh), the lanes carry h_{t-1} of their unit instead
+// of c, and the stash row is (r, z, n, n_h + b_hn) as the per-step kernels'.
+template <int NCC, int NH32, int NM32, bool GRU = false>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
@@ -1058,8 +1072,11 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   f4* B1 = BC + 2 * NCC * 3 * 64;       // mlp tile: [NH32][3][64]
   f4* B2 = B1 + NH32 * 3 * 64;          // emit: mu tile, lv tile: [2][NM32][3][64]
   float* LVX = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [2][16][16]
-  if (nx32) stage_x6(BC, a.Wih, Fp, Fp, 2, nx32, 0, NCC, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
-  stage_x6(BC, a.Whh, H, H, 2, H / 32, nx32, NCC, [&](int j, int rr) { return dec_cell_row(H, u0, j, rr); });
+  if (nx32)
+    stage_x6(BC, a.Wih, Fp, Fp, 2, nx32, 0, NCC,
+             [&](int j, int rr) { return GRU ? dec_gru_row(H, u0, j, rr, true) : dec_cell_row(H, u0, j, rr); });
+  stage_x6(BC, a.Whh, H, H, 2, H / 32, nx32, NCC,
+           [&](int j, int rr) { return GRU ? dec_gru_row(H, u0, j, rr, false) : dec_cell_row(H, u0, j, rr); });
   if (has1) stage_x6(B1, a.W1, H, H, 1, NH32, 0, NH32, [&](int, int rr) { return 16 * mem + rr; });
   if (has2) {
     stage_x6(B2, a.W2m, Hm, Hm, 1, NM32, 0, NM32, [&](int, int rr) { return 16 * j2 + rr; });
@@ -1079,11 +1096,11 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     const int next_off = off[t + 1];
     const int next_bs = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
     // ---------------- cell ----------------
-    if (i == 0) {  // c_0 from feature2hidden (dec_init wrote it to the stash rows of step 0)
+    if (i == 0) {  // c_0 (GRU: h_0) from feature2hidden (dec_init wrote it to the stash rows of step 0)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int b = row0 + 4 * q + g;
-        cst[g] = b < bs ? a.Cprev[(long)(o + b) * H + unit] : 0.f;
+        cst[g] = b < bs ? (GRU ? a.Hprev : a.Cprev)[(long)(o + b) * H + unit] : 0.f;
       }
     }
     if (i > 0) gs.wait(3u * i);
@@ -1098,17 +1115,27 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q);
     }
     PSTAMP(7);
+    // LSTM: (gi, gf, gg, go) = (i, f, g, o); GRU: (r, z, n, n_h + b_hn)
     float gi[4], gf[4], gg[4], go[4], hv[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const float v0 = acc[0][g] + bias0, v1 = acc[1][g] + bias1;
       const float w0 = __shfl_xor(v0, 8, 64), w1 = __shfl_xor(v1, 8, 64);
-      gi[g] = fsigmoid(lo ? v0 : w0);
-      gf[g] = fsigmoid(lo ? w0 : v0);
-      gg[g] = ftanh(lo ? v1 : w1);
-      go[g] = fsigmoid(lo ? w1 : v1);
-      cst[g] = gf[g] * cst[g] + gi[g] * gg[g];
-      hv[g] = go[g] * ftanh(cst[g]);
+      if constexpr (GRU) {
+        gi[g] = fsigmoid(lo ? v0 : w0);
+        gf[g] = fsigmoid(lo ? w0 : v0);
+        go[g] = lo ? w1 : v1;
+        gg[g] = ftanh((lo ? v1 : w1) + gi[g] * go[g]);
+        hv[g] = (1.f - gf[g]) * gg[g] + gf[g] * cst[g];
+        cst[g] = hv[g];
+      } else {
+        gi[g] = fsigmoid(lo ? v0 : w0);
+        gf[g] = fsigmoid(lo ? w0 : v0);
+        gg[g] = ftanh(lo ? v1 : w1);
+        go[g] = fsigmoid(lo ? w1 : v1);
+        cst[g] = gf[g] * cst[g] + gi[g] * gg[g];
+        hv[g] = go[g] * ftanh(cst[g]);
+      }
       const int b = row0 + 4 * q + g;
       if (b < bs) {
         if (lo) st_ho(a.Hs + (long)(o + b) * H + unit, hv[g], loc);                       // -> mlp
@@ -1125,10 +1152,10 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       float* Gr = a.Gst + rr * 4 * H;
       if (lo) {
         Gr[unit] = gi[g]; Gr[H + unit] = gf[g];
-        a.Cst[rr * H + unit] = cst[g];
+        if (!GRU) a.Cst[rr * H + unit] = cst[g];
       } else {
         Gr[2 * H + unit] = gg[g]; Gr[3 * H + unit] = go[g];
-        if (b < next_bs) a.Cprev[(long)(next_off + b) * H + unit] = cst[g];
+        if (!GRU && b < next_bs) a.Cprev[(long)(next_off + b) * H + unit] = cst[g];
       }
     }
     // ---------------- mlp ----------------
@@ -1927,13 +1954,13 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32>
+template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
   const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
@@ -1941,7 +1968,7 @@ static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_x6<NCC, NH32, NM32><<<grid, 256, lds, s>>>(b);
+    dec_fwd_x6<NCC, NH32, NM32, GRU><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
   *launched = true;
@@ -1950,9 +1977,19 @@ static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched
 
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {
   *launched = false;
-  if (!persist_enabled() || G != 4 || a.H % 8) return 0;
-  // all-x6 form: H = Hm = 256 (one mlp tile per member), 2 Fp/16 emit members
+  if (!persist_enabled() || a.H % 8) return 0;
   const char* v6 = getenv("ABCD_DECX6");
+  if (G == 3) {  // GRU: the all-x6 form only (a.bias = [b_r | b_z | b_in | b_hn])
+    if (!(x6_enabled(a.H) && a.H == 256 && a.Hm == 256 && 2 * (a.Fp / 16) <= a.H / 8) || (v6 && v6[0] == '0'))
+      return 0;
+    const int ncc = (a.feedback ? cdiv(a.Fp, 32) : 0) + a.H / 32;
+    if (ncc == 13) return launch_dec_fwd_x6<13, 8, 8, true>(s, a, launched);
+    if (ncc == 11) return launch_dec_fwd_x6<11, 8, 8, true>(s, a, launched);
+    if (ncc == 8) return launch_dec_fwd_x6<8, 8, 8, true>(s, a, launched);
+    return 0;
+  }
+  if (G != 4) return 0;
+  // all-x6 form: H = Hm = 256 (one mlp tile per member), 2 Fp/16 emit members
   if (x6_enabled(a.H) && a.H == 256 && a.Hm == 256 && 2 * (a.Fp / 16) <= a.H / 8 && !(v6 && v6[0] == '0')) {
     const int ncc = (a.feedback ? cdiv(a.Fp, 32) : 0) + a.H / 32;
     if (ncc == 13) return launch_dec_fwd_x6<13, 8, 8>(s, a, launched);

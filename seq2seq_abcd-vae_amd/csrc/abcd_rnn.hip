@@ -918,7 +918,7 @@ __global__ void unpad_rows(const float* src, int Fp, float* dst, int F, long row
 
 struct DecWS {
   // derived weights
-  float *Wihp, *bcomb, *W1cat, *b1cat, *W2mp, *W2lp, *b2mp, *b2lp;
+  float *Wihp, *bcomb, *bgru, *W1cat, *b1cat, *W2mp, *W2lp, *b2mp, *b2lp;
   float *WihTp, *WhhT, *W2mT, *W2lT, *W1catT, *W1oT, *Wf2hT;
   // forward stash
   float *FS, *Hinit, *Xin, *Hprev, *Cprev, *Gst, *Cst, *Hs, *Aact, *MU, *LV, *OUT, *Zo, *offlog, *dlog_raw, *bce;
@@ -947,7 +947,7 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
   const int G = c->rnn_type == ABCD_LSTM ? 4 : 3, GH = G * H;
   const int Htot = c->rnn_type == ABCD_LSTM ? 2 * H : H;
   const int DS = c->feature_size + (c->num_speakers > 0 ? c->speaker_dim : 0);
-  w.Wihp = A.f((size_t)GH * Fp); w.bcomb = A.f(GH);
+  w.Wihp = A.f((size_t)GH * Fp); w.bcomb = A.f(GH); w.bgru = A.f((size_t)4 * H);
   w.W1cat = A.f((size_t)2 * Hm * H); w.b1cat = A.f(2 * Hm);
   w.W2mp = A.f((size_t)Fp * Hm); w.W2lp = A.f((size_t)Fp * Hm); w.b2mp = A.f(Fp); w.b2lp = A.f(Fp);
   w.WihTp = A.f((size_t)Fp * GH); w.WhhT = A.f((size_t)H * GH);
@@ -1025,7 +1025,13 @@ extern "C" int abcd_decoder_forward_dropout(const abcd_decoder_cfg* c, const abc
     Packs pk(s);
     ABCD_TRY((hipError_t)pk.add(cw.w_ih, F, GH, F, false, w.Wihp, Fp, GH, Fp));
     if (G == 4) ABCD_TRY((hipError_t)pk.add(cw.b_ih, GH, 1, GH, false, w.bcomb, GH, 1, GH, cw.b_hh));
-    else ABCD_TRY((hipError_t)pk.add(cw.b_ih, GH, 1, GH, false, w.bcomb, GH, 1, GH));
+    else {
+      ABCD_TRY((hipError_t)pk.add(cw.b_ih, GH, 1, GH, false, w.bcomb, GH, 1, GH));
+      // persistent GRU cell bias [b_r | b_z | b_in | b_hn] (r, z: b_ih + b_hh)
+      ABCD_TRY((hipError_t)pk.add(cw.b_ih, 2 * H, 1, 2 * H, false, w.bgru, 2 * H, 1, 2 * H, cw.b_hh));
+      ABCD_TRY((hipError_t)pk.add(cw.b_ih + 2 * H, H, 1, H, false, w.bgru + 2 * H, H, 1, H));
+      ABCD_TRY((hipError_t)pk.add(cw.b_hh + 2 * H, H, 1, H, false, w.bgru + 3 * H, H, 1, H));
+    }
     ABCD_TRY((hipError_t)pk.add(p->mu.w1, H, Hm, H, false, w.W1cat, H, Hm, H));
     ABCD_TRY((hipError_t)pk.add(p->lv.w1, H, Hm, H, false, w.W1cat + (size_t)Hm * H, H, Hm, H));
     ABCD_TRY((hipError_t)pk.add(p->mu.b1, Hm, 1, Hm, false, w.b1cat, Hm, 1, Hm));
@@ -1054,13 +1060,13 @@ extern "C" int abcd_decoder_forward_dropout(const abcd_decoder_cfg* c, const abc
     pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS);
     pa.feedback = c->feedback;
     pa.off = w.off; pa.sync = w.sync;
-    pa.Wih = w.Wihp; pa.Whh = cw.w_hh; pa.bias = w.bcomb;
+    pa.Wih = w.Wihp; pa.Whh = cw.w_hh; pa.bias = G == 4 ? w.bcomb : w.bgru;
     pa.W1 = w.W1cat; pa.b1 = w.b1cat;
     pa.W2m = w.W2mp; pa.W2l = w.W2lp; pa.b2m = w.b2mp; pa.b2l = w.b2lp;
     pa.eps = eps; pa.seed = seed; pa.offset = offset; pa.xmask = xmask;
     pa.Xin = w.Xin; pa.Hprev = w.Hprev; pa.Cprev = w.Cprev; pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Hs = w.Hs;
     pa.Aact = w.Aact; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
-    if (persist_enabled() && G == 4) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+    if (persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
     ABCD_TRY((hipError_t)persist_decoder_fwd(s, G, pa, &done));
   }
   for (int t = 0; t < T && !done; ++t) {

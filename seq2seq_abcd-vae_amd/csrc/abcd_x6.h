@@ -96,11 +96,14 @@ DEV void stage_x6(f4* dst, const float* W, long ldw, int kvalid, int nsub, int n
         const int rowi = (e >> 2) / nseg;
         const int j = rowi >> 4, r = rowi & 15;
         const int k = c * 32 + 8 * q;
-        const float* src = W + (long)rowfn(j, r) * ldw + k;
-        if (k + 4 <= kvalid) v0[u] = *reinterpret_cast<const f4*>(src);
+        const int wr = rowfn(j, r);  // < 0: a zero row
+        const float* src = W + (long)(wr < 0 ? 0 : wr) * ldw + k;
+        if (wr < 0) {
+        } else if (k + 4 <= kvalid) v0[u] = *reinterpret_cast<const f4*>(src);
         else
           for (int s = 0; s < 4; ++s) v0[u][s] = k + s < kvalid ? src[s] : 0.f;
-        if (k + 8 <= kvalid) v1[u] = *reinterpret_cast<const f4*>(src + 4);
+        if (wr < 0) {
+        } else if (k + 8 <= kvalid) v1[u] = *reinterpret_cast<const f4*>(src + 4);
         else
           for (int s = 0; s < 4; ++s) v1[u][s] = k + 4 + s < kvalid ? src[4 + s] : 0.f;
         dsti[u] = ((j * nch + c0 + c) * 3) * 64 + q * 16 + r;
