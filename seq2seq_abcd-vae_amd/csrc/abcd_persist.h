@@ -86,10 +86,12 @@ struct PDecBwdArgs {
   const float *W2mT, *W2lT;        // Hm x Fp
   const float* W1T;                // H x 2Hm
   const float *Gst, *Cst, *Cprev, *MU, *LV, *OUT, *Aact, *DHO;
+  const float* Hprev;              // GRU: h_{t-1} of every row (the cell backward's dz term)
   const float* Y;                  // target frames (rows x F)
   const float* s_em;               // device scalar: d loss / d emission NLL
   const float* xmask;              // input-dropout noise (rows x F) of the cell inputs; null: none
   float *dG, *dMU, *dLV, *dZ, *DHR, *DC0;
+  float* dGH;                      // GRU: the recurrent-side gate gradients (dG holds the input side)
   float* part;  // split-K partials (dec_bwd_sk): 2 parity slots x groups x (Fp+H)/16 subtiles x 4 waves x H/8 x 256
 };
 inline size_t dec_part_floats(int B, int H, int Fp) {

@@ -1452,10 +1452,15 @@ DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc) {
     for (int k = 0; k < NB; ++k) acc += v[k];
   }
 }
-template <int NXS, int NHS, int NZ>
+// GRU: the member's 32 columns are dec_fwd_x6's [r | z | n_x | n_h]
+// (dG = [dr, dz, dn, dn r] pre-activation gradients), the split-K image takes
+// the n_x column from W_ih only and n_h from W_hh only, the carry is dh z, and
+// the stash is dGX = (dr, dz, dn), dGH = (dr, dz, dn r) with pitch 3H as the
+// per-step kernels write it.
+template <int NXS, int NHS, int NZ, bool GRU = false>
 __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
-  constexpr int H = NHS * 16, GH = 4 * H, M = H / 8, NS = NXS + NHS;
+  constexpr int H = NHS * 16, GH = (GRU ? 3 : 4) * H, M = H / 8, NS = NXS + NHS;
   const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
   const int nchx = Fp / 16, nFt = Fp / 16;
   const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
@@ -1481,10 +1486,14 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
   // own units 0..7) of output column 16s + rr: [W_ih | W_hh]^T row (col) ...
   for (int e = threadIdx.x; e < NS * 64; e += 256) {
     const int s = e >> 6, ln = e & 63, rr = ln & 15, qq = ln >> 4;
-    const float* src = s < NXS ? a.WihT + (long)(16 * s + rr) * GH + qq * H + u0
-                               : a.WhhT + (long)(16 * (s - NXS) + rr) * GH + qq * H + u0;
+    const bool xs = s < NXS;
+    int col = qq * H + u0;  // gate column (row of W) of the 8 own units
+    if (GRU && qq >= 2) col = (qq == 2) == xs ? 2 * H + u0 : -1;
+    const float* src = (xs ? a.WihT + (long)(16 * s + rr) * GH : a.WhhT + (long)(16 * (s - NXS) + rr) * GH) +
+                       (col < 0 ? 0 : col);
     bf8 h, m, l;
-    split8(*reinterpret_cast<const f4*>(src), *reinterpret_cast<const f4*>(src + 4), h, m, l);
+    split8(col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src),
+           col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src + 4), h, m, l);
     SK[(s * 3) * 64 + ln] = __builtin_bit_cast(f4, h);
     SK[(s * 3 + 1) * 64 + ln] = __builtin_bit_cast(f4, m);
     SK[(s * 3 + 2) * 64 + ln] = __builtin_bit_cast(f4, l);
@@ -1604,8 +1613,8 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       const float* Gr = a.Gst + rr * 4 * H;
 #pragma unroll
       for (int j = 0; j < 4; ++j) pg[g][j] = live ? Gr[j * H + unit] : 0.f;
-      pc[g] = live ? a.Cst[rr * H + unit] : 0.f;
-      pcp[g] = live ? a.Cprev[rr * H + unit] : 0.f;
+      pc[g] = (live && !GRU) ? a.Cst[rr * H + unit] : 0.f;
+      pcp[g] = live ? (GRU ? a.Hprev : a.Cprev)[rr * H + unit] : 0.f;
       pdho[g] = live ? a.DHO[rr * H + unit] : 0.f;
     }
     gs.wait(3u * i + 2);
@@ -1624,16 +1633,29 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       for (int j = 0; j < 4; ++j) dgh[g][j] = 0.f;
       if (b >= bs) continue;
       const bool fin = b >= succ_valid;
-      const float dh = acc[0][g] + (fin ? 0.f : dhr[g]) + pdho[g];
-      const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
-      const float tc = ftanh(pc[g]);
-      const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
-      dgh[g][0] = dc * g_ * i_ * (1.f - i_);
-      dgh[g][1] = dc * pcp[g] * f_ * (1.f - f_);
-      dgh[g][2] = dc * i_ * (1.f - g_ * g_);
-      dgh[g][3] = dh * tc * o_ * (1.f - o_);
-      carry[g] = dc * f_;
-      if (t == 0 && lo) a.DC0[(long)b * H + unit] = dc * f_;
+      if constexpr (GRU) {
+        // dh_t = dZ W1 + dh_rec + dh_offset + dh_{t+1} z_{t+1} (the carry)
+        const float dh = acc[0][g] + (fin ? 0.f : dhr[g] + carry[g]) + pdho[g];
+        const float r_ = pg[g][0], z_ = pg[g][1], n_ = pg[g][2], ghn = pg[g][3];
+        const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
+        dgh[g][0] = dnp * ghn * r_ * (1.f - r_);
+        dgh[g][1] = dh * (pcp[g] - n_) * z_ * (1.f - z_);
+        dgh[g][2] = dnp;
+        dgh[g][3] = dnp * r_;
+        carry[g] = dh * z_;
+        if (t == 0 && lo) a.DC0[(long)b * H + unit] = dh * z_;
+      } else {
+        const float dh = acc[0][g] + (fin ? 0.f : dhr[g]) + pdho[g];
+        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
+        const float tc = ftanh(pc[g]);
+        const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
+        dgh[g][0] = dc * g_ * i_ * (1.f - i_);
+        dgh[g][1] = dc * pcp[g] * f_ * (1.f - f_);
+        dgh[g][2] = dc * i_ * (1.f - g_ * g_);
+        dgh[g][3] = dh * tc * o_ * (1.f - o_);
+        carry[g] = dc * f_;
+        if (t == 0 && lo) a.DC0[(long)b * H + unit] = dc * f_;
+      }
     }
     // partials of this step's dG columns: the dx subtiles (read by the next
     // step's P0, on the critical path) are drained by this phase's publish;
@@ -1678,8 +1700,16 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
         const int b = row0 + 4 * q + g;
         if (b >= bs) continue;
         float* dg = a.dG + (long)(o + b) * GH;
+        if constexpr (GRU) {
+          float* dgr = a.dGH + (long)(o + b) * GH;
+          dg[unit] = dgr[unit] = dgh[g][0];
+          dg[H + unit] = dgr[H + unit] = dgh[g][1];
+          dg[2 * H + unit] = dgh[g][2];
+          dgr[2 * H + unit] = dgh[g][3];
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) dg[j * H + unit] = dgh[g][j];
+          for (int j = 0; j < 4; ++j) dg[j * H + unit] = dgh[g][j];
+        }
       }
     }
   }
@@ -2005,13 +2035,13 @@ int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launch
 }
 
 
-template <int NXS, int NHS, int NZ>
+template <int NXS, int NHS, int NZ, bool GRU = false>
 static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   constexpr int NS = NXS + NHS, M = NHS * 2;
   const size_t lds = (size_t)(NS + NZ) * 3 * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * 16 * DSK_PITCH * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_sk<NXS, NHS, NZ>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_sk<NXS, NHS, NZ, GRU>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
@@ -2019,7 +2049,7 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_sk<NXS, NHS, NZ><<<grid, 256, lds, s>>>(b);
+    dec_bwd_sk<NXS, NHS, NZ, GRU><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
   *launched = true;
@@ -2028,7 +2058,18 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
 
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {
   *launched = false;
-  if (!persist_enabled() || G != 4 || a.H % 8) return 0;
+  if (!persist_enabled() || a.H % 8) return 0;
+  if (G == 3) {  // GRU: the split-K form only
+    if (!(a.part && a.Hprev && a.dGH && x6_enabled(a.H) && splitk_enabled() && a.H == 256 && a.Hm == a.H &&
+          a.Fp / 16 <= a.H / 8))
+      return 0;
+    const int nxs = a.feedback ? a.Fp / 16 : 0;
+    if (nxs == 9) return launch_dec_bwd_sk<9, 16, 16, true>(s, a, launched);
+    if (nxs == 5) return launch_dec_bwd_sk<5, 16, 16, true>(s, a, launched);
+    if (nxs == 0) return launch_dec_bwd_sk<0, 16, 16, true>(s, a, launched);
+    return 0;
+  }
+  if (G != 4) return 0;
   // split-K form: H = 256 (32 members), 2Hm/16 == members, Fp/16 <= members
   if (a.part && x6_enabled(a.H) && splitk_enabled() && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8) {
     const int nxs = a.feedback ? a.Fp / 16 : 0;

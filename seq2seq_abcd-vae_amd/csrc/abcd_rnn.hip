@@ -972,7 +972,7 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
                                    (size_t)Htot * DS, (size_t)L});
   w.off = (int*)A.f((size_t)T + 1);
   w.sync = (unsigned*)A.f(persist_sync_uints(1, B));
-  w.skp = G == 4 ? A.f(dec_part_floats(B, H, Fp)) : nullptr;
+  w.skp = A.f(dec_part_floats(B, H, Fp));
   w.scratch_floats = std::max(maxMN * 64, (size_t)1 << 20);  // split-K slabs of the wgrad GEMMs
   w.scratch = A.f(w.scratch_floats);
   return w;
@@ -1208,8 +1208,9 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
     pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Cprev = w.Cprev; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
     pa.Aact = w.Aact; pa.DHO = w.DHO; pa.Y = x->data; pa.s_em = d_em; pa.xmask = xmask;
     pa.dG = w.dGX; pa.dMU = w.dMU; pa.dLV = w.dLV; pa.dZ = w.dZ; pa.DHR = w.DC; pa.DC0 = w.DC0;
+    pa.Hprev = w.Hprev; pa.dGH = w.dGH;
     pa.part = w.skp;
-    if (persist_enabled() && G == 4) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+    if (persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
     ABCD_TRY((hipError_t)persist_decoder_bwd(s, G, pa, &done));
   }
   const int TN = bwd_tn(H);
