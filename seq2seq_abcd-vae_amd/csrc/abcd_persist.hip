@@ -1045,7 +1045,12 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 // GRU: the cell columns are dec_gru_row's, a.bias is [b_r | b_z | b_in | b_hn]
 // (4H, r and z with b_ih + b_hh), the lanes carry h_{t-1} of their unit instead
 // of c, and the stash row is (r, z, n, n_h + b_hn) as the per-step kernels'.
-template <int NCC, int NH32, int NM32, bool GRU = false>
+// HPRE: the recurrent half of step t+1's cell product, h_t W_hh^T, is formed
+// in step t's mlp phase -- h_t is that phase's A operand already (rows of Hs =
+// the next step's Hprev rows) -- as two more tiles beside the mlp tile, and
+// carried in registers; step t+1's cell then waits only for x_{t+1} and runs
+// the NCC - 8 input chunks (H = 256: 8 recurrent chunks).
+template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
@@ -1089,6 +1094,8 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   const bool lo = r < 8;
   __syncthreads();
   float cst[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NXC = NCC - 8;  // input chunks of the cell product (H = 256)
+  f4 acch[2] = {f4zero(), f4zero()};  // HPRE: h_{t-1} W_hh^T of this step, from the previous mlp phase
   const int* off = a.off;
   for (int i = 0; i < T; ++i) {
     const int t = i;
@@ -1112,7 +1119,13 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.Xin + (size_t)o * Fp, t > 0 ? (uint32_t)bs * Fp * 4u : 0u);
       const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.Hprev + (size_t)o * H, (uint32_t)bs * H * 4u);
       const BufKC2x A{rx, rh, (uint32_t)Fp * 4u, (uint32_t)H * 4u, nx32, Fp};
-      wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q);
+      if (HPRE && i > 0) {
+        acc[0] = acch[0];
+        acc[1] = acch[1];
+        if constexpr (NXC > 0) wave_mma_x6<2, (NXC > 0 ? NXC : 1), 8>(acc, A, row0 + r, BC, NCC, lane, q);
+      } else {
+        wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q);
+      }
     }
     PSTAMP(7);
     // LSTM: (gi, gf, gg, go) = (i, f, g, o); GRU: (r, z, n, n_h + b_hn)
@@ -1165,7 +1178,16 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       f4 a1[1] = {f4zero()};
       if (row0 < bs) {
         const BufKC Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
-        wave_mma_x6<1, NH32, 8>(a1, Hs, row0 + r, B1, NH32, lane, q);
+        if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
+          f4 a3[3] = {f4zero(), f4zero(), f4zero()};
+          const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
+          wave_mma_x6p<3, NH32, 8>(a3, Hs, row0 + r, bp, lane, q);
+          a1[0] = a3[0];
+          acch[0] = a3[1];
+          acch[1] = a3[2];
+        } else {
+          wave_mma_x6<1, NH32, 8>(a1, Hs, row0 + r, B1, NH32, lane, q);
+        }
       }
       PSTAMP(6);
 #pragma unroll
@@ -1984,13 +2006,13 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32, bool GRU = false>
-static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
+template <int NCC, int NH32, int NM32, bool GRU, bool HPRE>
+static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
   const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
@@ -1998,11 +2020,19 @@ static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_x6<NCC, NH32, NM32, GRU><<<grid, 256, lds, s>>>(b);
+    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
   }
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
+}
+
+
+template <int NCC, int NH32, int NM32, bool GRU = false>
+static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
+  const char* hp = getenv("ABCD_DECHPRE");
+  if (hp && hp[0] == '0') return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, false>(s, a, launched);
+  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true>(s, a, launched);
 }
 
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {

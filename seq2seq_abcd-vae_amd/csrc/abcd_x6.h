@@ -173,4 +173,46 @@ DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch
   }
 }
 
+// wave_mma_x6 with one image segment per output tile: chunk c of tile j at
+// Bp[j] + c * 3 * 64 (tiles from different LDS images sharing one A operand)
+template <int NR, int NCH, int PD, class OA>
+DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp)[NR], int lane, int q) {
+  constexpr int P = PD < NCH ? PD : NCH;
+  f4 ra[P], rb[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) A.frag8(arow, p, q, ra[p], rb[p]);
+  f4 bw[NR][3];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bp[j][pl * 64 + lane];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int p = c % P;
+    f4 bn[NR][3];
+    if (c + 1 < NCH) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bp[j][((c + 1) * 3 + pl) * 64 + lane];
+    }
+    bf8 a0, a1, a2;
+    split8(ra[p], rb[p], a0, a1, a2);
+    if (c + P < NCH) A.frag8(arow, c + P, q, ra[p], rb[p]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      acc[j] = mma_x6(acc[j], a0, a1, a2, __builtin_bit_cast(bf8, bw[j][0]), __builtin_bit_cast(bf8, bw[j][1]),
+                      __builtin_bit_cast(bf8, bw[j][2]));
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < NCH) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bw[j][pl] = bn[j][pl];
+    }
+  }
+}
+
 }  // namespace abcd
