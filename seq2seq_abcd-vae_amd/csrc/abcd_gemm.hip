@@ -689,11 +689,8 @@ static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, l
 
 // split-fp32 GEMM routing (default on; ABCD_X6S=0 keeps the f32-MFMA kernels)
 static bool x6s_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("ABCD_X6S");
-    return !(v && v[0] == '0');
-  }();
-  return on;
+  const char* v = getenv("ABCD_X6S");  // read per call: tests flip it in-process
+  return !(v && v[0] == '0');
 }
 
 // both operands K-major with 16-B aligned rows covering roundup(M|N, 4).
