@@ -141,6 +141,14 @@ int abcd_sampler_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params
                           int mode, float temperature, double entire_data_size, const float* d_feats,
                           const float* d_kl, float* d_h, const abcd_sampler_grads* g, void* ws, size_t ws_bytes,
                           void* stream);
+/* the same, with the parameter gradients (codebook, posterior_shape_logits,
+ * MLP weights and biases) queued on wgrad_stream (NULL or == stream: one
+ * stream) after an event on `stream`; only the d_h chain stays on `stream`.
+ * The caller joins wgrad_stream before reading the gradients. */
+int abcd_sampler_backward_split(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
+                                int mode, float temperature, double entire_data_size, const float* d_feats,
+                                const float* d_kl, float* d_h, const abcd_sampler_grads* g, void* ws,
+                                size_t ws_bytes, void* stream, void* wgrad_stream);
 /* The same backward split the way autograd sees the three reference methods:
  * sample_backward:  d_feats -> d_logits (written), d_codebook (written, may be NULL)
  *                   (plain: d_feats -> d[mean | log_var])

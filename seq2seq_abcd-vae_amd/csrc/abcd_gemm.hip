@@ -12,6 +12,8 @@
 #include <cstdlib>
 
 #include "abcd_common.h"
+#include <mutex>
+
 #include "abcd_internal.h"
 #include "abcd_x6.h"
 
@@ -23,8 +25,25 @@ namespace abcd {
 // CU, so they fill the SIMDs the latency-bound recurrence leaves idle instead
 // of displacing its workgroups.
 static thread_local int tl_side = 0;
-GemmSideScope::GemmSideScope(bool on) : prev(tl_side) { tl_side = on ? 1 : 0; }
+GemmSideScope::GemmSideScope(bool on) : prev(tl_side) { tl_side = on ? 1 : prev; }  // off: keep the caller's mode
 GemmSideScope::~GemmSideScope() { tl_side = prev; }
+
+int stream_fork(hipStream_t from, hipStream_t to, int slot) {
+  if (from == to) return 0;
+  static std::mutex mu;
+  static hipEvent_t evs[64][8] = {};
+  int dev = 0;
+  ABCD_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64 || slot < 0 || slot >= 8) return (int)hipErrorInvalidValue;
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!evs[dev][slot]) ABCD_TRY(hipEventCreateWithFlags(&evs[dev][slot], hipEventDisableTiming));
+    ev = evs[dev][slot];
+  }
+  ABCD_TRY(hipEventRecord(ev, from));
+  return (int)hipStreamWaitEvent(to, ev, 0);
+}
 
 struct EpiArgs {
   float* C; long ldc; int M, N; float alpha, beta; const float* bias; int act;

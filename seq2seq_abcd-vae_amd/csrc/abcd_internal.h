@@ -90,6 +90,10 @@ struct GemmSideScope {
   ~GemmSideScope();
 };
 
+// `to` waits for everything queued on `from` so far (a reusable per-device
+// event per slot, re-recorded each call).  No-op when from == to.
+int stream_fork(hipStream_t from, hipStream_t to, int slot);
+
 }  // namespace abcd
 
 namespace abcd {

@@ -1261,10 +1261,6 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
   dec_feats_bwd<<<launch_grid((long)B * std::max(D, 1)), 256, 0, s>>>(w.dFS, D, S, B, speakers, c->num_speakers,
                                                                      d_features, S > 0 ? g->embed_speaker : nullptr);
   ABCD_CHECK_LAUNCH();
-  if (g->f2h_w)
-    ABCD_TRY((hipError_t)gemm(s, Htot, DS, B, opKM(w.dhid, Htot, Htot), opKM(FS, DS, DS), g->f2h_w, DS, 1.f, 0.f,
-                              nullptr, ACT_NONE, sc, scf));
-  if (g->f2h_b) ABCD_TRY((hipError_t)colsum(s, w.dhid, Htot, B, Htot, nullptr, g->f2h_b, 0.f, sc, scf));
   // ---- weight gradients, K = L frames ----
   // With a separate wgrad stream they run there, behind the data-gradient
   // path above, beside whatever the caller queues next on `stream` (the
@@ -1278,6 +1274,10 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
     ABCD_TRY(hipStreamWaitEvent(s, ev, 0));
   }
   GemmSideScope side_tiles(side);
+  if (g->f2h_w)
+    ABCD_TRY((hipError_t)gemm(s, Htot, DS, B, opKM(w.dhid, Htot, Htot), opKM(FS, DS, DS), g->f2h_w, DS, 1.f, 0.f,
+                              nullptr, ACT_NONE, sc, scf));
+  if (g->f2h_b) ABCD_TRY((hipError_t)colsum(s, w.dhid, Htot, B, Htot, nullptr, g->f2h_b, 0.f, sc, scf));
   const abcd_rnn_g& cg = g->cell;
   if (cg.w_ih) {
     if (c->feedback)

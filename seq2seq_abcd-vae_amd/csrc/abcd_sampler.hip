@@ -420,16 +420,23 @@ extern "C" int abcd_sampler_kl(const abcd_sampler_cfg* c, const abcd_sampler_par
 }
 
 // ---- backward, split the way autograd sees the reference (three Functions) ----
+// Every piece takes two streams: `s` carries the data-gradient chain to d_h
+// (the encoder backward waits on it), `sw` the parameter gradients, which
+// nothing reads before the caller joins sw (clip + SGD).  With sw == s it is
+// one in-order stream.  Only sw uses the workspace's split-K scratch, so the
+// two never share a buffer that either writes.
+namespace {
+struct SideWork {  // parameter-gradient launches: side-stream tiling when sw != s
+  GemmSideScope scope;
+  explicit SideWork(hipStream_t s, hipStream_t sw) : scope(sw != s) {}
+};
+}  // namespace
+
 // sample():  d_feats -> d_logits (write), d_codebook (write)
 //   ABCD : feats = softmax((l+g)/tau) C^T        plain: feats = mu + e^{lv/2} eps
-extern "C" int abcd_sampler_sample_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, int B, int mode,
-                                            float temperature, const float* d_feats, float* d_logits,
-                                            float* d_codebook, void* ws, size_t ws_bytes, void* stream) {
-  ABCD_REQUIRE(samp_check(c) == 0 && p && d_feats && d_logits && ws && B > 0);
-  hipStream_t s = (hipStream_t)stream;
-  Arena A(ws, ws_bytes);
-  SampWS w = carve_sampler(A, c, B);
-  ABCD_REQUIRE(A.ok);
+static int samp_sample_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p, int B, int mode,
+                           float temperature, const float* d_feats, float* d_logits, float* d_codebook,
+                           const SampWS& w, hipStream_t s, hipStream_t sw) {
   const int D = c->feature_dim, K = c->num_categories;
   if (c->plain) {
     plain_dparams<<<std::max(1, std::min(4096, cdiv((long)B * D, 256))), 256, 0, s>>>(w.MV, w.EPS, B, D, d_feats,
@@ -439,9 +446,11 @@ extern "C" int abcd_sampler_sample_backward(const abcd_sampler_cfg* c, const abc
   }
   ABCD_TRY((hipError_t)gemm(s, B, K, D, opKC(d_feats, D, B), opKM(p->codebook, K, K), w.dY, K, 1.f, 0.f, nullptr,
                             ACT_NONE, nullptr, 0));
-  if (d_codebook)
-    ABCD_TRY((hipError_t)gemm(s, D, K, B, opKM(d_feats, D, D), opKM(w.Y, K, K), d_codebook, K, 1.f, 0.f, nullptr,
+  if (d_codebook) {
+    SideWork side(s, sw);
+    ABCD_TRY((hipError_t)gemm(sw, D, K, B, opKM(d_feats, D, D), opKM(w.Y, K, K), d_codebook, K, 1.f, 0.f, nullptr,
                               ACT_NONE, w.scratch, w.scratch_floats));
+  }
   sample_softmax_bwd<<<cdiv(B, 4), 256, 0, s>>>(w.Y, w.dY, B, K, mode == ABCD_SAMPLE_GUMBEL ? temperature : 1.f, 0,
                                                 d_logits);
   ABCD_CHECK_LAUNCH();
@@ -449,14 +458,9 @@ extern "C" int abcd_sampler_sample_backward(const abcd_sampler_cfg* c, const abc
 }
 
 // kl_divergence(): d_kl (device scalar) -> d_logits (write or accumulate), d_psl (write)
-extern "C" int abcd_sampler_kl_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, int B, double N,
-                                        const float* d_kl, int accumulate, float* d_logits, float* d_psl, void* ws,
-                                        size_t ws_bytes, void* stream) {
-  ABCD_REQUIRE(samp_check(c) == 0 && p && d_kl && d_logits && ws && B > 0);
-  hipStream_t s = (hipStream_t)stream;
-  Arena A(ws, ws_bytes);
-  SampWS w = carve_sampler(A, c, B);
-  ABCD_REQUIRE(A.ok);
+static int samp_kl_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p, int B, double N, const float* d_kl,
+                       int accumulate, float* d_logits, float* d_psl, const SampWS& w, hipStream_t s,
+                       hipStream_t sw) {
   const int D = c->feature_dim, K = c->num_categories;
   if (c->plain) {
     if (accumulate) {
@@ -472,10 +476,11 @@ extern "C" int abcd_sampler_kl_backward(const abcd_sampler_cfg* c, const abcd_sa
   }
   kl_rows_bwd<<<cdiv(B, 4), 256, 0, s>>>(w.Q, w.elog, w.v, B, K, d_kl, accumulate, d_logits);
   ABCD_CHECK_LAUNCH();
-  if (d_psl) {
-    ABCD_TRY((hipError_t)colsum(s, w.Q, K, B, K, nullptr, w.Qsum, 0.f, w.scratch, w.scratch_floats));
-    kl_prior_bwd<<<1, 256, 0, s>>>(w.p, w.alpha, w.tri, w.kl_small, w.Qsum, K, B, N, p->prior_concentration, d_kl,
-                                   d_psl);
+  if (d_psl) {  // forward products only: no wait on s beyond the caller's fork
+    SideWork side(s, sw);
+    ABCD_TRY((hipError_t)colsum(sw, w.Q, K, B, K, nullptr, w.Qsum, 0.f, w.scratch, w.scratch_floats));
+    kl_prior_bwd<<<1, 256, 0, sw>>>(w.p, w.alpha, w.tri, w.kl_small, w.Qsum, K, B, N, p->prior_concentration, d_kl,
+                                    d_psl);
     ABCD_CHECK_LAUNCH();
   }
   return 0;
@@ -483,48 +488,54 @@ extern "C" int abcd_sampler_kl_backward(const abcd_sampler_cfg* c, const abcd_sa
 
 // forward(): d_logits (plain: d [mean|log_var]) -> MLP grads, codebook grad of
 // logits = U C / sqrt(D) (written, or accumulated when accumulate_codebook), d_h
-extern "C" int abcd_sampler_forward_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
-                                             int B, const float* d_logits, float* d_h, const abcd_sampler_grads* g,
-                                             int accumulate_codebook, void* ws, size_t ws_bytes, void* stream) {
-  ABCD_REQUIRE(samp_check(c) == 0 && p && h && d_logits && g && ws && B > 0);
-  hipStream_t s = (hipStream_t)stream;
-  Arena A(ws, ws_bytes);
-  SampWS w = carve_sampler(A, c, B);
-  ABCD_REQUIRE(A.ok);
+static int samp_fwd_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h, int B,
+                        const float* d_logits, float* d_h, const abcd_sampler_grads* g, int accumulate_codebook,
+                        const SampWS& w, hipStream_t s, hipStream_t sw) {
   const int E = c->input_size, Hm = c->mlp_hidden, D = c->feature_dim, K = c->num_categories;
   float* sc = w.scratch;
   const size_t scf = w.scratch_floats;
   const int nm = c->plain ? 2 : 1;
   const float* dOut[2];
   long ldOut;
+  ABCD_TRY((hipError_t)stream_fork(s, sw, 1));  // d_logits final
   if (c->plain) {
     dOut[0] = d_logits; dOut[1] = d_logits + D; ldOut = 2 * D;
   } else {
     const float rs = 1.f / sqrtf((float)D);
-    if (g->codebook)
-      ABCD_TRY((hipError_t)gemm(s, D, K, B, opKM(w.U, D, D), opKM(d_logits, K, K), g->codebook, K, rs,
+    if (g->codebook) {
+      SideWork side(s, sw);
+      ABCD_TRY((hipError_t)gemm(sw, D, K, B, opKM(w.U, D, D), opKM(d_logits, K, K), g->codebook, K, rs,
                                 accumulate_codebook ? 1.f : 0.f, nullptr, ACT_NONE, sc, scf));
+    }
     ABCD_TRY((hipError_t)gemm(s, B, D, K, opKC(d_logits, K, B), opKC(p->codebook, K, D), w.dU, D, rs, 0.f, nullptr,
                               ACT_NONE, nullptr, 0));
+    ABCD_TRY((hipError_t)stream_fork(s, sw, 2));  // dU
     dOut[0] = w.dU; dOut[1] = nullptr; ldOut = D;
   }
   for (int k = 0; k < nm; ++k) {
     const abcd_mlp_w& m = p->mlp[k];
     const abcd_mlp_g& mg = g->mlp[k];
-    if (mg.w2)
-      ABCD_TRY((hipError_t)gemm(s, D, Hm, B, opKM(dOut[k], ldOut, D), opKM(w.Z1[k], Hm, Hm), mg.w2, Hm, 1.f, 0.f,
-                                nullptr, ACT_NONE, sc, scf));
-    if (mg.b2) ABCD_TRY((hipError_t)colsum(s, dOut[k], ldOut, B, D, nullptr, mg.b2, 0.f, sc, scf));
+    {
+      SideWork side(s, sw);
+      if (mg.w2)
+        ABCD_TRY((hipError_t)gemm(sw, D, Hm, B, opKM(dOut[k], ldOut, D), opKM(w.Z1[k], Hm, Hm), mg.w2, Hm, 1.f, 0.f,
+                                  nullptr, ACT_NONE, sc, scf));
+      if (mg.b2) ABCD_TRY((hipError_t)colsum(sw, dOut[k], ldOut, B, D, nullptr, mg.b2, 0.f, sc, scf));
+    }
     ABCD_TRY((hipError_t)pack2d(s, m.w2, Hm, Hm, D, true, w.W2T[k], D, Hm, D));
     ABCD_TRY((hipError_t)gemm(s, B, Hm, D, opKC(dOut[k], ldOut, B), opKC(w.W2T[k], D, Hm), w.dZ1[k], Hm, 1.f, 0.f,
                               nullptr, ACT_NONE, nullptr, 0));
     tanh_bwd_inplace<<<std::max(1, std::min(2048, cdiv((long)B * Hm, 256))), 256, 0, s>>>(w.dZ1[k], w.Z1[k],
                                                                                           (long)B * Hm);
     ABCD_CHECK_LAUNCH();
-    if (mg.w1)
-      ABCD_TRY((hipError_t)gemm(s, Hm, E, B, opKM(w.dZ1[k], Hm, Hm), opKM(h, E, E), mg.w1, E, 1.f, 0.f, nullptr,
-                                ACT_NONE, sc, scf));
-    if (mg.b1) ABCD_TRY((hipError_t)colsum(s, w.dZ1[k], Hm, B, Hm, nullptr, mg.b1, 0.f, sc, scf));
+    ABCD_TRY((hipError_t)stream_fork(s, sw, 3));  // dZ1[k]
+    {
+      SideWork side(s, sw);
+      if (mg.w1)
+        ABCD_TRY((hipError_t)gemm(sw, Hm, E, B, opKM(w.dZ1[k], Hm, Hm), opKM(h, E, E), mg.w1, E, 1.f, 0.f, nullptr,
+                                  ACT_NONE, sc, scf));
+      if (mg.b1) ABCD_TRY((hipError_t)colsum(sw, w.dZ1[k], Hm, B, Hm, nullptr, mg.b1, 0.f, sc, scf));
+    }
     if (d_h) {
       ABCD_TRY((hipError_t)pack2d(s, m.w1, E, E, Hm, true, w.W1T[k], Hm, E, Hm));
       ABCD_TRY((hipError_t)gemm(s, B, E, Hm, opKC(w.dZ1[k], Hm, B), opKC(w.W1T[k], Hm, E), d_h, E, 1.f,
@@ -534,21 +545,60 @@ extern "C" int abcd_sampler_forward_backward(const abcd_sampler_cfg* c, const ab
   return 0;
 }
 
-// fused: sample + kl + forward backward in one call (the training step)
-extern "C" int abcd_sampler_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h, int B,
-                                     int mode, float temperature, double N, const float* d_feats, const float* d_kl,
-                                     float* d_h, const abcd_sampler_grads* g, void* ws, size_t ws_bytes,
-                                     void* stream) {
-  ABCD_REQUIRE(samp_check(c) == 0 && p && h && g && ws && B > 0);
+static int samp_ws(const abcd_sampler_cfg* c, int B, void* ws, size_t ws_bytes, SampWS* w) {
   Arena A(ws, ws_bytes);
-  SampWS w = carve_sampler(A, c, B);
-  ABCD_REQUIRE(A.ok);
+  *w = carve_sampler(A, c, B);
+  return A.ok ? 0 : ABCD_EINVAL;
+}
+
+extern "C" int abcd_sampler_sample_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, int B, int mode,
+                                            float temperature, const float* d_feats, float* d_logits,
+                                            float* d_codebook, void* ws, size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(samp_check(c) == 0 && p && d_feats && d_logits && ws && B > 0);
+  SampWS w;
+  ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
+  hipStream_t s = (hipStream_t)stream;
+  return samp_sample_bwd(c, p, B, mode, temperature, d_feats, d_logits, d_codebook, w, s, s);
+}
+
+extern "C" int abcd_sampler_kl_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, int B, double N,
+                                        const float* d_kl, int accumulate, float* d_logits, float* d_psl, void* ws,
+                                        size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(samp_check(c) == 0 && p && d_kl && d_logits && ws && B > 0);
+  SampWS w;
+  ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
+  hipStream_t s = (hipStream_t)stream;
+  return samp_kl_bwd(c, p, B, N, d_kl, accumulate, d_logits, d_psl, w, s, s);
+}
+
+extern "C" int abcd_sampler_forward_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
+                                             int B, const float* d_logits, float* d_h, const abcd_sampler_grads* g,
+                                             int accumulate_codebook, void* ws, size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(samp_check(c) == 0 && p && h && d_logits && g && ws && B > 0);
+  SampWS w;
+  ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
+  hipStream_t s = (hipStream_t)stream;
+  return samp_fwd_bwd(c, p, h, B, d_logits, d_h, g, accumulate_codebook, w, s, s);
+}
+
+// fused: sample + kl + forward backward in one call (the training step).
+// wgrad_stream (may be NULL or == stream): where the parameter gradients go;
+// the caller joins it before reading them.
+extern "C" int abcd_sampler_backward_split(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
+                                           int B, int mode, float temperature, double N, const float* d_feats,
+                                           const float* d_kl, float* d_h, const abcd_sampler_grads* g, void* ws,
+                                           size_t ws_bytes, void* stream, void* wgrad_stream) {
+  ABCD_REQUIRE(samp_check(c) == 0 && p && h && g && ws && B > 0);
+  SampWS w;
+  ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
+  hipStream_t s = (hipStream_t)stream;
+  hipStream_t sw = wgrad_stream ? (hipStream_t)wgrad_stream : s;
+  ABCD_TRY((hipError_t)stream_fork(s, sw, 0));  // d_feats and the forward products
   const int D = c->feature_dim, K = c->num_categories;
   float* dL = c->plain ? w.dMV + 0 : w.dL;
   int have = 0;
   if (c->plain) {
     // plain_dparams handles both terms in one pass
-    hipStream_t s = (hipStream_t)stream;
     plain_dparams<<<std::max(1, std::min(4096, cdiv((long)B * D, 256))), 256, 0, s>>>(w.MV, w.EPS, B, D, d_feats,
                                                                                       d_kl, w.dL);
     ABCD_CHECK_LAUNCH();
@@ -556,24 +606,29 @@ extern "C" int abcd_sampler_backward(const abcd_sampler_cfg* c, const abcd_sampl
     have = 1;
   } else {
     if (d_feats) {
-      ABCD_TRY((hipError_t)abcd_sampler_sample_backward(c, p, B, mode, temperature, d_feats, dL, g->codebook, ws,
-                                                        ws_bytes, stream));
+      ABCD_TRY((hipError_t)samp_sample_bwd(c, p, B, mode, temperature, d_feats, dL, g->codebook, w, s, sw));
       have = 1;
     }
     if (d_kl) {
-      ABCD_TRY((hipError_t)abcd_sampler_kl_backward(c, p, B, N, d_kl, have, dL, g->posterior_shape_logits, ws,
-                                                    ws_bytes, stream));
+      ABCD_TRY((hipError_t)samp_kl_bwd(c, p, B, N, d_kl, have, dL, g->posterior_shape_logits, w, s, sw));
       have = 1;
     } else if (g->posterior_shape_logits) {
-      ABCD_TRY(hipMemsetAsync(g->posterior_shape_logits, 0, (size_t)K * 4, (hipStream_t)stream));
+      ABCD_TRY(hipMemsetAsync(g->posterior_shape_logits, 0, (size_t)K * 4, sw));
     }
     if (!have) {
-      ABCD_TRY(hipMemsetAsync(dL, 0, (size_t)B * K * 4, (hipStream_t)stream));
-      if (g->codebook) ABCD_TRY(hipMemsetAsync(g->codebook, 0, (size_t)D * K * 4, (hipStream_t)stream));
+      ABCD_TRY(hipMemsetAsync(dL, 0, (size_t)B * K * 4, s));
+      if (g->codebook) ABCD_TRY(hipMemsetAsync(g->codebook, 0, (size_t)D * K * 4, sw));
     }
   }
-  return abcd_sampler_forward_backward(c, p, h, B, dL, d_h, g, c->plain ? 0 : (d_feats ? 1 : 0), ws, ws_bytes,
-                                       stream);
+  return samp_fwd_bwd(c, p, h, B, dL, d_h, g, c->plain ? 0 : (d_feats ? 1 : 0), w, s, sw);
+}
+
+extern "C" int abcd_sampler_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h, int B,
+                                     int mode, float temperature, double N, const float* d_feats, const float* d_kl,
+                                     float* d_h, const abcd_sampler_grads* g, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  return abcd_sampler_backward_split(c, p, h, B, mode, temperature, N, d_feats, d_kl, d_h, g, ws, ws_bytes, stream,
+                                     nullptr);
 }
 
 // learning.py:171-178 perplexities (single workgroup; diagnostics only).

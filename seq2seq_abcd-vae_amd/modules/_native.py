@@ -99,6 +99,9 @@ _SIGS = {
                                 c_size_t, c_void_p]),
     "abcd_sampler_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float, c_double,
                                       c_void_p, c_void_p, c_void_p, _P(SamplerGrads), c_void_p, c_size_t, c_void_p]),
+    "abcd_sampler_backward_split": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float,
+                                            c_double, c_void_p, c_void_p, c_void_p, _P(SamplerGrads), c_void_p,
+                                            c_size_t, c_void_p, c_void_p]),
     "abcd_sampler_sample_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_int, c_float, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_kl_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_double, c_void_p, c_int,

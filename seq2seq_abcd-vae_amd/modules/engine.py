@@ -14,6 +14,8 @@ synchronises with the host; loss terms and diagnostics stay on the device in
 """
 import itertools
 
+import os
+
 import torch
 
 from . import _native as N
@@ -173,17 +175,21 @@ class FusedStep:
             return sc, logits
         inv = self._inv_b(B)
         d_feats = torch.empty(B, self.Dfeat, device=dev)
-        # the decoder's weight-gradient reductions run on a side stream beside
-        # the sampler + encoder backward (joined below, before clip + SGD)
+        # the decoder's and sampler's weight-gradient reductions run on a side
+        # stream beside the d_h chain + encoder backward (joined below, before
+        # clip + SGD)
         side = self._side_stream()
         N.check(L_.abcd_decoder_backward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
                                                  N.ptr(xmask), N.ptr(inv), N.ptr(inv), N.ptr(d_feats), self.dec_g,
                                                  N.ptr(ws_d), ws_d.numel(), st, N.c_void_p(side.cuda_stream)),
                 "decoder backward")
         d_h = torch.empty(B, self.E, device=dev)
-        N.check(L_.abcd_sampler_backward(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, float(entire_data_size),
-                                         N.ptr(d_feats), N.ptr(inv), N.ptr(d_h), self.samp_g, N.ptr(ws_s),
-                                         ws_s.numel(), st), "sampler backward")
+        # parameter gradients of the sampler join the decoder's on the side stream
+        N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
+                                               float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
+                                               self.samp_g, N.ptr(ws_s), ws_s.numel(), st,
+                                               N.c_void_p(None if os.environ.get("ABCD_SAMPSPLIT") == "0"
+                                                          else side.cuda_stream)), "sampler backward")
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
                                                  self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
                                                  N.c_void_p(side.cuda_stream)), "encoder backward")

@@ -194,3 +194,28 @@ def test_decoder_input_dropout_persist_vs_stepwise(rnn):
         assert abs(sc_p[k] - sc_s[k]) <= 1e-5 * abs(sc_s[k]) + 1e-6, (k, sc_p[k].item(), sc_s[k].item())
     assert _rel(g_p, g_s) < 1e-4
     assert sc_p[0] != sc_0[0] and _rel(g_p, g_0) > 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name", ["c2", "c4", "c5"])
+def test_sampler_wgrad_stream_bit_exact(cfg_name):
+    """The sampler's parameter gradients (and feature2hidden's) queued on the
+    weight-gradient stream beside the d_h chain give the one-stream order's
+    results (ABCD_SAMPSPLIT=0): losses bit-identical, gradients within 1e-6
+    (the side-stream GEMMs pick a smaller split-K, another summation order)."""
+    import bench
+    cfg = bench.CONFIGS[cfg_name]
+    step = bench.build(cfg, "cuda")
+    batch = bench.make_batch(cfg, 0, "cuda")
+    sc_d, g_d = _fused_run(step, batch, True)
+    old = os.environ.get("ABCD_SAMPSPLIT")
+    os.environ["ABCD_SAMPSPLIT"] = "0"
+    try:
+        sc_o, g_o = _fused_run(step, batch, True)
+    finally:
+        if old is None:
+            os.environ.pop("ABCD_SAMPSPLIT", None)
+        else:
+            os.environ["ABCD_SAMPSPLIT"] = old
+    assert torch.equal(sc_o[:4], sc_d[:4])
+    assert _rel(g_o, g_d) < 1e-6
