@@ -114,6 +114,10 @@ inline size_t persist_sync_uints(int nd, int B) { return (size_t)(66 * persist_g
 // Copy off[0..T] to device memory `dst` on stream s through a pinned ring
 // (asynchronous, no host/device synchronisation).
 int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst);
+// The same copy left pending: the next persistent launch's counter reset on s
+// performs it (one kernel); flush_offsets() issues it if no launch took it.
+int stage_offsets(hipStream_t s, const std::vector<int>& off, int* dst);
+int flush_offsets();
 
 // Launch the persistent kernel if its grid can be co-resident on this device
 // (*launched = true); otherwise leave *launched = false (caller runs the

@@ -1745,31 +1745,83 @@ bool persist_enabled() {
   return !(v && v[0] == '0');
 }
 
-int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst) {
-  constexpr int NSLOT = 32;
-  constexpr size_t SLOT = 64 * 1024;
-  static std::mutex mu;
-  static char* ring = nullptr;
-  static hipEvent_t ev[NSLOT];
-  static bool used[NSLOT];
-  static int next = 0;
+// Pinned ring of offset tables.  upload_offsets copies one to the device with
+// hipMemcpyAsync.  stage_offsets only fills a slot and leaves the copy pending
+// (per host thread): the next zero_sync on the same stream folds it into the
+// counter-reset kernel (one launch instead of a copy and two fills before
+// each persistent kernel); flush_offsets issues a pending copy that no reset
+// took (the per-step fallback paths).
+namespace {
+constexpr int OFF_NSLOT = 32;
+constexpr size_t OFF_SLOT = 64 * 1024;
+std::mutex g_off_mu;
+char* g_off_ring = nullptr;
+hipEvent_t g_off_ev[OFF_NSLOT];
+bool g_off_used[OFF_NSLOT];
+int g_off_next = 0;
+struct PendingOff {
+  hipStream_t s;
+  int* dst;
+  const int* src;  // pinned host slot
+  int n, slot;
+  bool on;
+};
+thread_local PendingOff g_pend{};
+
+int off_slot(const std::vector<int>& off, int* slot_out, const int** src) {
   const size_t bytes = off.size() * sizeof(int);
-  if (bytes > SLOT) return (int)hipErrorInvalidValue;
-  std::lock_guard<std::mutex> lk(mu);
-  if (!ring) {
-    ABCD_TRY(hipHostMalloc((void**)&ring, SLOT * NSLOT, hipHostMallocDefault));
-    for (int k = 0; k < NSLOT; ++k) {
-      ABCD_TRY(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
-      used[k] = false;
+  if (bytes > OFF_SLOT) return (int)hipErrorInvalidValue;
+  std::lock_guard<std::mutex> lk(g_off_mu);
+  if (!g_off_ring) {
+    ABCD_TRY(hipHostMalloc((void**)&g_off_ring, OFF_SLOT * OFF_NSLOT, hipHostMallocDefault));
+    for (int k = 0; k < OFF_NSLOT; ++k) {
+      ABCD_TRY(hipEventCreateWithFlags(&g_off_ev[k], hipEventDisableTiming));
+      g_off_used[k] = false;
     }
   }
-  const int k = next;
-  next = (next + 1) % NSLOT;
-  if (used[k]) ABCD_TRY(hipEventSynchronize(ev[k]));  // the copy that last read this slot is done
-  std::copy(off.begin(), off.end(), (int*)(ring + k * SLOT));
-  ABCD_TRY(hipMemcpyAsync(dst, ring + k * SLOT, bytes, hipMemcpyHostToDevice, s));
-  ABCD_TRY(hipEventRecord(ev[k], s));
-  used[k] = true;
+  const int k = g_off_next;
+  g_off_next = (g_off_next + 1) % OFF_NSLOT;
+  if (g_off_used[k]) ABCD_TRY(hipEventSynchronize(g_off_ev[k]));  // the op that last read this slot is done
+  g_off_used[k] = false;
+  std::copy(off.begin(), off.end(), (int*)(g_off_ring + k * OFF_SLOT));
+  *slot_out = k;
+  *src = (const int*)(g_off_ring + k * OFF_SLOT);
+  return 0;
+}
+int off_release(hipStream_t s, int k) {  // after the op that reads slot k is queued on s
+  ABCD_TRY(hipEventRecord(g_off_ev[k], s));
+  std::lock_guard<std::mutex> lk(g_off_mu);
+  g_off_used[k] = true;
+  return 0;
+}
+}  // namespace
+
+int flush_offsets() {
+  if (!g_pend.on) return 0;
+  g_pend.on = false;
+  ABCD_TRY(hipMemcpyAsync(g_pend.dst, g_pend.src, (size_t)g_pend.n * sizeof(int), hipMemcpyHostToDevice, g_pend.s));
+  return off_release(g_pend.s, g_pend.slot);
+}
+
+// a table staged by a call that returned early (error path) is dropped, never
+// copied: its destination workspace may be gone
+static void drop_stale_offsets() { g_pend.on = false; }
+
+int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst) {
+  drop_stale_offsets();
+  int k;
+  const int* src;
+  ABCD_TRY((hipError_t)off_slot(off, &k, &src));
+  ABCD_TRY(hipMemcpyAsync(dst, src, off.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  return off_release(s, k);
+}
+
+int stage_offsets(hipStream_t s, const std::vector<int>& off, int* dst) {
+  drop_stale_offsets();
+  int k;
+  const int* src;
+  ABCD_TRY((hipError_t)off_slot(off, &k, &src));
+  g_pend = PendingOff{s, dst, src, (int)off.size(), k, true};
   return 0;
 }
 
@@ -1792,12 +1844,38 @@ static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
 // cycles per step), so by default XCD 0's ticket count is pre-loaded with 1,
 // the grid never looks evenly spread and every workgroup takes the fallback
 // roles with sc1 hand-off stores.
-static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
-  hipError_t e = hipMemsetAsync(
-      sync, 0, (size_t)(2 * ngroups + PERSIST_REG_LINES + PERSIST_FLAG_LINES * ngroups) * PERSIST_SYNC_STRIDE * 4, s);
+// One launch: every sync word zeroed, XCD 0's ticket pre-loaded (unless
+// ABCD_XCD=1) and, when a staged offset table is pending on s, that table
+// read from its pinned host slot into device memory.
+__global__ __launch_bounds__(256) void persist_reset(unsigned* sync, long nwords, long ticket, const int* off_src,
+                                                     int* off_dst, int noff) {
+  const long i0 = (long)blockIdx.x * 256 + threadIdx.x, stride = (long)gridDim.x * 256;
+  for (long i = i0; i < nwords / 4; i += stride) {
+    uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    if (i == ticket / 4) z.x = 1u;  // ticket is a multiple of PERSIST_SYNC_STRIDE (-1: none)
+    reinterpret_cast<uint4*>(sync)[i] = z;
+  }
+  for (long i = i0; i < noff; i += stride) off_dst[i] = off_src[i];
+}
+
+static int zero_sync_impl(hipStream_t s, unsigned* sync, int ngroups) {
+  const long nwords = (long)(2 * ngroups + PERSIST_REG_LINES + PERSIST_FLAG_LINES * ngroups) * PERSIST_SYNC_STRIDE;
   const char* v = getenv("ABCD_XCD");
-  if (e == hipSuccess && !(v && v[0] == '1')) e = hipMemsetAsync(sync + (size_t)ngroups * PERSIST_SYNC_STRIDE, 1, 1, s);
-  return e;
+  const long ticket = (v && v[0] == '1') ? -1 : (long)ngroups * PERSIST_SYNC_STRIDE;
+  const bool take = g_pend.on && g_pend.s == s;
+  const int* src = nullptr;
+  if (take) ABCD_TRY(hipHostGetDevicePointer((void**)&src, (void*)g_pend.src, 0));
+  const int blocks = (int)std::min<long>(64, std::max<long>(1, (nwords / 4 + 255) / 256));
+  persist_reset<<<blocks, 256, 0, s>>>(sync, nwords, ticket, src, take ? g_pend.dst : nullptr, take ? g_pend.n : 0);
+  ABCD_TRY(hipGetLastError());
+  if (take) {
+    g_pend.on = false;
+    ABCD_TRY((hipError_t)off_release(s, g_pend.slot));
+  }
+  return 0;
+}
+static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
+  return (hipError_t)zero_sync_impl(s, sync, ngroups);
 }
 
 // per-member flag hand-offs unless ABCD_FLAGS=0 (then the group counter)

@@ -429,7 +429,7 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
         f.rev = d == 1;
         f.X = X; f.ldx = Inp; f.Wih = w.Wihp[l] + (size_t)d * G * H * Inp; f.bih = w.bcat[l] + d * G * H;
       }
-      if (l == 0 && persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+      if (l == 0 && persist_enabled()) ABCD_TRY((hipError_t)stage_offsets(s, off, w.off));
       // layer 0: input projection fused into the persistent kernel when it fits;
       // otherwise the L x D*G*H projection GEMM feeds the recurrence
       if (l == 0) ABCD_TRY((hipError_t)persist_encoder_fwd_fused(s, G, pa, &done));
@@ -438,6 +438,7 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
                                   (long)D * G * H, 1.f, 0.f, w.bcat[l], ACT_NONE, w.scratch, w.scratch_floats));
         ABCD_TRY((hipError_t)persist_encoder_fwd(s, G, pa, &done));
       }
+      ABCD_TRY((hipError_t)flush_offsets());
     }
     for (int i = 0; i < T && !done && !(diag_mask() & 8); ++i) {
       FwdArgs a{};
@@ -541,7 +542,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
         b.dGX = w.dGX[l][d]; b.dGH = w.dGH[l][d];
         b.rev = d == 1;
       }
-      if (l == c->layers - 1 && persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+      if (l == c->layers - 1 && persist_enabled()) ABCD_TRY((hipError_t)stage_offsets(s, off, w.off));
       // gated overlap (single layer, side stream given): the weight gradients
       // of the rows the BPTT finishes in its first half run on wgrad_stream
       // beside the second half (split-K kernel only: write-through stashes)
@@ -550,6 +551,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done, zeroed));
       if (gate_ok && !done) ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done));  // gather form
       else if (gate_ok && done) gated = true;
+      ABCD_TRY((hipError_t)flush_offsets());
     }
     for (int i = 0; i < T && !done; ++i) {
       BwdArgs a{};
@@ -1066,8 +1068,9 @@ extern "C" int abcd_decoder_forward_dropout(const abcd_decoder_cfg* c, const abc
     pa.eps = eps; pa.seed = seed; pa.offset = offset; pa.xmask = xmask;
     pa.Xin = w.Xin; pa.Hprev = w.Hprev; pa.Cprev = w.Cprev; pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Hs = w.Hs;
     pa.Aact = w.Aact; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
-    if (persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+    if (persist_enabled()) ABCD_TRY((hipError_t)stage_offsets(s, off, w.off));
     ABCD_TRY((hipError_t)persist_decoder_fwd(s, G, pa, &done));
+    ABCD_TRY((hipError_t)flush_offsets());
   }
   for (int t = 0; t < T && !done; ++t) {
     const int b_t = (int)bs[t];
@@ -1210,8 +1213,9 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
     pa.dG = w.dGX; pa.dMU = w.dMU; pa.dLV = w.dLV; pa.dZ = w.dZ; pa.DHR = w.DC; pa.DC0 = w.DC0;
     pa.Hprev = w.Hprev; pa.dGH = w.dGH;
     pa.part = w.skp;
-    if (persist_enabled()) ABCD_TRY((hipError_t)upload_offsets(s, off, w.off));
+    if (persist_enabled()) ABCD_TRY((hipError_t)stage_offsets(s, off, w.off));
     ABCD_TRY((hipError_t)persist_decoder_bwd(s, G, pa, &done));
+    ABCD_TRY((hipError_t)flush_offsets());
   }
   const int TN = bwd_tn(H);
   for (int t = T - 1; t >= 0 && !done; --t) {

@@ -175,26 +175,44 @@ class FusedStep:
             return sc, logits
         inv = self._inv_b(B)
         d_feats = torch.empty(B, self.Dfeat, device=dev)
-        # the decoder's and sampler's weight-gradient reductions run on a side
-        # stream beside the d_h chain + encoder backward (joined below, before
-        # clip + SGD)
+        # the decoder's weight-gradient reductions run on a side stream beside
+        # the sampler + encoder backward (joined below, before clip + SGD).
+        # ABCD_DECSIDE=0 keeps them on the main stream: measured at c2 the
+        # encoder BPTT then runs 1.85 ms instead of 2.37, but the step is
+        # ~0.55 ms longer (the wgrads cost ~1.05 ms alone)
         side = self._side_stream()
         N.check(L_.abcd_decoder_backward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
                                                  N.ptr(xmask), N.ptr(inv), N.ptr(inv), N.ptr(d_feats), self.dec_g,
-                                                 N.ptr(ws_d), ws_d.numel(), st, N.c_void_p(side.cuda_stream)),
+                                                 N.ptr(ws_d), ws_d.numel(), st,
+                                                 N.c_void_p(None if os.environ.get("ABCD_DECSIDE") == "0"
+                                                            else side.cuda_stream)),
                 "decoder backward")
         d_h = torch.empty(B, self.E, device=dev)
-        # parameter gradients of the sampler join the decoder's on the side stream
         N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
                                                float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
                                                self.samp_g, N.ptr(ws_s), ws_s.numel(), st,
-                                               N.c_void_p(None if os.environ.get("ABCD_SAMPSPLIT") == "0"
-                                                          else side.cuda_stream)), "sampler backward")
+                                               N.c_void_p(self._sampler_wgrad_stream(side))), "sampler backward")
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
                                                  self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
                                                  N.c_void_p(side.cuda_stream)), "encoder backward")
         torch.cuda.current_stream(dev).wait_stream(side)
+        if getattr(self, "_side2", None) is not None:
+            torch.cuda.current_stream(dev).wait_stream(self._side2)
         return sc, logits
+
+    def _sampler_wgrad_stream(self, side):
+        # Default: one stream.  Measured at c2 (same box, A/B): the sampler's
+        # parameter gradients on the wgrad stream (1) or a third stream (2)
+        # shorten the chain into the encoder BPTT by ~150 us but slow the
+        # BPTT by ~200 us (more side work co-resident with its workgroups).
+        mode = os.environ.get("ABCD_SAMPSPLIT", "0")
+        if mode == "0":
+            return None
+        if mode == "1":
+            return side.cuda_stream
+        if getattr(self, "_side2", None) is None:
+            self._side2 = torch.cuda.Stream(self.device)
+        return self._side2.cuda_stream
 
     def _side_stream(self):
         s = getattr(self, "_side", None)

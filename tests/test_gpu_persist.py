@@ -198,10 +198,11 @@ def test_decoder_input_dropout_persist_vs_stepwise(rnn):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg_name", ["c2", "c4", "c5"])
-def test_sampler_wgrad_stream_bit_exact(cfg_name):
-    """The sampler's parameter gradients (and feature2hidden's) queued on the
-    weight-gradient stream beside the d_h chain give the one-stream order's
-    results (ABCD_SAMPSPLIT=0): losses bit-identical, gradients within 1e-6
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_sampler_wgrad_stream_matches_one_stream(cfg_name, mode):
+    """The sampler's parameter gradients queued on the weight-gradient stream
+    (ABCD_SAMPSPLIT=1) or a third stream (2) beside the d_h chain give the
+    one-stream default's results: losses bit-identical, gradients within 1e-6
     (the side-stream GEMMs pick a smaller split-K, another summation order)."""
     import bench
     cfg = bench.CONFIGS[cfg_name]
@@ -209,7 +210,7 @@ def test_sampler_wgrad_stream_bit_exact(cfg_name):
     batch = bench.make_batch(cfg, 0, "cuda")
     sc_d, g_d = _fused_run(step, batch, True)
     old = os.environ.get("ABCD_SAMPSPLIT")
-    os.environ["ABCD_SAMPSPLIT"] = "0"
+    os.environ["ABCD_SAMPSPLIT"] = mode
     try:
         sc_o, g_o = _fused_run(step, batch, True)
     finally:
