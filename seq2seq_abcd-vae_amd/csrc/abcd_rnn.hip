@@ -288,6 +288,32 @@ static int bwd_tn(int H) { return (H / 16) % 4 == 0 ? 64 : ((H / 16) % 2 == 0 ? 
 // ===========================================================================
 // ENCODER
 // ===========================================================================
+// Bias gradients folded into the input weight-gradient GEMM (layer 0 with a
+// padded input, Fp > F): column F of the padded frame copy Xp is set to 1 after
+// the forward has used it, so the GEMM dG^T [X | 1] of width F + 1 yields
+// dW_ih and, in its last column, sum_r dG[r] = the bias gradient -- one
+// colsum pass over the L x G*H gate gradients fewer per direction.
+__global__ __launch_bounds__(256) void set_col_kernel(float* X, long ld, long rows, int col, float v) {
+  for (long r = (long)blockIdx.x * 256 + threadIdx.x; r < rows; r += (long)gridDim.x * 256) X[r * ld + col] = v;
+}
+__global__ __launch_bounds__(256) void split_wb_kernel(const float* dWx, int rows, int F, float* w, float* b1,
+                                                       float* b2) {
+  const long n = (long)rows * (F + 1);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / (F + 1)), j = (int)(i % (F + 1));
+    const float v = dWx[i];
+    if (j < F) w[(long)r * F + j] = v;
+    else {
+      b1[r] = v;
+      if (b2) b2[r] = v;
+    }
+  }
+}
+static bool bias_col_enabled() {
+  const char* v = getenv("ABCD_BIASCOL");  // read per call: tests flip it in-process
+  return !(v && v[0] == '0');
+}
+
 struct EncWS {
   float* Xp;
   float* Wihp[ABCD_MAX_LAYERS];
@@ -508,7 +534,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
   EncWS w = carve_encoder(A, c, x->T, x->L, x->B);
   ABCD_REQUIRE(A.ok);
   const int H = c->hidden_size, D = c->bidirectional ? 2 : 1, G = c->rnn_type == ABCD_LSTM ? 4 : 3;
-  const int F = c->input_size, T = x->T, L = x->L, GH = G * H;
+  const int F = c->input_size, Fp = rup16(F), T = x->T, L = x->L, GH = G * H;
   const int E = abcd_encoder_out_size(c);
   const std::vector<int> off = step_offsets(x->batch_sizes, T);
   const int64_t* bs = x->batch_sizes;
@@ -591,6 +617,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
     }
     // weight gradients: reductions over all L packed frames (K = L, K-major
     // operands), over the row range [r0, r1) into the gradient with weight beta
+    const bool ones_col = l == 0 && F < Fp && !gated && bias_col_enabled();
     auto wgrad = [&](hipStream_t st, int d, int r0, int r1, float beta, float* scratch, size_t scf) -> int {
       const abcd_rnn_g& gr = g->g[l][d];
       const float* X = l == 0 ? w.Xp : ((noise && noise[l - 1]) ? w.Ydrop[l - 1] : w.Y[l - 1]);  // Xp: padded copy
@@ -598,6 +625,20 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       const int K = r1 - r0;
       const float* dGX = w.dGX[l][d] + (size_t)r0 * GH;
       const float* dGH = w.dGH[l][d] + (size_t)r0 * GH;
+      if (ones_col && r0 == 0 && r1 == L && beta == 0.f && gr.w_ih && gr.b_ih) {
+        // [dW_ih | db] in one GEMM into the free input-projection buffer GX
+        ABCD_TRY((hipError_t)gemm(st, GH, In + 1, K, opKM(dGX, GH, GH), opKM(X, ldxx, In + 1), w.GX, In + 1, 1.f,
+                                  0.f, nullptr, ACT_NONE, scratch, scf));
+        const bool same = dGX == dGH;  // LSTM: b_hh receives the same sum
+        split_wb_kernel<<<(int)std::min<long>(1024, cdiv((long)GH * (In + 1), 256)), 256, 0, st>>>(
+            w.GX, GH, In, gr.w_ih, gr.b_ih, same ? gr.b_hh : nullptr);
+        ABCD_CHECK_LAUNCH();
+        if (gr.w_hh)
+          ABCD_TRY((hipError_t)gemm(st, GH, H, K, opKM(dGH, GH, GH), opKM(w.Hprev[l][d], H, H), gr.w_hh, H, 1.f,
+                                    0.f, nullptr, ACT_NONE, scratch, scf));
+        if (!same && gr.b_hh) ABCD_TRY((hipError_t)colsum(st, dGH, GH, K, GH, nullptr, gr.b_hh, 0.f, scratch, scf));
+        return 0;
+      }
       if (gr.w_ih)
         ABCD_TRY((hipError_t)gemm(st, GH, In, K, opKM(dGX, GH, GH), opKM(X + (size_t)r0 * ldxx, ldxx, In), gr.w_ih,
                                   In, 1.f, beta, nullptr, ACT_NONE, scratch, scf));
@@ -635,6 +676,10 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       ABCD_TRY((hipError_t)wgrad(s, 0, 0, f0, 1.f, w.scratch, w.scratch_floats));
       ABCD_TRY((hipError_t)wgrad(s, 1, r1, L, 1.f, w.scratch, w.scratch_floats));
     } else {
+      if (ones_col) {
+        set_col_kernel<<<std::max(1, std::min(1024, cdiv(L, 256))), 256, 0, s>>>(w.Xp, Fp, L, F, 1.f);
+        ABCD_CHECK_LAUNCH();
+      }
       for (int d = 0; d < D; ++d) ABCD_TRY((hipError_t)wgrad(s, d, 0, L, 0.f, w.scratch, w.scratch_floats));
     }
     if (l > 0) {  // dX of this layer = dh of the layer below (both directions)
