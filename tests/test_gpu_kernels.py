@@ -66,3 +66,23 @@ def test_philox_normal_moments():
     y = torch.empty(n, device="cuda")
     Nn.check(Nn.lib().abcd_fill_normal(Nn.ptr(y), n, 1234, 0, Nn.stream()), "normal")
     assert torch.equal(x, y)  # counter-based: reproducible
+
+
+@pytest.mark.parametrize("B,K", [(512, 128), (100, 16), (37, 1024), (5, 200)])
+def test_perplexities_vs_torch_f64(B, K):
+    """abcd_perplexities (learning.py:171-178): exp of the mean per-row entropy
+    of softmax(logits), of the entropy of the batch-mean probabilities, and of
+    the entropy of softmax(posterior_shape_logits); float64 torch reference."""
+    from modules import _native as Nn
+    g = torch.Generator(device="cuda").manual_seed(3)
+    logits = torch.randn(B, K, device="cuda", generator=g) * 3
+    psl = torch.randn(K, device="cuda", generator=g)
+    out = torch.zeros(3, device="cuda")
+    Nn.check(Nn.lib().abcd_perplexities(Nn.ptr(logits), B, K, Nn.ptr(psl), Nn.ptr(out), Nn.stream()), "perplex")
+    torch.cuda.synchronize()
+    q = torch.softmax(logits.double(), -1)
+    ent = -(q * torch.log_softmax(logits.double(), -1)).sum(-1).mean()
+    bm = q.mean(0)
+    pp = torch.softmax(psl.double(), -1)
+    ref = torch.stack([ent.exp(), (-(bm * bm.log()).sum()).exp(), (-(pp * pp.log()).sum()).exp()])
+    assert torch.allclose(out.double().cpu(), ref.cpu(), rtol=1e-5, atol=0), (out, ref)
