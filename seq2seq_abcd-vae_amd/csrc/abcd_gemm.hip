@@ -716,7 +716,15 @@ static bool x6s_enabled() {
 // Tile: 128 rows x 32*NR columns covering N up to 256 per tile.
 static int gemm_tn(hipStream_t s, int M, int N, int K, const Operand& A, const Operand& B, EpiArgs e,
                    float* scratch, size_t scratch_floats) {
-  const int nr = std::min(tl_side ? 4 : 8, cdiv(N, 32));
+  int nr = std::min(tl_side ? 4 : 8, cdiv(N, 32));
+  // one 160-wide tile for N in (128, 160] (the decoder's dW_ih, N = F = 129)
+  // instead of a second, nearly empty 128-wide one: 38 KB LDS, 142 VGPRs --
+  // still one workgroup per CU beside enc_bwd_sk (98 KB, 258 registers)
+  const char* s5 = getenv("ABCD_SIDE5");
+  if (tl_side && N > 128 && N <= 160 && !(s5 && s5[0] == '0')) nr = 5;
+  // the same along M (the emission MLPs' dW2, M = F = 129): one 160-row tile
+  if (tl_side && nr == 4 && M > 128 && M <= 160 && !(s5 && s5[0] == '0'))
+    return gemm_tn_launch<5, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
 #define TN_CASE(n) \
   case n: return gemm_tn_launch<4, n>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
   switch (nr) {
