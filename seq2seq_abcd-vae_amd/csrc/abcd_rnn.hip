@@ -969,6 +969,7 @@ struct DecWS {
   float *WihTp, *WhhT, *W2mT, *W2lT, *W1catT, *W1oT, *Wf2hT;
   // forward stash
   float *FS, *Hinit, *Xin, *Hprev, *Cprev, *Gst, *Cst, *Hs, *Aact, *MU, *LV, *OUT, *Zo, *offlog, *dlog_raw, *bce;
+  float* dWb;  // [dW_ih | db] of the cell (bias column folded into the GEMM)
   double* part;
   // backward
   float *dGX, *dGH, *DC, *DC0, *dH0, *dhid, *dFS, *DHO, *dMU, *dLV, *dZ, *dZo, *dlog_s;
@@ -1015,6 +1016,7 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
   w.dhid = A.f((size_t)B * Htot); w.dFS = A.f((size_t)B * DS); w.DHO = A.f((size_t)L * H);
   w.dMU = A.f((size_t)L * Fp); w.dLV = A.f((size_t)L * Fp); w.dZ = A.f((size_t)L * 2 * Hm);
   w.dZo = A.f((size_t)L * Hm); w.dlog_s = A.f(L);
+  w.dWb = A.f((size_t)GH * (F + 1));
   size_t maxMN = std::max<size_t>({(size_t)GH * std::max(Fp, H), (size_t)Fp * Hm, (size_t)Hm * H,
                                    (size_t)Htot * DS, (size_t)L});
   w.off = (int*)A.f((size_t)T + 1);
@@ -1328,7 +1330,20 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
                               nullptr, ACT_NONE, sc, scf));
   if (g->f2h_b) ABCD_TRY((hipError_t)colsum(s, w.dhid, Htot, B, Htot, nullptr, g->f2h_b, 0.f, sc, scf));
   const abcd_rnn_g& cg = g->cell;
-  if (cg.w_ih) {
+  // bias gradients as the last column of dG^T [Xin | 1] (Xin's pad column F
+  // set to 1 after the BPTT; the packed W_ih pads are 0, so a later forward
+  // that keeps it is unaffected) -- the colsum pass over L x G*H is gone
+  const bool same_b = w.dGX == w.dGH;
+  const bool ones = c->feedback && F < Fp && cg.w_ih && cg.b_ih && bias_col_enabled();
+  if (ones) {
+    set_col_kernel<<<std::max(1, std::min(1024, cdiv(L, 256))), 256, 0, s>>>(w.Xin, Fp, L, F, 1.f);
+    ABCD_CHECK_LAUNCH();
+    ABCD_TRY((hipError_t)gemm(s, GH, F + 1, L, opKM(w.dGX, GH, GH), opKM(w.Xin, Fp, F + 1), w.dWb, F + 1, 1.f, 0.f,
+                              nullptr, ACT_NONE, sc, scf));
+    split_wb_kernel<<<(int)std::min<long>(1024, cdiv((long)GH * (F + 1), 256)), 256, 0, s>>>(
+        w.dWb, GH, F, cg.w_ih, cg.b_ih, same_b ? cg.b_hh : nullptr);
+    ABCD_CHECK_LAUNCH();
+  } else if (cg.w_ih) {
     if (c->feedback)
       ABCD_TRY((hipError_t)gemm(s, GH, F, L, opKM(w.dGX, GH, GH), opKM(w.Xin, Fp, F), cg.w_ih, F, 1.f, 0.f, nullptr,
                                 ACT_NONE, sc, scf));
@@ -1338,7 +1353,9 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
   if (cg.w_hh)
     ABCD_TRY((hipError_t)gemm(s, GH, H, L, opKM(w.dGH, GH, GH), opKM(w.Hprev, H, H), cg.w_hh, H, 1.f, 0.f, nullptr,
                               ACT_NONE, sc, scf));
-  if (w.dGX == w.dGH && cg.b_ih) {  // LSTM: one pass for both bias gradients
+  if (ones) {
+    if (!same_b && cg.b_hh) ABCD_TRY((hipError_t)colsum(s, w.dGH, GH, L, GH, nullptr, cg.b_hh, 0.f, sc, scf));
+  } else if (same_b && cg.b_ih) {  // LSTM: one pass for both bias gradients
     ABCD_TRY((hipError_t)colsum(s, w.dGX, GH, L, GH, nullptr, cg.b_ih, 0.f, sc, scf, cg.b_hh));
   } else {
     if (cg.b_ih) ABCD_TRY((hipError_t)colsum(s, w.dGX, GH, L, GH, nullptr, cg.b_ih, 0.f, sc, scf));
