@@ -125,8 +125,10 @@ def build(cfg, device):
     return engine.FusedStep(enc, samp, dec, device)
 
 
-def cpu_baseline(cfg, budget_s=25.0):
-    """Time the CPU oracle on a bounded sample of the same workload."""
+def cpu_baseline(cfg, target_s=10.0, budget_s=25.0):
+    """Time the CPU oracle on a bounded sample of the same workload: one
+    untimed warm-up step, then b = 64 steps until ~target_s of CPU work
+    (at least 3, stopping past budget_s)."""
     from oracle import abcd_oracle as O
     threads = max(1, min(16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
@@ -140,8 +142,9 @@ def cpu_baseline(cfg, budget_s=25.0):
     feat = torch.randn(b, cfg["D"]) if cfg["plain"] else -torch.empty(b, cfg["K"]).exponential_().log()
     eps = torch.randn(batch["L"], cfg["F"])
     noise = dict(feat=feat, eps=eps)
+    O.train_step(P, dict(data=batch["data"], batch_sizes=bsz, is_offset=batch["is_offset"]), ocfg, noise, cfg["N"])
     steps, t_total = 0, 0.0
-    while steps < 3:
+    while steps < 3 or t_total < target_s:
         t0 = time.perf_counter()
         O.train_step(P, dict(data=batch["data"], batch_sizes=bsz, is_offset=batch["is_offset"]), ocfg, noise,
                      cfg["N"])
