@@ -331,6 +331,7 @@ struct EncWS {
   float* DC[ABCD_MAX_LAYERS][2];
   float* DHX[ABCD_MAX_LAYERS];
   float* Ydrop[ABCD_MAX_LAYERS];  // layer output x dropout noise (input of layer l + 1)
+  float* dWb;                     // layer 0: [dW_ih | db] (bias column folded into the GEMM)
   int* off;          // device copy of the step offsets (persistent kernels)
   unsigned* sync;    // persistent-kernel group counters
   float* skp;        // dec_bwd_sk split-K partials
@@ -373,6 +374,7 @@ static EncWS carve_encoder(Arena& A, const abcd_encoder_cfg* c, int T, int L, in
     maxMN = std::max(maxMN, (size_t)G * H * std::max(In, H));
   }
   w.GX = A.f((size_t)L * D * G * H);
+  w.dWb = A.f((size_t)G * H * (F + 1));
   w.off = (int*)A.f((size_t)T + 1);
   w.sync = (unsigned*)A.f(persist_sync_uints(D, B));
   w.part = A.f(persist_part_floats(D, B, H));
@@ -626,12 +628,12 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       const float* dGX = w.dGX[l][d] + (size_t)r0 * GH;
       const float* dGH = w.dGH[l][d] + (size_t)r0 * GH;
       if (ones_col && r0 == 0 && r1 == L && beta == 0.f && gr.w_ih && gr.b_ih) {
-        // [dW_ih | db] in one GEMM into the free input-projection buffer GX
-        ABCD_TRY((hipError_t)gemm(st, GH, In + 1, K, opKM(dGX, GH, GH), opKM(X, ldxx, In + 1), w.GX, In + 1, 1.f,
+        // [dW_ih | db] in one GEMM
+        ABCD_TRY((hipError_t)gemm(st, GH, In + 1, K, opKM(dGX, GH, GH), opKM(X, ldxx, In + 1), w.dWb, In + 1, 1.f,
                                   0.f, nullptr, ACT_NONE, scratch, scf));
         const bool same = dGX == dGH;  // LSTM: b_hh receives the same sum
         split_wb_kernel<<<(int)std::min<long>(1024, cdiv((long)GH * (In + 1), 256)), 256, 0, st>>>(
-            w.GX, GH, In, gr.w_ih, gr.b_ih, same ? gr.b_hh : nullptr);
+            w.dWb, GH, In, gr.w_ih, gr.b_ih, same ? gr.b_hh : nullptr);
         ABCD_CHECK_LAUNCH();
         if (gr.w_hh)
           ABCD_TRY((hipError_t)gemm(st, GH, H, K, opKM(dGH, GH, GH), opKM(w.Hprev[l][d], H, H), gr.w_hh, H, 1.f,
