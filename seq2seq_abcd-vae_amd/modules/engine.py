@@ -156,8 +156,16 @@ class FusedStep:
             nt, seed, off = _noise.gumbel(B, W, dev)
         N.check(L_.abcd_sampler_sample(self.samp_cfg, self.samp_p, N.ptr(logits), B, mode, tau, N.ptr(nt), seed, off,
                                        N.ptr(feats), N.ptr(ws_s), ws_s.numel(), st), "sampler sample")
+        # the Dirichlet KL (three small kernels) only feeds the loss scalar and
+        # the backward: on the idle side stream beside the decoder's setup
+        # (ABCD flavour only: plain KL and sample share the MV stash copy)
+        kl_side = None
+        if not self.plain and os.environ.get("ABCD_KLSIDE", "1") != "0":
+            kl_side = self._side_stream()
+            kl_side.wait_stream(torch.cuda.current_stream(dev))
         N.check(L_.abcd_sampler_kl(self.samp_cfg, self.samp_p, N.ptr(logits), B, float(entire_data_size),
-                                   N.ptr(sc[KL:KL + 1]), N.ptr(ws_s), ws_s.numel(), st), "sampler kl")
+                                   N.ptr(sc[KL:KL + 1]), N.ptr(ws_s), ws_s.numel(),
+                                   st if kl_side is None else N.c_void_p(kl_side.cuda_stream)), "sampler kl")
         F = self.decoder.rnn_cell.cell.input_size
         pdrop = self.decoder._input_dropout_p() if train else 0.0
         eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
@@ -169,6 +177,8 @@ class FusedStep:
                                                 N.ptr(eps), N.ptr(xmask), eseed, eoff, None, None, None, None,
                                                 N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st),
                 "decoder forward")
+        if kl_side is not None:
+            torch.cuda.current_stream(dev).wait_stream(kl_side)
         N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), B, N.ptr(sc[LOSS:LOSS + 1]), st),
                 "total loss")
         if not train:
