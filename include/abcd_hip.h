@@ -234,6 +234,14 @@ int abcd_decoder_forward_dropout(const abcd_decoder_cfg* cfg, const abcd_decoder
                                  const float* eps, const float* xmask, uint64_t seed, uint64_t offset,
                                  float* flatten_out, float* mu, float* log_var, float* offset_logits, float* losses,
                                  void* ws, size_t ws_bytes, void* stream);
+/* the same, with the loss reductions (emission NLL, offset BCE sum -> losses)
+ * queued on loss_stream (NULL or == stream: one stream) after events on
+ * `stream`; the caller joins loss_stream before reading `losses`. */
+int abcd_decoder_forward_split(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
+                               const float* features, const int64_t* speakers, const float* gt_offset,
+                               const float* eps, const float* xmask, uint64_t seed, uint64_t offset,
+                               float* flatten_out, float* mu, float* log_var, float* offset_logits, float* losses,
+                               void* ws, size_t ws_bytes, void* stream, void* loss_stream);
 int abcd_decoder_backward_dropout(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
                                   const float* features, const int64_t* speakers, const float* gt_offset,
                                   const float* xmask, const float* d_em, const float* d_off, float* d_features,

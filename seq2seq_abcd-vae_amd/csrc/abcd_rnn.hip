@@ -1049,12 +1049,38 @@ extern "C" int abcd_decoder_forward(const abcd_decoder_cfg* c, const abcd_decode
                                       flatten_out, mu_out, lv_out, offset_logits, losses, ws, ws_bytes, stream);
 }
 
+static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params* p, const abcd_packed* x,
+                            const float* features, const int64_t* speakers, const float* gt_offset, const float* eps,
+                            const float* xmask, uint64_t seed, uint64_t offset, float* flatten_out, float* mu_out,
+                            float* lv_out, float* offset_logits, float* losses, void* ws, size_t ws_bytes,
+                            void* stream, hipStream_t sl);
+
 extern "C" int abcd_decoder_forward_dropout(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
                                             const abcd_packed* x, const float* features, const int64_t* speakers,
                                             const float* gt_offset, const float* eps, const float* xmask,
                                             uint64_t seed, uint64_t offset, float* flatten_out, float* mu_out,
                                             float* lv_out, float* offset_logits, float* losses, void* ws,
                                             size_t ws_bytes, void* stream) {
+  return dec_forward_impl(c, p, x, features, speakers, gt_offset, eps, xmask, seed, offset, flatten_out, mu_out,
+                          lv_out, offset_logits, losses, ws, ws_bytes, stream, (hipStream_t)stream);
+}
+
+extern "C" int abcd_decoder_forward_split(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
+                                          const abcd_packed* x, const float* features, const int64_t* speakers,
+                                          const float* gt_offset, const float* eps, const float* xmask,
+                                          uint64_t seed, uint64_t offset, float* flatten_out, float* mu_out,
+                                          float* lv_out, float* offset_logits, float* losses, void* ws,
+                                          size_t ws_bytes, void* stream, void* loss_stream) {
+  return dec_forward_impl(c, p, x, features, speakers, gt_offset, eps, xmask, seed, offset, flatten_out, mu_out,
+                          lv_out, offset_logits, losses, ws, ws_bytes, stream,
+                          loss_stream ? (hipStream_t)loss_stream : (hipStream_t)stream);
+}
+
+static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params* p, const abcd_packed* x,
+                            const float* features, const int64_t* speakers, const float* gt_offset, const float* eps,
+                            const float* xmask, uint64_t seed, uint64_t offset, float* flatten_out, float* mu_out,
+                            float* lv_out, float* offset_logits, float* losses, void* ws, size_t ws_bytes,
+                            void* stream, hipStream_t sl) {
   ABCD_REQUIRE(dec_check(c) == 0 && p && x && features && ws);
   ABCD_REQUIRE(!xmask || c->feedback);
   ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
@@ -1153,21 +1179,25 @@ extern "C" int abcd_decoder_forward_dropout(const abcd_decoder_cfg* c, const abc
     dec_emit_fwd<<<cdiv(b_t, 16) * (Fp / 16), 256, 0, s>>>(e);
     ABCD_CHECK_LAUNCH();
   }
+  // ---- loss reductions: only the loss scalars read them, so with a loss
+  // stream sl they run there beside the offset head (w.part is theirs alone)
+  if (losses && x->data) {
+    ABCD_TRY((hipError_t)stream_fork(s, sl, 4));  // MU, LV
+    const int nbk = 1024;
+    dec_emission_nll<<<nbk, 256, 0, sl>>>(w.MU, w.LV, Fp, x->data, F, L, w.part);
+    ABCD_CHECK_LAUNCH();
+    sum_partials<<<1, 256, 0, sl>>>(w.part, nbk, losses);
+    ABCD_CHECK_LAUNCH();
+  }
   // ---- offset head over all frames (off the recurrent critical path) ----
   ABCD_TRY((hipError_t)gemm(s, L, Hm, H, opKC(w.Hs, H, L), opKC(p->offset.w1, H, Hm), w.Zo, Hm, 1.f, 0.f,
                             p->offset.b1, ACT_TANH, w.scratch, w.scratch_floats));
   dec_offset_head<<<cdiv(L, 4), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, p->offset.b2, gt_offset, w.offlog,
                                              w.dlog_raw, w.bce);
   ABCD_CHECK_LAUNCH();
-  if (losses) {
-    if (x->data) {
-      const int nbk = 1024;
-      dec_emission_nll<<<nbk, 256, 0, s>>>(w.MU, w.LV, Fp, x->data, F, L, w.part);
-      ABCD_CHECK_LAUNCH();
-      sum_partials<<<1, 256, 0, s>>>(w.part, nbk, losses);
-      ABCD_CHECK_LAUNCH();
-    }
-    if (gt_offset) ABCD_TRY((hipError_t)reduce_sum(s, w.bce, L, w.part + 1024, losses + 1, nullptr));
+  if (losses && gt_offset) {
+    ABCD_TRY((hipError_t)stream_fork(s, sl, 5));  // bce
+    ABCD_TRY((hipError_t)reduce_sum(sl, w.bce, L, w.part + 1024, losses + 1, nullptr));
   }
   if (flatten_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.OUT, Fp, flatten_out, F, L); ABCD_CHECK_LAUNCH(); }
   if (mu_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.MU, Fp, mu_out, F, L); ABCD_CHECK_LAUNCH(); }

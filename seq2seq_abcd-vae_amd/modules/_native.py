@@ -121,6 +121,9 @@ _SIGS = {
     "abcd_decoder_forward_dropout": (c_int, [_P(DecoderCfg), _P(DecoderParams), _P(Packed), c_void_p, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "abcd_decoder_forward_split": (c_int, [_P(DecoderCfg), _P(DecoderParams), _P(Packed), c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
     "abcd_decoder_backward_dropout": (c_int, [_P(DecoderCfg), _P(DecoderParams), _P(Packed), c_void_p, c_void_p,
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, _P(DecoderGrads),
                                               c_void_p, c_size_t, c_void_p, c_void_p]),

@@ -173,15 +173,32 @@ class FusedStep:
         if self.decoder.embed_speaker is not None:
             spk = speakers.to(dev, torch.int64).contiguous()
         gt_off = is_offset.contiguous()
-        N.check(L_.abcd_decoder_forward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
-                                                N.ptr(eps), N.ptr(xmask), eseed, eoff, None, None, None, None,
-                                                N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st),
+        # the loss reductions (emission NLL, BCE sum, total loss) only feed the
+        # scalars: ABCD_LOSSSIDE=1 queues them on the side stream beside the
+        # offset head (joined with the rest of the side work).  Measured at c2
+        # (10 alternating runs): 13.692 vs 13.704 ms -- within noise (the NLL
+        # pass shares the chip with the offset-head GEMM), so off by default.
+        loss_side = self._side_stream() if os.environ.get("ABCD_LOSSSIDE", "0") == "1" else None
+        kl_done = None
+        if kl_side is not None and loss_side is not None:
+            kl_done = torch.cuda.Event()
+            kl_done.record(kl_side)
+        N.check(L_.abcd_decoder_forward_split(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
+                                              N.ptr(eps), N.ptr(xmask), eseed, eoff, None, None, None, None,
+                                              N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st,
+                                              N.c_void_p(None if loss_side is None else loss_side.cuda_stream)),
                 "decoder forward")
-        if kl_side is not None:
-            torch.cuda.current_stream(dev).wait_stream(kl_side)
-        N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), B, N.ptr(sc[LOSS:LOSS + 1]), st),
-                "total loss")
+        if loss_side is None:
+            if kl_side is not None:
+                torch.cuda.current_stream(dev).wait_stream(kl_side)
+            N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), B, N.ptr(sc[LOSS:LOSS + 1]),
+                                       st), "total loss")
+        else:  # the side stream already holds the KL (or waited for it on the main stream)
+            N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), B, N.ptr(sc[LOSS:LOSS + 1]),
+                                       N.c_void_p(loss_side.cuda_stream)), "total loss")
         if not train:
+            if loss_side is not None:
+                torch.cuda.current_stream(dev).wait_stream(loss_side)
             return sc, logits
         inv = self._inv_b(B)
         d_feats = torch.empty(B, self.Dfeat, device=dev)
@@ -198,6 +215,8 @@ class FusedStep:
                                                             else side.cuda_stream)),
                 "decoder backward")
         d_h = torch.empty(B, self.E, device=dev)
+        if kl_done is not None:  # the KL stash (Q, v) feeds the sampler backward
+            torch.cuda.current_stream(dev).wait_event(kl_done)
         N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
                                                float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
                                                self.samp_g, N.ptr(ws_s), ws_s.numel(), st,

@@ -150,7 +150,8 @@ def test_fused_step_persist_vs_stepwise_bench_size(cfg_name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("knob,value", [("ABCD_FUSEX", "1"), ("ABCD_X6GEMM", "1"), ("ABCD_ENCGATE", "1"),
                                          ("ABCD_DECHPRE", "0"), ("ABCD_X6S", "0"), ("ABCD_BIASCOL", "0"),
-                                         ("ABCD_SIDE5", "0"), ("ABCD_KLSIDE", "0")])
+                                         ("ABCD_SIDE5", "0"), ("ABCD_KLSIDE", "0"),
+                                         ("ABCD_LOSSSIDE", "1")])
 def test_opt_in_paths_match_default(knob, value):
     """The opt-in variants -- input projection fused into the persistent
     encoder kernel (ABCD_FUSEX=1), split-fp32 weight-gradient GEMMs
@@ -159,8 +160,9 @@ def test_opt_in_paths_match_default(knob, value):
     GEMMs (ABCD_X6S=0), the encoder bias gradients as colsum passes instead of
     the ones column of the input weight-gradient GEMM (ABCD_BIASCOL=0), the
     side-stream GEMMs without the 160-wide tiles (ABCD_SIDE5=0), the KL on the
-    main stream (ABCD_KLSIDE=0) -- give the default path's losses and
-    gradients at c2."""
+    main stream (ABCD_KLSIDE=0), the loss reductions on the side stream
+    (ABCD_LOSSSIDE=1) -- give
+    the default path's losses and gradients at c2."""
     import bench
     cfg = bench.CONFIGS["c2"]
     step = bench.build(cfg, "cuda")
