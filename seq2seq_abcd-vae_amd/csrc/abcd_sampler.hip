@@ -357,8 +357,10 @@ extern "C" int abcd_sampler_forward(const abcd_sampler_cfg* c, const abcd_sample
     return 0;
   }
   const abcd_mlp_w& m = p->mlp[0];
+  // K = E = 1024 over 64 output tiles: split-K (8 slabs + reduce, tanh in the
+  // reduce epilogue) fills the chip instead of 64 long workgroups
   ABCD_TRY((hipError_t)gemm(s, B, Hm, E, opKC(h, E, B), opKC(m.w1, E, Hm), w.Z1[0], Hm, 1.f, 0.f, m.b1, ACT_TANH,
-                            nullptr, 0));
+                            w.scratch, w.scratch_floats));
   ABCD_TRY((hipError_t)gemm(s, B, D, Hm, opKC(w.Z1[0], Hm, B), opKC(m.w2, Hm, D), w.U, D, 1.f, 0.f, m.b2, ACT_NONE,
                             nullptr, 0));
   // logits = U @ codebook / sqrt(D)   (codebook D x K used as a K-major operand)
