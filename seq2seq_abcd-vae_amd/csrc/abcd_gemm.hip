@@ -847,7 +847,11 @@ int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const 
            float beta, float* scratch, size_t scratch_floats, float* out2) {
   if (ncols <= 0) return 0;
   const int cblocks = cdiv(ncols, 64);
-  int slices = std::max(1, std::min(cdiv(std::max(nrows, 1), 256), std::max(1, 1024 / cblocks)));
+  // slices of >= 16 rows (one 4-load round per thread) until ~1024 workgroups:
+  // the short batch reductions (nrows = B = 512) take 32 slices instead of 2
+  // slices of 256 rows (16 dependent load rounds, ~18 us); the frame
+  // reductions (nrows = L) keep the 1024-workgroup cap
+  int slices = std::max(1, std::min(cdiv(std::max(nrows, 1), 16), std::max(1, 1024 / cblocks)));
   slices = std::min(slices, 256);
   slices = (int)std::max<long>(1, std::min<long>(slices, (long)(scratch_floats / (size_t)ncols)));
   const int rows_per = cdiv(std::max(nrows, 1), slices);
