@@ -866,6 +866,7 @@ __global__ void dec_offset_head(const float* Zo, int L, int Hm, const float* w2,
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= L) return;
   float s = 0.f;
+#pragma unroll 4
   for (int j = lane; j < Hm; j += 64) s += Zo[(long)row * Hm + j] * w2[j];
   for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
   if (lane == 0) {
@@ -883,13 +884,15 @@ __global__ void dec_emission_nll(const float* MU, const float* LV, int Fp, const
                                  double* part) {
   __shared__ double sh[16];
   double acc = 0.0;
-  const long n = L * F;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / F;
-    const int j = (int)(i % F);
-    const float mu = MU[r * Fp + j], lv = LV[r * Fp + j], d = Y[i] - mu;
-    acc += 0.5f * (1.8378770664093453f + lv + d * d * __expf(-lv));
-  }
+  // one wave per row (grid-stride over rows): coalesced row reads, no
+  // per-element 64-bit index division
+  const int nwv = gridDim.x * (blockDim.x >> 6);
+  for (long r = blockIdx.x * (long)(blockDim.x >> 6) + (threadIdx.x >> 6); r < L; r += nwv)
+#pragma unroll 3
+    for (int j = threadIdx.x & 63; j < F; j += 64) {
+      const float mu = MU[r * Fp + j], lv = LV[r * Fp + j], d = Y[r * F + j] - mu;
+      acc += 0.5f * (1.8378770664093453f + lv + d * d * __expf(-lv));
+    }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) sh[w] = acc;
@@ -917,15 +920,17 @@ __global__ void sum_partials(const double* part, int np, float* out) {
 // offset-head backward: dlog = s_off * (sigmoid(x) - y); dZo = dlog * w2 * (1 - Zo^2)
 __global__ void dec_offset_bwd(const float* Zo, int L, int Hm, const float* w2, const float* dlog_raw,
                                const float* s_off, float* dZo, float* dlog_s) {
-  const long n = (long)L * Hm;
   const float s = *s_off;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / Hm;
-    const int j = (int)(i % Hm);
-    const float z = Zo[i];
+  // one wave per row (grid-stride over rows), as dec_offset_head
+  const int lane = threadIdx.x & 63, nwv = gridDim.x * (blockDim.x >> 6);
+  for (long r = blockIdx.x * (long)(blockDim.x >> 6) + (threadIdx.x >> 6); r < L; r += nwv) {
     const float dl = s * dlog_raw[r];
-    dZo[i] = dl * w2[j] * (1.f - z * z);
-    if (j == 0) dlog_s[r] = dl;
+#pragma unroll 4
+    for (int j = lane; j < Hm; j += 64) {
+      const float z = Zo[r * Hm + j];
+      dZo[r * Hm + j] = dl * w2[j] * (1.f - z * z);
+    }
+    if (lane == 0) dlog_s[r] = dl;
   }
 }
 // gradient of feature2hidden output from the t=0 carries
@@ -1184,7 +1189,7 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
   if (losses && x->data) {
     ABCD_TRY((hipError_t)stream_fork(s, sl, 4));  // MU, LV
     const int nbk = 1024;
-    dec_emission_nll<<<nbk, 256, 0, sl>>>(w.MU, w.LV, Fp, x->data, F, L, w.part);
+    dec_emission_nll<<<nbk, 1024, 0, sl>>>(w.MU, w.LV, Fp, x->data, F, L, w.part);  // 16 waves / block
     ABCD_CHECK_LAUNCH();
     sum_partials<<<1, 256, 0, sl>>>(w.part, nbk, losses);
     ABCD_CHECK_LAUNCH();
