@@ -311,11 +311,23 @@ int abcd_timing_read(double* out);
 /* the same for one kernel: 0 per-step recurrent kernels, 1 encoder forward,
  * 2 encoder backward, 3 decoder forward, 4 decoder backward (persistent) */
 int abcd_timing_read_kernel(int kid, double* out);
+/* which kernel the last launch of a role ran (same ids as abcd_timing_read_kernel,
+ * e.g. "dec_bwd_sk<9,16,16,LSTM> grid 256" or "per-step ..."), and how many
+ * launches of the role since abcd_dispatch_reset; host-side bookkeeping only */
+const char* abcd_dispatch_name(int kid);
+long abcd_dispatch_count(int kid);
+void abcd_dispatch_reset(void);
 /* 0 if no persistent recurrent kernel has timed out waiting for its group
  * since the last call (a timeout means the grid was not co-resident; the
  * results of that launch are invalid).  Reads and clears the device word;
  * synchronises the device.  Returns -1 on a HIP error. */
 int abcd_device_status(void);
+/* stream-ordered form for the training step (no host sync): out[0] = the
+ * timeout status raised since the previous call (0 ok, 1 a persistent kernel's
+ * hand-off wait timed out, 2 a side-stream gate timed out; non-zero means
+ * that step's results are invalid), then clears it.  The trainer and bench.py
+ * raise on a non-zero value. */
+int abcd_step_status(float* out, void* stream);
 /* library build identification (gfx target, version) */
 const char* abcd_version(void);
 

@@ -312,7 +312,7 @@ def decoder_forward(P, feats, batch_sizes, cfg, eps, speakers=None, gt=None, gt_
 # ----------------------------------------------------------------------------
 # one training step (learning.py:147-163)
 # ----------------------------------------------------------------------------
-def forward_losses(P, batch, cfg, noise, N, pretrain=False, tau=1.0, train=True):
+def forward_losses(P, batch, cfg, noise, N, pretrain=False, tau=1.0, train=True, loss_batch=None):
     data, batch_sizes = batch["data"], batch["batch_sizes"]
     last_hidden = encoder_forward(P, data, batch_sizes, cfg)
     if cfg["plain"]:
@@ -327,17 +327,20 @@ def forward_losses(P, batch, cfg, noise, N, pretrain=False, tau=1.0, train=True)
     em, off, out, (mu, lv), off_logits = decoder_forward(
         P, feats, batch_sizes, cfg, noise["eps"], speakers=batch.get("speakers"),
         gt=data, gt_off=batch["is_offset"], train=train, xmask=noise.get("xmask"))
-    B = int(batch_sizes[0])
+    # learning.py:156 divides by batch_sizes[0]; a data-parallel shard divides
+    # by the global batch size instead (loss_batch), so the ranks' losses sum
+    # to the global-batch loss
+    B = int(batch_sizes[0]) if loss_batch is None else int(loss_batch)
     loss = (em + off + kl) / B
     return dict(loss=loss, em=em, off=off, kl=kl, last_hidden=last_hidden, logits=logits, feats=feats,
                 flatten_out=out, mu=mu, lv=lv, offset_logits=off_logits)
 
 
 def train_step(P, batch, cfg, noise, N, pretrain=False, tau=1.0, lr=1.0, clip=1.0,
-               momentum=0.0, momentum_buf=None):
+               momentum=0.0, momentum_buf=None, loss_batch=None):
     """Returns (outputs, grads, new_params, total_norm, momentum_buf)."""
     P = OrderedDict((k, v.detach().clone().requires_grad_(not is_buffer(k))) for k, v in P.items())
-    out = forward_losses(P, batch, cfg, noise, N, pretrain, tau)
+    out = forward_losses(P, batch, cfg, noise, N, pretrain, tau, loss_batch=loss_batch)
     out["loss"].backward()
     names = [k for k in P if not is_buffer(k)]
     grads = OrderedDict((k, P[k].grad.detach().clone() if P[k].grad is not None else torch.zeros_like(P[k]))

@@ -125,6 +125,10 @@ namespace abcd {
 enum TimedKernel { TK_STEP = 0, TK_ENC_FWD = 1, TK_ENC_BWD = 2, TK_DEC_FWD = 3, TK_DEC_BWD = 4, TK_N = 5 };
 bool timing_on();
 void timing_mark(hipStream_t s, int kid);
+// records which kernel (template instance) a role's last launch ran, so the
+// tests can assert that the production-shape dispatch is the one checked
+// against the reference (abcd_dispatch_name / abcd_dispatch_count)
+void note_dispatch(int kid, const char* fmt, ...);
 struct TimedScope {
   hipStream_t s;
   bool on;

@@ -136,6 +136,8 @@ extern "C" const char* abcd_version(void) { return "abcd_hip 0.1 gfx950 fp32-mfm
 // ---------------------------------------------------------------------------
 // live kernel timing (bench.py): event pairs around recurrent-kernel launches
 // ---------------------------------------------------------------------------
+#include <cstdarg>
+#include <cstdio>
 #include <vector>
 namespace abcd {
 struct TimingState {
@@ -173,6 +175,30 @@ static int timing_sum(int want, double* out) {
   return 0;
 }
 }  // namespace abcd
+
+namespace abcd {
+static char g_dispatch[TK_N][128];
+static long g_dispatch_n[TK_N];
+void note_dispatch(int kid, const char* fmt, ...) {
+  if (kid < 0 || kid >= TK_N) return;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_dispatch[kid], sizeof(g_dispatch[kid]), fmt, ap);
+  va_end(ap);
+  ++g_dispatch_n[kid];
+}
+}  // namespace abcd
+
+extern "C" const char* abcd_dispatch_name(int kid) {
+  return (kid < 0 || kid >= abcd::TK_N) ? "" : abcd::g_dispatch[kid];
+}
+extern "C" long abcd_dispatch_count(int kid) { return (kid < 0 || kid >= abcd::TK_N) ? -1 : abcd::g_dispatch_n[kid]; }
+extern "C" void abcd_dispatch_reset(void) {
+  for (int k = 0; k < abcd::TK_N; ++k) {
+    abcd::g_dispatch[k][0] = 0;
+    abcd::g_dispatch_n[k] = 0;
+  }
+}
 
 extern "C" void abcd_timing_enable(int on) { abcd::g_timing.on = on != 0; }
 extern "C" void abcd_timing_reset(void) { abcd::g_timing.used = 0; }

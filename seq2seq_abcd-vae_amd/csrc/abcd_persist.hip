@@ -38,6 +38,8 @@
 namespace abcd {
 
 __device__ unsigned g_persist_status = 0;
+__device__ unsigned g_persist_sticky = 0;       // OR of every status abcd_step_status folded (abcd_device_status)
+__device__ unsigned g_spin_limit = 1u << 22;    // polls before a hand-off wait gives up (ABCD_SPIN_LIMIT, tests)
 __device__ unsigned g_local_wgs = 0;  // diagnostics: workgroups that ran in XCD-local mode
 
 // ---------------------------------------------------------------------------
@@ -107,9 +109,10 @@ DEV void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, 
 DEV void group_wait(unsigned* cnt, unsigned target) {
   if (threadIdx.x == 0) {
     unsigned spins = 0;
+    const unsigned lim = g_spin_limit;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) {
+      if (++spins > lim) {
         __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -142,13 +145,14 @@ DEV void flags_wait(const unsigned* fl, int M, unsigned epoch) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     unsigned spins = 0;
+    const unsigned lim = g_spin_limit;
     for (;;) {
       bool ok = true;
       if (lane < M)
         ok = __hip_atomic_load(fl + lane * PERSIST_SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
       if (__all(ok)) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) {
+      if (++spins > lim) {
         if (lane == 0) __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -228,9 +232,10 @@ DEV Role assign_role(unsigned* reg, int ngroups, int nmem, int* sh) {
     __hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     bool ok = true;
+    const unsigned lim = g_spin_limit;
     while (__hip_atomic_load(arrived, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) {
+      if (++spins > lim) {
         __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = false;
         break;
@@ -1754,44 +1759,55 @@ bool persist_enabled() {
 namespace {
 constexpr int OFF_NSLOT = 32;
 constexpr size_t OFF_SLOT = 64 * 1024;
+constexpr int OFF_MAXDEV = 16;
 std::mutex g_off_mu;
-char* g_off_ring = nullptr;
-hipEvent_t g_off_ev[OFF_NSLOT];
-bool g_off_used[OFF_NSLOT];
-int g_off_next = 0;
+// one ring per device: a slot's event is recorded on streams of that device only
+struct OffRing {
+  char* ring = nullptr;
+  hipEvent_t ev[OFF_NSLOT];
+  bool used[OFF_NSLOT];
+  int next = 0;
+};
+OffRing g_rings[OFF_MAXDEV];
 struct PendingOff {
   hipStream_t s;
   int* dst;
   const int* src;  // pinned host slot
-  int n, slot;
+  int n, slot, dev;
   bool on;
 };
 thread_local PendingOff g_pend{};
 
-int off_slot(const std::vector<int>& off, int* slot_out, const int** src) {
+int off_slot(const std::vector<int>& off, int* slot_out, const int** src, int* dev_out) {
   const size_t bytes = off.size() * sizeof(int);
   if (bytes > OFF_SLOT) return (int)hipErrorInvalidValue;
+  int dev = 0;
+  ABCD_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= OFF_MAXDEV) return (int)hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lk(g_off_mu);
-  if (!g_off_ring) {
-    ABCD_TRY(hipHostMalloc((void**)&g_off_ring, OFF_SLOT * OFF_NSLOT, hipHostMallocDefault));
+  OffRing& R = g_rings[dev];
+  if (!R.ring) {
+    ABCD_TRY(hipHostMalloc((void**)&R.ring, OFF_SLOT * OFF_NSLOT, hipHostMallocDefault));
     for (int k = 0; k < OFF_NSLOT; ++k) {
-      ABCD_TRY(hipEventCreateWithFlags(&g_off_ev[k], hipEventDisableTiming));
-      g_off_used[k] = false;
+      ABCD_TRY(hipEventCreateWithFlags(&R.ev[k], hipEventDisableTiming));
+      R.used[k] = false;
     }
   }
-  const int k = g_off_next;
-  g_off_next = (g_off_next + 1) % OFF_NSLOT;
-  if (g_off_used[k]) ABCD_TRY(hipEventSynchronize(g_off_ev[k]));  // the op that last read this slot is done
-  g_off_used[k] = false;
-  std::copy(off.begin(), off.end(), (int*)(g_off_ring + k * OFF_SLOT));
+  const int k = R.next;
+  R.next = (R.next + 1) % OFF_NSLOT;
+  if (R.used[k]) ABCD_TRY(hipEventSynchronize(R.ev[k]));  // the op that last read this slot is done
+  R.used[k] = false;
+  std::copy(off.begin(), off.end(), (int*)(R.ring + k * OFF_SLOT));
   *slot_out = k;
-  *src = (const int*)(g_off_ring + k * OFF_SLOT);
+  *dev_out = dev;
+  *src = (const int*)(R.ring + k * OFF_SLOT);
   return 0;
 }
-int off_release(hipStream_t s, int k) {  // after the op that reads slot k is queued on s
-  ABCD_TRY(hipEventRecord(g_off_ev[k], s));
+int off_release(hipStream_t s, int dev, int k) {  // after the op that reads slot k is queued on s
+  OffRing& R = g_rings[dev];
+  ABCD_TRY(hipEventRecord(R.ev[k], s));
   std::lock_guard<std::mutex> lk(g_off_mu);
-  g_off_used[k] = true;
+  R.used[k] = true;
   return 0;
 }
 }  // namespace
@@ -1800,7 +1816,7 @@ int flush_offsets() {
   if (!g_pend.on) return 0;
   g_pend.on = false;
   ABCD_TRY(hipMemcpyAsync(g_pend.dst, g_pend.src, (size_t)g_pend.n * sizeof(int), hipMemcpyHostToDevice, g_pend.s));
-  return off_release(g_pend.s, g_pend.slot);
+  return off_release(g_pend.s, g_pend.dev, g_pend.slot);
 }
 
 // a table staged by a call that returned early (error path) is dropped, never
@@ -1809,19 +1825,19 @@ static void drop_stale_offsets() { g_pend.on = false; }
 
 int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst) {
   drop_stale_offsets();
-  int k;
+  int k, dev;
   const int* src;
-  ABCD_TRY((hipError_t)off_slot(off, &k, &src));
+  ABCD_TRY((hipError_t)off_slot(off, &k, &src, &dev));
   ABCD_TRY(hipMemcpyAsync(dst, src, off.size() * sizeof(int), hipMemcpyHostToDevice, s));
-  return off_release(s, k);
+  return off_release(s, dev, k);
 }
 
 int stage_offsets(hipStream_t s, const std::vector<int>& off, int* dst) {
   drop_stale_offsets();
-  int k;
+  int k, dev;
   const int* src;
-  ABCD_TRY((hipError_t)off_slot(off, &k, &src));
-  g_pend = PendingOff{s, dst, src, (int)off.size(), k, true};
+  ABCD_TRY((hipError_t)off_slot(off, &k, &src, &dev));
+  g_pend = PendingOff{s, dst, src, (int)off.size(), k, dev, true};
   return 0;
 }
 
@@ -1858,7 +1874,23 @@ __global__ __launch_bounds__(256) void persist_reset(unsigned* sync, long nwords
   for (long i = i0; i < noff; i += stride) off_dst[i] = off_src[i];
 }
 
+// ABCD_SPIN_LIMIT=<polls> (debug/tests): shrink the hand-off spin bound so a
+// wait times out at once; the device word is only rewritten when the value
+// changes (never in a default run)
+static int sync_spin_limit(hipStream_t s) {
+  static unsigned cur = 1u << 22, staged;
+  const char* v = getenv("ABCD_SPIN_LIMIT");
+  const unsigned want = (v && v[0]) ? (unsigned)strtoul(v, nullptr, 10) : (1u << 22);
+  if (want == cur) return 0;
+  staged = want;
+  ABCD_TRY(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_spin_limit), &staged, sizeof(staged), 0, hipMemcpyHostToDevice, s));
+  ABCD_TRY(hipStreamSynchronize(s));
+  cur = want;
+  return 0;
+}
+
 static int zero_sync_impl(hipStream_t s, unsigned* sync, int ngroups) {
+  ABCD_TRY((hipError_t)sync_spin_limit(s));
   const long nwords = (long)(2 * ngroups + PERSIST_REG_LINES + PERSIST_FLAG_LINES * ngroups) * PERSIST_SYNC_STRIDE;
   const char* v = getenv("ABCD_XCD");
   const long ticket = (v && v[0] == '1') ? -1 : (long)ngroups * PERSIST_SYNC_STRIDE;
@@ -1870,7 +1902,7 @@ static int zero_sync_impl(hipStream_t s, unsigned* sync, int ngroups) {
   ABCD_TRY(hipGetLastError());
   if (take) {
     g_pend.on = false;
-    ABCD_TRY((hipError_t)off_release(s, g_pend.slot));
+    ABCD_TRY((hipError_t)off_release(s, g_pend.dev, g_pend.slot));
   }
   return 0;
 }
@@ -1910,6 +1942,7 @@ static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
     TimedScope ts(s, TK_ENC_FWD);
     enc_fwd_persist<G, PD, X6, NXC><<<grid, 256, lds, s>>>(b);
   }
+  note_dispatch(TK_ENC_FWD, "enc_fwd_persist<%d,%d,%d,%d> grid %d", G, PD, X6, NXC, grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -1928,6 +1961,7 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
     TimedScope ts(s, TK_ENC_BWD);
     enc_bwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
   }
+  note_dispatch(TK_ENC_BWD, "enc_bwd_persist<%d,%d,%d> grid %d", G, PD, X6, grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -1990,6 +2024,7 @@ static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched, hipEv
     TimedScope ts(s, TK_ENC_BWD);
     enc_bwd_sk<G, NSUB><<<grid, 256, lds, s>>>(b);
   }
+  note_dispatch(TK_ENC_BWD, "enc_bwd_sk<%d,%d> grid %d", G, NSUB, grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -2006,13 +2041,14 @@ static bool splitk_enabled() {
 __global__ void gate_counters(const unsigned* sync, int ngroups, unsigned target) {
   const int lane = threadIdx.x;
   unsigned spins = 0;
+  const unsigned lim = g_spin_limit;
   for (;;) {
     bool ok = true;
     if (lane < ngroups)
       ok = __hip_atomic_load(sync + lane * PERSIST_SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
     if (__all(ok)) break;
     __builtin_amdgcn_s_sleep(8);
-    if (++spins > (1u << 22)) {
+    if (++spins > lim) {
       if (lane == 0) __hip_atomic_store(&g_persist_status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
@@ -2079,6 +2115,7 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
     TimedScope ts(s, TK_DEC_FWD);
     dec_fwd_persist<NCC><<<grid, 256, lds, s>>>(b);
   }
+  note_dispatch(TK_DEC_FWD, "dec_fwd_persist<%d> grid %d", NCC, grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -2100,6 +2137,7 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
     TimedScope ts(s, TK_DEC_FWD);
     dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
   }
+  note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -2159,6 +2197,7 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
     TimedScope ts(s, TK_DEC_BWD);
     dec_bwd_sk<NXS, NHS, NZ, GRU><<<grid, 256, lds, s>>>(b);
   }
+  note_dispatch(TK_DEC_BWD, "dec_bwd_sk<%d,%d,%d,%s> grid %d", NXS, NHS, NZ, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -2200,6 +2239,7 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
     TimedScope ts(s, TK_DEC_BWD);
     dec_bwd_persist<<<grid, 256, lds, s>>>(b);
   }
+  note_dispatch(TK_DEC_BWD, "dec_bwd_persist grid %d", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -2214,13 +2254,36 @@ extern "C" void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask) {
   abcd::g_prof_mask = mask;
 }
 
+namespace abcd {
+// stream-ordered: out[0] = the timeout status raised since the last fold
+// (0 ok, 1 hand-off wait, 2 side-stream gate), the word cleared and OR-ed
+// into the sticky word
+__global__ void step_status_kernel(float* out) {
+  if (threadIdx.x == 0) {
+    const unsigned v = __hip_atomic_exchange(&g_persist_status, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    out[0] = (float)v;
+    if (v) __hip_atomic_fetch_or(&g_persist_sticky, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+}  // namespace abcd
+
+extern "C" int abcd_step_status(float* out, void* stream) {
+  if (!out) return ABCD_EINVAL;
+  abcd::step_status_kernel<<<1, 64, 0, (hipStream_t)stream>>>(out);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
 // 0 = no persistent-kernel spin has timed out since the last call (reads and
-// clears the device word; synchronises the device)
+// clears the device words; synchronises the device)
 extern "C" int abcd_device_status(void) {
-  unsigned v = 0, z = 0;
+  unsigned v = 0, w = 0, z = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(abcd::g_persist_status), sizeof(v)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&w, HIP_SYMBOL(abcd::g_persist_sticky), sizeof(w)) != hipSuccess) return -1;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(abcd::g_persist_status), &z, sizeof(z));
-  return (int)v;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(abcd::g_persist_sticky), &z, sizeof(z));
+  return (int)(v | w);
 }
 
 // diagnostics only: number of persistent workgroups that ran in XCD-local

@@ -468,6 +468,7 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
       }
       ABCD_TRY((hipError_t)flush_offsets());
     }
+    if (!done) note_dispatch(TK_ENC_FWD, "per-step rnn_fwd_step<%d>", G);
     for (int i = 0; i < T && !done && !(diag_mask() & 8); ++i) {
       FwdArgs a{};
       a.H = H;
@@ -581,6 +582,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       else if (gate_ok && done) gated = true;
       ABCD_TRY((hipError_t)flush_offsets());
     }
+    if (!done) note_dispatch(TK_ENC_BWD, "per-step launch_bwd_step<%d>", G);
     for (int i = 0; i < T && !done; ++i) {
       BwdArgs a{};
       a.H = H;
@@ -1152,6 +1154,7 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
     ABCD_TRY((hipError_t)persist_decoder_fwd(s, G, pa, &done));
     ABCD_TRY((hipError_t)flush_offsets());
   }
+  if (!done) note_dispatch(TK_DEC_FWD, "per-step decoder forward<%d>", G);
   for (int t = 0; t < T && !done; ++t) {
     const int b_t = (int)bs[t];
     const int nb = t + 1 < T ? (int)bs[t + 1] : 0;
@@ -1302,6 +1305,7 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
     ABCD_TRY((hipError_t)flush_offsets());
   }
   const int TN = bwd_tn(H);
+  if (!done) note_dispatch(TK_DEC_BWD, "per-step decoder backward<%d>", G);
   for (int t = T - 1; t >= 0 && !done; --t) {
     const int b_t = (int)bs[t];
     const int nb = t + 1 < T ? (int)bs[t + 1] : 0;

@@ -84,7 +84,8 @@ class Learner(object):
         else:
             torch.manual_seed(seed)
             torch.cuda.manual_seed_all(seed)
-            noise.manual_seed(seed)
+            noise.manual_seed(seed, rank=self.rank)
+            self.seed = seed
             if encoder_hidden_dropout > 0.0 and encoder_rnn_layers == 1:
                 logger.warning("Non-zero dropout cannot be used for the single-layer encoder RNN "
                                "(because there is no non-top hidden layers).")
@@ -147,12 +148,16 @@ class Learner(object):
             speaker.to(self.device, non_blocking=True)
 
     def _shard(self, packed_input, is_offset, speaker):
-        """Rank's length-balanced shard of a global batch (parallel.shard_global_batch)."""
+        """Rank's length-balanced shard of a global batch (parallel.shard_global_batch),
+        or None when the global batch has fewer segments than ranks and this
+        rank gets none (it still joins the all-reduce: FusedStep.empty_step)."""
         if self.world == 1:
             return packed_input, is_offset, speaker
         seqs = torch.nn.utils.rnn.unpack_sequence(packed_input)
         offs = torch.nn.utils.rnn.unpack_sequence(is_offset)
         mine = parallel.shard_global_batch([len(s) for s in seqs], self.rank, self.world)
+        if not mine:
+            return None
         return (torch.nn.utils.rnn.pack_sequence([seqs[i] for i in mine]),
                 torch.nn.utils.rnn.pack_sequence([offs[i] for i in mine]), speaker[mine])
 
@@ -174,10 +179,15 @@ class Learner(object):
         records = []
         group = self.optimizer.param_groups[0]
         for batch_ix, (packed_input, is_offset, speaker, _) in enumerate(dataloader, 1):
-            packed_input, is_offset, speaker = self._shard(packed_input, is_offset, speaker)
-            data, bsz, off, spk = self._to_device(packed_input, is_offset, speaker)
-            sc = self.step.step(data, bsz, off, spk, num_strings, is_pretraining=is_pretraining, lr=group["lr"],
-                                momentum=group["momentum"], clip=self.gradient_clip)
+            # loss / batch_sizes[0] of the GLOBAL batch (learning.py:156) on every rank
+            b_global = int(packed_input.batch_sizes[0])
+            shard = self._shard(packed_input, is_offset, speaker)
+            if shard is None:
+                sc = self.step.empty_step(lr=group["lr"], momentum=group["momentum"], clip=self.gradient_clip)
+            else:
+                data, bsz, off, spk = self._to_device(*shard)
+                sc = self.step.step(data, bsz, off, spk, num_strings, is_pretraining=is_pretraining, lr=group["lr"],
+                                    momentum=group["momentum"], clip=self.gradient_clip, loss_batch=b_global)
             self._momentum_views()
             records.append(sc.clone())
             if not is_pretraining and hasattr(self.feature_sampler, "increment_iter_counts"):
@@ -185,9 +195,12 @@ class Learner(object):
         recs = torch.stack(records)
         if self.world > 1:
             dist.all_reduce(recs, op=dist.ReduceOp.SUM)
-            recs[:, engine.LOSS] /= self.world
-            recs[:, engine.PPL_CLUSTER:] /= self.world
-        recs = recs.cpu().double().numpy()
+            # LOSS sums to the global-batch loss; the perplexities are per-shard
+            # diagnostics, averaged
+            recs[:, engine.PPL_CLUSTER:engine.PPL_SHAPE + 1] /= self.world
+        recs = recs.cpu()
+        engine.check_status(recs, "training batch")
+        recs = recs.double().numpy()
         for batch_ix, r in enumerate(recs, 1):
             logger.info("{batch_ix}/{num_batches} training batches complete. mean loss: {loss:5.4f}. Perplexity of "
                         "the posterior clustering probs.: {cluster_perplex:5.4f}. Perplexity of the mean clustering "
@@ -221,17 +234,23 @@ class Learner(object):
         records = []
         with torch.no_grad():
             for batch_ix, (packed_input, is_offset, speaker, _) in enumerate(dataloader, 1):
-                packed_input, is_offset, speaker = self._shard(packed_input, is_offset, speaker)
-                data, bsz, off, spk = self._to_device(packed_input, is_offset, speaker)
+                b_global = int(packed_input.batch_sizes[0])
+                shard = self._shard(packed_input, is_offset, speaker)
+                if shard is None:
+                    records.append(torch.zeros_like(self.step.scalars))
+                    continue
+                data, bsz, off, spk = self._to_device(*shard)
                 sc, _ = self.step.forward_backward(data, bsz, off, spk, num_strings, is_pretraining=is_pretraining,
-                                                   train=False)
-                records.append(sc[:engine.LOSS].clone())
+                                                   train=False, loss_batch=b_global)
+                records.append(sc.clone())
                 logger.info("{batch_ix}/{num_batches} validation batches complete.".format(
                     batch_ix=batch_ix, num_batches=num_batches))
         recs = torch.stack(records)
         if self.world > 1:
             dist.all_reduce(recs, op=dist.ReduceOp.SUM)
-        recs = recs.cpu().double().numpy()
+        recs = recs.cpu()
+        engine.check_status(recs, "validation batch")
+        recs = recs.double().numpy()
         emission_loss = recs[:, engine.EM].sum() / num_strings
         end_prediction_loss = recs[:, engine.OFF].sum() / num_strings
         kl_loss = recs[:, engine.KL].sum() / num_strings
@@ -247,8 +266,16 @@ class Learner(object):
               learning_rate=0.1, momentum=0.9, gradient_clip=0.25, patience=0, featurizer=None):
         """learning.py:245-290.  featurizer: a data_utils.DeviceFeaturizer when the
         datasets return raw samples (--gpu_featurize)."""
+        # single device: RandomSampler draws from the global CPU generator as in
+        # the reference (bit-exact batch order).  Data parallel: a generator of
+        # its own, seeded alike on every rank, so the host-side noise draws of
+        # --noise reference (shard-sized, so rank-dependent) cannot make the
+        # ranks shuffle -- and shard -- different global batches
+        gen = None
+        if self.world > 1:
+            gen = torch.Generator().manual_seed(getattr(self, "seed", 1111))
         train_dataloader = data_utils.DataLoader(train_dataset, batch_size=batch_size_train, shuffle=True,
-                                                 featurizer=featurizer)
+                                                 featurizer=featurizer, generator=gen)
         valid_dataloader = data_utils.DataLoader(valid_dataset, batch_size=batch_size_valid, featurizer=featurizer)
         self.optimizer = torch.optim.SGD(self.parameters(), lr=learning_rate, momentum=momentum)
         if self.retrieval:
@@ -299,7 +326,14 @@ class Learner(object):
             self._momentum_views()
 
     def save_model(self, epoch):
-        """learning.py:293-314 (same keys; plus the Philox noise state)."""
+        """learning.py:293-314 (same keys; plus the Philox noise state).  Under
+        data parallelism the stored Philox offset is the maximum over the ranks,
+        so a resumed rank never re-draws counters it already used."""
+        nstate = noise.get_state()
+        if self.world > 1:
+            o = torch.tensor([nstate["offset"]], dtype=torch.int64, device=self.device)
+            dist.all_reduce(o, op=dist.ReduceOp.MAX)
+            nstate["offset"] = int(o)
         if self.rank != 0:
             return
         self._momentum_views()
@@ -315,7 +349,7 @@ class Learner(object):
             "lr_scheduler": self.lr_scheduler.state_dict(),
             "gradient_clip": self.gradient_clip,
             "random_state": torch.get_rng_state(),
-            "abcd_noise_state": noise.get_state(),
+            "abcd_noise_state": nstate,
         }
         if torch.cuda.is_available():
             checkpoint["random_state_cuda"] = torch.cuda.get_rng_state_all()
@@ -344,7 +378,7 @@ class Learner(object):
         except RuntimeError:
             logger.warning("Failed to retrieve random_state.")
         if "abcd_noise_state" in self.checkpoint:
-            noise.set_state(self.checkpoint["abcd_noise_state"])
+            noise.set_state(self.checkpoint["abcd_noise_state"], rank=self.rank)
         if "random_state_cuda" in self.checkpoint:
             try:
                 torch.cuda.set_rng_state_all(self.checkpoint["random_state_cuda"])

@@ -147,9 +147,13 @@ _SIGS = {
     "abcd_timing_reset": (None, []),
     "abcd_timing_read": (c_int, [ctypes.POINTER(c_double)]),
     "abcd_timing_read_kernel": (c_int, [c_int, ctypes.POINTER(c_double)]),
+    "abcd_dispatch_name": (ctypes.c_char_p, [c_int]),
+    "abcd_dispatch_count": (c_long, [c_int]),
+    "abcd_dispatch_reset": (None, []),
     "abcd_fill_normal": (c_int, [c_void_p, c_long, c_uint64, c_uint64, c_void_p]),
     "abcd_fill_dropout": (c_int, [c_void_p, c_long, c_float, c_uint64, c_uint64, c_void_p]),
     "abcd_device_status": (c_int, []),
+    "abcd_step_status": (c_int, [c_void_p, c_void_p]),
 }
 EXPORTED = sorted(_SIGS)
 
@@ -176,6 +180,17 @@ class HipError(RuntimeError):
     pass
 
 
+class PersistTimeout(HipError):
+    """A persistent recurrent kernel's hand-off wait timed out: the grid was
+    not co-resident and the step's results are invalid."""
+
+
+def raise_on_status(status, where):
+    if status:
+        raise PersistTimeout(f"{where}: a persistent recurrent kernel timed out waiting for its group "
+                             f"(status {int(status)}); the results of that step are invalid")
+
+
 def check(rc, what):
     if rc != 0:
         if rc == ABCD_EINVAL:
@@ -199,6 +214,16 @@ def stream():
 
 def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+ENC_FWD, ENC_BWD, DEC_FWD, DEC_BWD = 1, 2, 3, 4
+
+
+def dispatch():
+    """{role: (kernel name of its last launch, launches since reset)}"""
+    L = lib()
+    return {r: (L.abcd_dispatch_name(k).decode(), int(L.abcd_dispatch_count(k)))
+            for r, k in (("enc_fwd", ENC_FWD), ("enc_bwd", ENC_BWD), ("dec_fwd", DEC_FWD), ("dec_bwd", DEC_BWD))}
 
 
 def ptr_array(tensors):

@@ -205,12 +205,12 @@ class DataLoader(object):
     samples (transform=None) and the whole batch is featurised and packed on
     the GPU; batch order, in-batch sort and outputs are those of the host path."""
 
-    def __init__(self, dataset, batch_size=1, shuffle=False, featurizer=None):
+    def __init__(self, dataset, batch_size=1, shuffle=False, featurizer=None, generator=None):
         self.dataset = dataset
         self.featurizer = featurizer
         self.shuffle = shuffle
         if shuffle:
-            sampler = torch.utils.data.RandomSampler(self.dataset, replacement=False)
+            sampler = torch.utils.data.RandomSampler(self.dataset, replacement=False, generator=generator)
         else:
             sampler = torch.utils.data.SequentialSampler(self.dataset)
         self.batch_sampler = torch.utils.data.BatchSampler(sampler, batch_size, drop_last=False)

@@ -14,17 +14,17 @@ synchronises with the host; loss terms and diagnostics stay on the device in
 """
 import itertools
 
-import os
-
 import torch
 
 from . import _native as N
 from . import noise as _noise
 from .model import ABCDSampler
 
-# layout of the device scalar vector returned by FusedStep.step
-EM, OFF, KL, LOSS, NORM, PPL_CLUSTER, PPL_BATCH, PPL_SHAPE = range(8)
-N_SCALARS = 8
+# layout of the device scalar vector returned by FusedStep.step; STATUS is the
+# persistent kernels' timeout status of the step (abcd_step_status, non-zero =
+# the step's results are invalid; check_status raises)
+EM, OFF, KL, LOSS, NORM, PPL_CLUSTER, PPL_BATCH, PPL_SHAPE, STATUS = range(9)
+N_SCALARS = 9
 
 
 class FlatParams:
@@ -122,14 +122,21 @@ class FusedStep:
 
     # --------------------------------------------------------------- the step
     def forward_backward(self, data, batch_sizes, is_offset, speakers, entire_data_size, is_pretraining=False,
-                         train=True):
-        """Forward + backward of learning.py:149-158; gradients land in flat.grad."""
+                         train=True, loss_batch=None):
+        """Forward + backward of learning.py:149-158; gradients land in flat.grad.
+
+        loss_batch: the loss normaliser (learning.py:156 ``batch_sizes[0]``).
+        Default: this batch's B.  Under data parallelism every rank passes the
+        GLOBAL batch size, so its loss is (em_r + off_r + kl_r) / B_global and
+        the SUM of the ranks' gradients (and losses) is exactly the reference's
+        global-batch value (parallel.py)."""
         L_ = N.lib()
         st = N.stream()
         data = data.contiguous()
         N.require_gpu(data)
         pk, bs_keep = _packed(data, batch_sizes, self.enc_cfg.input_size)
         T, L, B = pk.T, pk.L, pk.B
+        Bn = int(loss_batch) if loss_batch is not None else B
         dev = self.device
         sc = self.scalars
         ws_e = self._workspace("enc", L_.abcd_encoder_workspace_bytes(self.enc_cfg, T, L, B))
@@ -146,6 +153,7 @@ class FusedStep:
         N.check(L_.abcd_sampler_forward(self.samp_cfg, self.samp_p, N.ptr(h), B, N.ptr(logits), N.ptr(ws_s),
                                         ws_s.numel(), st), "sampler forward")
         feats = torch.empty(B, self.Dfeat, device=dev)
+        self.last_hidden, self.feats = h, feats  # kept for inspection (encode paths, parity tests)
         if self.plain:
             mode, tau = 0, 1.0
             nt, seed, off = _noise.normal(B, self.Dfeat, dev)
@@ -158,9 +166,10 @@ class FusedStep:
                                        N.ptr(feats), N.ptr(ws_s), ws_s.numel(), st), "sampler sample")
         # the Dirichlet KL (three small kernels) only feeds the loss scalar and
         # the backward: on the idle side stream beside the decoder's setup
-        # (ABCD flavour only: plain KL and sample share the MV stash copy)
+        # (ABCD flavour only: plain KL and sample share the MV stash copy);
+        # measured ~30 us/step at c2
         kl_side = None
-        if not self.plain and os.environ.get("ABCD_KLSIDE", "1") != "0":
+        if not self.plain:
             kl_side = self._side_stream()
             kl_side.wait_stream(torch.cuda.current_stream(dev))
         N.check(L_.abcd_sampler_kl(self.samp_cfg, self.samp_p, N.ptr(logits), B, float(entire_data_size),
@@ -173,75 +182,36 @@ class FusedStep:
         if self.decoder.embed_speaker is not None:
             spk = speakers.to(dev, torch.int64).contiguous()
         gt_off = is_offset.contiguous()
-        # the loss reductions (emission NLL, BCE sum, total loss) only feed the
-        # scalars: ABCD_LOSSSIDE=1 queues them on the side stream beside the
-        # offset head (joined with the rest of the side work).  Measured at c2
-        # (10 alternating runs): 13.692 vs 13.704 ms -- within noise (the NLL
-        # pass shares the chip with the offset-head GEMM), so off by default.
-        loss_side = self._side_stream() if os.environ.get("ABCD_LOSSSIDE", "0") == "1" else None
-        kl_done = None
-        if kl_side is not None and loss_side is not None:
-            kl_done = torch.cuda.Event()
-            kl_done.record(kl_side)
         N.check(L_.abcd_decoder_forward_split(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
                                               N.ptr(eps), N.ptr(xmask), eseed, eoff, None, None, None, None,
-                                              N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st,
-                                              N.c_void_p(None if loss_side is None else loss_side.cuda_stream)),
+                                              N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st, None),
                 "decoder forward")
-        if loss_side is None:
-            if kl_side is not None:
-                torch.cuda.current_stream(dev).wait_stream(kl_side)
-            N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), B, N.ptr(sc[LOSS:LOSS + 1]),
-                                       st), "total loss")
-        else:  # the side stream already holds the KL (or waited for it on the main stream)
-            N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), B, N.ptr(sc[LOSS:LOSS + 1]),
-                                       N.c_void_p(loss_side.cuda_stream)), "total loss")
+        if kl_side is not None:
+            torch.cuda.current_stream(dev).wait_stream(kl_side)
+        N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), Bn, N.ptr(sc[LOSS:LOSS + 1]), st),
+                "total loss")
         if not train:
-            if loss_side is not None:
-                torch.cuda.current_stream(dev).wait_stream(loss_side)
+            N.check(L_.abcd_step_status(N.ptr(sc[STATUS:STATUS + 1]), st), "step status")
             return sc, logits
-        inv = self._inv_b(B)
+        inv = self._inv_b(Bn)
         d_feats = torch.empty(B, self.Dfeat, device=dev)
         # the decoder's weight-gradient reductions run on a side stream beside
-        # the sampler + encoder backward (joined below, before clip + SGD).
-        # ABCD_DECSIDE=0 keeps them on the main stream: measured at c2 the
-        # encoder BPTT then runs 1.85 ms instead of 2.37, but the step is
-        # ~0.55 ms longer (the wgrads cost ~1.05 ms alone)
+        # the sampler + encoder backward (joined below, before clip + SGD):
+        # measured at c2 ~0.5 ms/step shorter than serial (DESIGN.md §3 Streams)
         side = self._side_stream()
         N.check(L_.abcd_decoder_backward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
                                                  N.ptr(xmask), N.ptr(inv), N.ptr(inv), N.ptr(d_feats), self.dec_g,
-                                                 N.ptr(ws_d), ws_d.numel(), st,
-                                                 N.c_void_p(None if os.environ.get("ABCD_DECSIDE") == "0"
-                                                            else side.cuda_stream)),
+                                                 N.ptr(ws_d), ws_d.numel(), st, N.c_void_p(side.cuda_stream)),
                 "decoder backward")
         d_h = torch.empty(B, self.E, device=dev)
-        if kl_done is not None:  # the KL stash (Q, v) feeds the sampler backward
-            torch.cuda.current_stream(dev).wait_event(kl_done)
         N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
                                                float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
-                                               self.samp_g, N.ptr(ws_s), ws_s.numel(), st,
-                                               N.c_void_p(self._sampler_wgrad_stream(side))), "sampler backward")
+                                               self.samp_g, N.ptr(ws_s), ws_s.numel(), st, None), "sampler backward")
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
                                                  self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
                                                  N.c_void_p(side.cuda_stream)), "encoder backward")
         torch.cuda.current_stream(dev).wait_stream(side)
-        if getattr(self, "_side2", None) is not None:
-            torch.cuda.current_stream(dev).wait_stream(self._side2)
         return sc, logits
-
-    def _sampler_wgrad_stream(self, side):
-        # Default: one stream.  Measured at c2 (same box, A/B): the sampler's
-        # parameter gradients on the wgrad stream (1) or a third stream (2)
-        # shorten the chain into the encoder BPTT by ~150 us but slow the
-        # BPTT by ~200 us (more side work co-resident with its workgroups).
-        mode = os.environ.get("ABCD_SAMPSPLIT", "0")
-        if mode == "0":
-            return None
-        if mode == "1":
-            return side.cuda_stream
-        if getattr(self, "_side2", None) is None:
-            self._side2 = torch.cuda.Stream(self.device)
-        return self._side2.cuda_stream
 
     def _side_stream(self):
         s = getattr(self, "_side", None)
@@ -266,16 +236,35 @@ class FusedStep:
         if buf is not None:
             self.momentum_init = False
 
+    def empty_step(self, lr, momentum=0.0, clip=1.0):
+        """A data-parallel rank whose shard of the global batch is empty: zero
+        gradient and loss terms, but it still joins the all-reduce and applies
+        the identical clip + SGD (so no rank waits on it)."""
+        self.flat.grad.zero_()
+        self.scalars.zero_()
+        self.optimizer_step(lr, momentum, clip)
+        return self.scalars
+
     def step(self, data, batch_sizes, is_offset, speakers, entire_data_size, is_pretraining=False, lr=1.0,
-             momentum=0.0, clip=1.0):
+             momentum=0.0, clip=1.0, loss_batch=None):
         sc, logits = self.forward_backward(data, batch_sizes, is_offset, speakers, entire_data_size,
-                                           is_pretraining)
+                                           is_pretraining, loss_batch=loss_batch)
         self.optimizer_step(lr, momentum, clip)
         if not self.plain:  # learning.py:171-178 reads posterior_shape_logits AFTER the SGD step
             N.check(N.lib().abcd_perplexities(N.ptr(logits), logits.shape[0], logits.shape[1],
                                               N.ptr(self.sampler.posterior_shape_logits),
                                               N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 3]), N.stream()), "perplexities")
+        N.check(N.lib().abcd_step_status(N.ptr(sc[STATUS:STATUS + 1]), N.stream()), "step status")
         return sc
+
+
+def check_status(records, where="training step"):
+    """Raise if any step's STATUS slot (rows of stacked scalar vectors, or
+    one vector) is non-zero.  Call at a host read the caller already makes."""
+    r = records.detach().reshape(-1, records.shape[-1])[:, STATUS]
+    bad = r.nonzero()
+    if bad.numel():
+        N.raise_on_status(float(r[bad[0, 0]]), f"{where} {int(bad[0, 0]) + 1}")
 
 
 def _packed(data, batch_sizes, F):

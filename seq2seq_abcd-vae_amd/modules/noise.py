@@ -43,8 +43,15 @@ def get_mode():
     return _state["mode"]
 
 
-def manual_seed(seed):
-    _state["seed"] = int(seed) & 0xFFFFFFFFFFFFFFFF
+def manual_seed(seed, rank=0):
+    """Seed the Philox stream.  Under data parallelism every rank passes its
+    rank: rank r > 0 gets its own key (seed xor a rank hash), so the ranks'
+    shards draw independent Gumbel / decoder / dropout noise as one device
+    would for the global batch; rank 0 keeps the single-device stream."""
+    key = int(seed) & 0xFFFFFFFFFFFFFFFF
+    if rank:
+        key ^= (0x9E3779B97F4A7C15 * (int(rank) + 1)) & 0xFFFFFFFFFFFFFFFF
+    _state["seed"] = key
     _state["offset"] = 0
 
 
@@ -52,8 +59,12 @@ def get_state():
     return dict(_state)
 
 
-def set_state(st):
+def set_state(st, rank=0):
+    """Restore a state saved by get_state (rank 0's, under data parallelism);
+    rank r > 0 re-derives its own key from it (manual_seed's rank hash)."""
     _state.update({k: st[k] for k in ("mode", "seed", "offset") if k in st})
+    if rank and "seed" in st:
+        _state["seed"] = (int(st["seed"]) ^ ((0x9E3779B97F4A7C15 * (int(rank) + 1)) & 0xFFFFFFFFFFFFFFFF))
 
 
 class mode:

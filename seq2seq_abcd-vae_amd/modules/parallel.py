@@ -4,12 +4,14 @@ step.
 The reference is single-device (learning.py:74,360).  Segments are independent,
 so the batch shards naturally: every rank runs the full step on
 its own b segments, then the flat fp32 gradient buffer (all 1.95 M parameters,
-7.4 MiB) is averaged with ONE all-reduce -- RCCL over xGMI with the "nccl"
+7.4 MiB) is SUMMED with ONE all-reduce -- RCCL over xGMI with the "nccl"
 backend on ROCm, gloo on CPU for tests -- and every rank applies the identical
-global-norm clip + SGD.  With equal per-rank batch sizes the averaged gradient
-equals the gradient of the reference loss on the concatenated global batch
-(loss_r = (em_r + off_r + kl_r) / B_r, kl_r with the per-rank B_r and the global
-N).
+global-norm clip + SGD (clip after the reduce, learning.py:161).  Each rank
+normalises its loss by the GLOBAL batch size (FusedStep(..., loss_batch=B)):
+loss_r = (em_r + off_r + kl_r) / B_global with kl_r using the rank's B_r in the
+prior term (B_r / N) and the global N, so sum_r loss_r is exactly the
+reference's (em + off + kl) / batch_sizes[0] on the concatenated batch
+(learning.py:155-157), for any split, unequal or empty shards included.
 
 ``shard_global_batch`` implements the straggler-free partition of §8e: sort
 the global batch by length (desc) and deal rows round-robin, so every rank gets
@@ -26,24 +28,18 @@ def world():
 
 
 def make_allreduce(group=None):
-    """Returns f(flat_grad) that averages the flat gradient buffer in place."""
-    backend = dist.get_backend(group)
+    """Returns f(flat_grad) that sums the flat gradient buffer over the ranks
+    in place (each rank's gradient is already scaled by 1 / B_global)."""
 
     def allreduce(g):
-        ws = dist.get_world_size(group)
-        if ws == 1:
-            return
-        if backend == "nccl":
-            dist.all_reduce(g, op=dist.ReduceOp.AVG, group=group)
-        else:
+        if dist.get_world_size(group) > 1:
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
-            g.div_(ws)
 
     return allreduce
 
 
 def attach(step, group=None):
-    """Make a FusedStep data-parallel: gradients are averaged before clip+SGD."""
+    """Make a FusedStep data-parallel: gradients are summed before clip+SGD."""
     step.allreduce = make_allreduce(group)
     return step
 

@@ -31,7 +31,8 @@ class Learner(learning.Learner):
             return
         torch.manual_seed(seed)
         torch.cuda.manual_seed_all(seed)
-        noise.manual_seed(seed)
+        noise.manual_seed(seed, rank=self.rank)
+        self.seed = seed
         self.encoder = model.RNN_Variational_Encoder(input_size, encoder_rnn_hidden_size, rnn_type=encoder_rnn_type,
                                                      rnn_layers=encoder_rnn_layers,
                                                      hidden_dropout=encoder_hidden_dropout,

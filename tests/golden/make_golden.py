@@ -262,6 +262,128 @@ def run_small(name, cfg):
 
 
 # --------------------------------------------------------------------------
+# production-shape one-step fixtures
+# --------------------------------------------------------------------------
+# Widths of BASELINE.json configs 2/4/5 (F = 129, H = Hm = D = 256, K = 128 or
+# 1024, speaker 256) with B = 72 segments, so the persistent kernels run two
+# 64-row tile groups (the second one 8 rows, all short), and T <= 24 so the
+# reference finishes in seconds.  Weights are NOT stored: they are re-created
+# by the init order (torch.manual_seed(1111), encoder -> sampler -> decoder)
+# and pinned by per-module checksums.  Inputs and noise are regenerated from
+# seeds by tests/golden_io.py:prod_inputs (sha256 stored).
+PROD_DIMS = dict(F=129, H=256, Hm=256, D=256, K=128, S=None, NSPK=None, FPLAIN=16)
+PROD_VARIANTS = {
+    "lstm_k128": dict(rnn="LSTM"),
+    "lstm_k128_pretrain": dict(rnn="LSTM", pretrain=True),
+    "gru_k1024_spk": dict(rnn="GRU", K=1024, S=256, NSPK=16),
+    "lstm_k1024_spk": dict(rnn="LSTM", K=1024, S=256, NSPK=16),
+    "plain_lstm": dict(rnn="LSTM", plain=True),
+}
+FULL_GRAD_MAX = 40000  # gradients up to this many elements are stored in full
+
+
+def run_prod(name, cfg):
+    plain = cfg.get("plain", False)
+    torch, model, data_utils, clip_legacy = import_reference("plain" if plain else "ABCD-VAE")
+    sys.path.insert(0, os.path.dirname(HERE))
+    from golden_io import prod_inputs, sha16  # noqa: E402  (build-owned helper)
+    d = dict(PROD_DIMS, **{k: cfg[k] for k in ("K", "S", "NSPK") if k in cfg})
+    meta = dict(cfg, name=name, dims=d, B=72, tmin=4, tmax=20, seed_data=4242, seed_noise=777, N=10000,
+                lr=1.0, clip=1.0)
+    F, H, Hm, D, K = d["F"], d["H"], d["Hm"], d["D"], d["K"]
+    rnn, pretrain, speaker = cfg["rnn"], cfg.get("pretrain", False), d["NSPK"] is not None
+    inp = prod_inputs(meta)
+    B = meta["B"]
+
+    torch.manual_seed(1111)
+    enc = model.RNN_Variational_Encoder(F, H, rnn_type=rnn)
+    if plain:
+        samp = model.Sampler(enc.hidden_size_total, Hm, d["FPLAIN"])
+        fdim = d["FPLAIN"]
+    else:
+        samp = model.ABCDSampler(enc.hidden_size_total, Hm, K, D)
+        fdim = D
+    dec = model.RNN_Variational_Decoder(F, H, Hm, fdim, rnn_type=rnn, num_speakers=d["NSPK"],
+                                        speaker_embed_dim=d["S"])
+    modules = [("encoder", enc), ("feature_sampler", samp), ("decoder", dec)]
+    init = {f"{p}/{k}": v.detach().clone() for p, m in modules for k, v in m.state_dict().items()}
+    meta["init_sha"] = {p: module_checksums(torch, m)[1] for p, m in modules}
+    meta["init_sum"] = {p: module_checksums(torch, m)[0] for p, m in modules}
+    enc.train(); samp.train(); dec.train()
+
+    # the reference draws its noise from the global generator: seed it so the
+    # draws are exactly prod_inputs' generator stream (checked below)
+    torch.manual_seed(meta["seed_noise"])
+    packed = torch.nn.utils.rnn.PackedSequence(inp["data"], inp["batch_sizes"])
+    params = list(enc.parameters()) + list(samp.parameters()) + list(dec.parameters())
+    opt = torch.optim.SGD(params, lr=1.0, momentum=0.0)
+    opt.zero_grad()
+    last_hidden = enc(packed)
+    if plain:
+        fparams = samp(last_hidden)
+        feats = samp.sample(fparams)
+        kl = samp.kl_divergence(fparams)
+        logits = torch.cat(fparams, -1)
+    else:
+        logits = samp(last_hidden)
+        feats = samp.sample(logits, no_sample=pretrain)
+        kl = samp.kl_divergence(logits, meta["N"])
+    spk = inp["speakers"] if speaker else torch.full((B,), float("nan"))
+    em, off, flat_out, (mu, lv), off_logits = dec(
+        feats, batch_sizes=inp["batch_sizes"], speaker=spk, ground_truth_out=inp["data"],
+        ground_truth_offset=inp["is_offset"])
+    loss = (em + off + kl) / inp["batch_sizes"][0]
+    loss.backward()
+    # the replayed noise is what the reference consumed
+    assert torch.equal(flat_out, mu + (0.5 * lv).exp() * inp["eps"]) or \
+        torch.allclose(flat_out, mu + (0.5 * lv).exp() * inp["eps"], rtol=1e-6, atol=1e-6)
+    if not plain and not pretrain:
+        y = torch.softmax((logits + inp["feat_noise"]) / samp.temperature, -1)
+        assert torch.allclose(feats, y @ samp.codebook.t(), rtol=1e-5, atol=1e-6)
+    out = {"last_hidden": last_hidden, "logits": logits, "feats": feats, "kl": kl, "em": em, "off": off,
+           "loss": loss, "offset_logits": off_logits,
+           "mu_rowsum": mu.sum(1), "lv_rowsum": lv.sum(1), "flat_rowsum": flat_out.sum(1),
+           "mu_colsum": mu.sum(0), "lv_colsum": lv.sum(0)}
+    for p, m in modules:
+        for k, v in m.named_parameters():
+            g = v.grad
+            if g is None:
+                continue
+            g = g.to_dense() if g.is_sparse else g
+            out[f"gn/{p}/{k}"] = g.norm()
+            if g.numel() <= FULL_GRAD_MAX:
+                out[f"g/{p}/{k}"] = g.clone()
+            elif g.dim() == 2:
+                out[f"grow/{p}/{k}"] = g.sum(1)
+                out[f"gcol/{p}/{k}"] = g.sum(0)
+    total_norm = clip_legacy(params, 1.0) if speaker else float(torch.nn.utils.clip_grad_norm_(params, 1.0))
+    opt.step()
+    for p, m in modules:
+        for k, v in m.state_dict().items():
+            delta = (v.detach() - init[f"{p}/{k}"]).double()
+            out[f"dq_sum/{p}/{k}"] = delta.sum()
+            out[f"dq_norm/{p}/{k}"] = delta.norm()
+    out["total_norm"] = torch.tensor(total_norm)
+    if not plain:
+        top2 = logits.topk(2, -1).values
+        meta["argmax_min_gap"] = float((top2[:, 0] - top2[:, 1]).min())
+    meta["sha"] = {k: sha16(inp[k]) for k in ("data", "eps", "speakers", "is_offset")}
+    if inp["feat_noise"] is not None:
+        meta["sha"]["feat_noise"] = sha16(inp["feat_noise"])
+    meta["L"] = int(inp["data"].shape[0])
+    meta["T"] = int(inp["batch_sizes"].numel())
+    meta["temperature"] = None if plain else samp.temperature
+    arrays = {k: v.detach().numpy() for k, v in out.items()}
+    arrays = {k: v.astype(np.float32) if v.dtype == np.float64 and not k.startswith("dq_") else v
+              for k, v in arrays.items()}
+    arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    path = os.path.join(HERE, f"prod_{name}.npz")
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path}: L={meta['L']} T={meta['T']} loss={float(loss):.6f} em={float(em):.4f} "
+          f"off={float(off):.4f} kl={float(kl):.6f} gap={meta.get('argmax_min_gap')}")
+
+
+# --------------------------------------------------------------------------
 # toy first-batch fixture at full widths (config 1)
 # --------------------------------------------------------------------------
 def module_checksums(torch, module):
@@ -420,7 +542,7 @@ def main():
         cli_child(vdir, script, sys.argv[5:])
         return
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=["small", "toy", "cli"], default=None)
+    ap.add_argument("--only", choices=["small", "prod", "toy", "cli", "ckpt"], default=None)
     ap.add_argument("--variant", default=None)
     ap.add_argument("--case", default=None, help="cli: regenerate only this trajectory")
     a = ap.parse_args()
@@ -435,6 +557,13 @@ def main():
             subprocess.run([sys.executable, "-c",
                             "import sys; sys.argv=['x']; sys.path.insert(0, %r); import make_golden as m; "
                             "m.run_small(%r, m.SMALL_VARIANTS[%r])" % (HERE, name, name)], check=True)
+    if a.only in (None, "prod"):
+        for name, cfg in PROD_VARIANTS.items():
+            if a.variant and name != a.variant:
+                continue
+            subprocess.run([sys.executable, "-c",
+                            "import sys; sys.argv=['x']; sys.path.insert(0, %r); import make_golden as m; "
+                            "m.run_prod(%r, m.PROD_VARIANTS[%r])" % (HERE, name, name)], check=True)
     if a.only in (None, "toy"):
         subprocess.run([sys.executable, "-c",
                         "import sys; sys.path.insert(0, %r); import make_golden as m; m.run_toy_step()" % HERE],

@@ -44,6 +44,53 @@ def noise_from(meta, arr):
     return dict(feat=feat, eps=arr["eps"], xmask=arr.get("xmask"))
 
 
+PROD = sorted(f[len("prod_"):-len(".npz")] for f in os.listdir(GOLDEN) if f.startswith("prod_"))
+
+
+def load_prod(name):
+    z = np.load(os.path.join(GOLDEN, f"prod_{name}.npz"), allow_pickle=False)
+    meta = json.loads(bytes(z["meta"]).decode())
+    arr = {k: torch.from_numpy(np.array(z[k])) for k in z.files if k != "meta"}
+    return meta, arr
+
+
+def sha16(t):
+    import hashlib
+    return hashlib.sha256(t.detach().contiguous().cpu().numpy().tobytes()).hexdigest()[:16]
+
+
+def prod_inputs(meta):
+    """Inputs of a production-shape fixture, regenerated from its seeds with
+    torch's CPU generator (same calls as tests/golden/make_golden.py:run_prod,
+    which stored the sha256 of each so a regeneration that differs fails).
+
+    Lengths U{tmin..tmax} (first forced to tmax), sorted desc; frames
+    x ~ N(0,1); speakers U{0..nspk-1}; then, from a second generator, the
+    step's noise in the reference's draw order: Gumbel -log(Exp(1)) (B x K)
+    unless pretraining (plain: randn(B, f)), then randn(bs_t, F) per decoder
+    step (model.py:604, 19)."""
+    d = meta["dims"]
+    F, B = d["F"], meta["B"]
+    g = torch.Generator().manual_seed(meta["seed_data"])
+    lens = torch.randint(meta["tmin"], meta["tmax"] + 1, (B,), generator=g)
+    lens[0] = meta["tmax"]
+    lens, _ = torch.sort(lens, descending=True)
+    seqs = [torch.randn(int(T), F, generator=g) for T in lens]
+    spk = torch.randint(0, max(d.get("NSPK") or 1, 1), (B,), generator=g)
+    packed = torch.nn.utils.rnn.pack_sequence(seqs)
+    is_off = torch.nn.utils.rnn.pack_sequence([torch.tensor([0.0] * (int(T) - 1) + [1.0]) for T in lens]).data
+    gn = torch.Generator().manual_seed(meta["seed_noise"])
+    if meta.get("plain"):
+        feat_noise = torch.randn(B, d["FPLAIN"], generator=gn)
+    elif not meta.get("pretrain", False):
+        feat_noise = -torch.empty(B, d["K"]).exponential_(generator=gn).log()
+    else:
+        feat_noise = None
+    eps = torch.cat([torch.randn(int(bs), F, generator=gn) for bs in packed.batch_sizes], 0)
+    return dict(data=packed.data, batch_sizes=packed.batch_sizes, is_offset=is_off, speakers=spk,
+                feat_noise=feat_noise, eps=eps, lengths=lens)
+
+
 def known_answers():
     with open(os.path.join(GOLDEN, "toy_known_answers.json")) as f:
         return json.load(f)

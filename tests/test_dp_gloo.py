@@ -1,14 +1,19 @@
-"""Data-parallel path on CPU with the gloo backend, world_size 2.
+"""Data-parallel path on CPU with the gloo backend.
 
 Checks, with the CPU oracle computing per-rank gradients:
 * the flat-gradient all-reduce used by the fused step (parallel.make_allreduce)
-  averages exactly;
+  sums exactly;
 * sharding a length-sorted global batch round-robin gives each rank a
   length-sorted shard of (nearly) equal frame count;
-* averaged per-rank gradients (loss_r = (em_r + off_r + kl_r) / B_r, kl_r with
-  the per-rank B_r and the global N) equal the gradient of the reference loss
-  on the concatenated global batch -- the invariant that makes one all-reduce
-  per step exact."""
+* summed per-rank gradients (loss_r = (em_r + off_r + kl_r) / B_global, kl_r
+  with the per-rank B_r and the global N) equal the gradient of the reference
+  loss on the concatenated global batch -- for 2 equal shards and for 3
+  unequal ones (8 = 3 + 3 + 2 segments): the invariant that makes one
+  all-reduce per step exact.
+* learning.py's host side of the same: the shard of a global batch with fewer
+  segments than ranks is empty (the rank joins the all-reduce with zero
+  gradients), and the per-rank Philox keys differ while rank 0 keeps the
+  single-device stream."""
 import os
 import sys
 
@@ -53,7 +58,8 @@ def _worker(rank, world, port, q):
     L = batch["data"].shape[0]
     g = torch.Generator().manual_seed(100 + rank)
     eps = torch.randn(L, F, generator=g)
-    _, grads, _, _, _ = O.train_step(P, batch, cfg, dict(feat=None, eps=eps), 40, pretrain=True)
+    _, grads, _, _, _ = O.train_step(P, batch, cfg, dict(feat=None, eps=eps), 40, pretrain=True,
+                                     loss_batch=len(lengths))
     flat = torch.cat([v.reshape(-1) for v in grads.values()])
     allreduce = parallel.make_allreduce()
     allreduce(flat)
@@ -63,21 +69,25 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_dp_two_ranks_equals_global_batch():
+@pytest.mark.parametrize("world", [2, 3])
+def test_dp_ranks_equal_global_batch(world):
     from oracle import abcd_oracle as O
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29000 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    port = 29000 + (os.getpid() * 7 + world * 131) % 1000
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    (r0, mine0, L0, eps0, flat0), (r1, mine1, L1, eps1, flat1) = res
-    assert torch.equal(flat0, flat1)  # every rank holds the same averaged gradient
-    assert sorted(mine0 + mine1) == list(range(8)) and abs(L0 - L1) <= 3
+    flat0 = res[0][4]
+    for r in res[1:]:
+        assert torch.equal(r[4], flat0)  # every rank holds the same summed gradient
+    assert sorted(sum((r[1] for r in res), [])) == list(range(8))
+    Ls = [r[2] for r in res]
+    assert max(Ls) - min(Ls) <= 9
     # global-batch gradient with the same per-row noise (eps rows follow their segment)
     F = 17
     cfg = O.default_cfg(F=F, H=16, Hdec=16, Hm=16, D=16, K=16)
@@ -85,15 +95,54 @@ def test_dp_two_ranks_equals_global_batch():
     seqs = _global_batch(F, [9, 8, 8, 7, 5, 5, 3, 2])
     # each rank's eps is per packed row; unpack per segment to rebuild the global packed eps
     per_seg = {}
-    for mine, eps in ((mine0, eps0), (mine1, eps1)):
+    for _, mine, _, eps, _ in res:
         b, order = _pack([seqs[i] for i in mine])
         segs = torch.nn.utils.rnn.unpack_sequence(torch.nn.utils.rnn.PackedSequence(eps, b["batch_sizes"]))
         for k, i in enumerate(order):
             per_seg[mine[i]] = segs[k]
     gb, gorder = _pack(seqs)
     geps = torch.nn.utils.rnn.pack_sequence([per_seg[i] for i in gorder]).data
-    # loss on the global batch with B = 8: mean of the two rank losses when B_r = 4 each
+    # loss on the global batch with B = 8 = the sum of the rank losses (each / 8)
     _, grads, _, _, _ = O.train_step(P, gb, cfg, dict(feat=None, eps=geps), 40, pretrain=True)
     gflat = torch.cat([v.reshape(-1) for v in grads.values()])
     err = (gflat - flat0).abs().max().item() / gflat.abs().max().item()
     assert err < 1e-5, err
+
+
+class _FakeLearner:
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+
+
+def test_shard_host_side_empty_and_unequal():
+    import learning
+    seqs = _global_batch(5, [6, 4, 3])
+    packed = torch.nn.utils.rnn.pack_sequence(seqs)
+    off = torch.nn.utils.rnn.pack_sequence([torch.tensor([0.0] * (len(s) - 1) + [1.0]) for s in seqs])
+    spk = torch.tensor([0, 1, 2])
+    shards = [learning.Learner._shard(_FakeLearner(r, 4), packed, off, spk) for r in range(4)]
+    assert shards[3] is None  # 3 segments over 4 ranks: rank 3 joins the all-reduce with zero gradients
+    got = sorted(int(s[2][0]) for s in shards[:3])
+    assert got == [0, 1, 2]
+    for s in shards[:3]:
+        assert int(s[0].batch_sizes[0]) == 1 and torch.equal(s[0].data, seqs[int(s[2][0])])
+
+
+def test_philox_keys_per_rank():
+    from modules import noise
+    noise.manual_seed(1234)
+    k0 = noise.get_state()["seed"]
+    assert k0 == 1234  # rank 0 = the single-device stream
+    keys = set()
+    for r in range(8):
+        noise.manual_seed(1234, rank=r)
+        keys.add(noise.get_state()["seed"])
+    assert len(keys) == 8 and k0 in keys
+    # a checkpoint's state (rank 0's) re-keys per rank on restore
+    noise.manual_seed(1234)
+    st = dict(noise.get_state(), offset=96)
+    noise.set_state(st, rank=3)
+    s3 = noise.get_state()
+    noise.manual_seed(1234, rank=3)
+    assert s3["seed"] == noise.get_state()["seed"] and s3["offset"] == 96
+    noise.manual_seed(1234)
