@@ -2,8 +2,7 @@
 """Times the library's GEMM routes at the c2 hot-path shapes (HIP events,
 median of 20 launches) -- the frame-parallel input projection / offset head
 (abcd_gemm_nt, both operands K-contiguous) and the weight gradients
-(abcd_gemm_tn, both K-major, K = packed frames).  Run once per routing
-setting, e.g. `ABCD_X6S=0 python scripts/gemm_shapes.py`."""
+(abcd_gemm_tn, both K-major, K = packed frames)."""
 import os
 import sys
 

@@ -46,11 +46,6 @@ def main():
     for _ in range(3):
         run()
     torch.cuda.synchronize()
-    lib.abcd_debug_local_wgs.restype = ctypes.c_int
-    lib.abcd_debug_local_wgs()
-    run()
-    torch.cuda.synchronize()
-    print(f"XCD-local workgroups in one step (4 launches x 256): {lib.abcd_debug_local_wgs()}")
     # which XCD each block of a 256-block grid lands on is not observable here
     grid = 256
     buf = torch.zeros(grid * T * 8, dtype=torch.int64, device=dev)

@@ -130,158 +130,6 @@ __global__ void slab_reduce_kernel(const float* slab, int Z, EpiArgs e) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// gemm_x6: C = A B^T on the bf16 matrix cores in split-fp32 (abcd_x6.h: each
-// fp32 operand = three bf16 pieces, six cross products, fp32 accumulation),
-// for the big frame-parallel GEMMs: the encoder input projection (K = F) and
-// the weight gradients (K = all packed frames).  WG tile 128 x 128, 4 waves
-// as 2 x 2 (64 x 64 each, 4 x 4 subtiles), K in 32-deep chunks.  Each chunk of
-// both operands is loaded from global memory once per workgroup, split into
-// its three bf16 planes ONCE, and stored in LDS as [plane][row][k] with an
-// 80-B row pitch (conflict-free 16-B writes and fragment reads); two stages
-// keep the next chunk's global loads in flight behind the MFMAs.
-//   KM operand (K-major, element (row, k) at p[k*ld + row]): a thread loads 8
-//     k of one row as 8 dwords (lanes on consecutive rows: 256-B segments);
-//   KC operand (element at p[row*ld + k]): a thread loads 8 k as 2 float4.
-// ---------------------------------------------------------------------------
-constexpr int X6T = 128, X6_PITCH = 40, X6_PLANE = X6T * X6_PITCH;  // bf16 units
-constexpr int X6_OPER = 3 * X6_PLANE;                               // one operand, one stage
-constexpr size_t X6_LDS = (size_t)2 * 2 * X6_OPER * 2;               // bytes: 2 stages x 2 operands
-
-// K-major operands (both, the weight-gradient shape): threads 0..127 stage A,
-// 128..255 stage B.  A thread owns 4 consecutive rows x 8 consecutive k of the
-// 128 x 32 chunk: 8 float4 loads (row-contiguous, 64-B segments across 4
-// lanes), a 4x8 register transpose, then per row one split8 and three 16-B
-// LDS writes.
-DEV void x6_gload_km(const float* __restrict__ p, long ld, int nrows, int K, int r0, int k0, f4 (&v)[8]) {
-  const int t = threadIdx.x & 127, rg = t & 31, kg = t >> 5;  // rows 4rg..4rg+3, k 8kg..8kg+7
-  const int row = r0 + 4 * rg, k = k0 + 8 * kg;
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const float* src = p + (long)(k + s) * ld + row;
-    if (k + s < K && row + 4 <= nrows) v[s] = *reinterpret_cast<const f4*>(src);
-    else {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[s][c] = (k + s < K && row + c < nrows) ? src[c] : 0.f;
-    }
-  }
-}
-DEV void x6_lstore_km(__bf16* st, const f4 (&v)[8]) {
-  const int t = threadIdx.x & 127, rg = t & 31, kg = t >> 5;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const f4 lo = {v[0][c], v[1][c], v[2][c], v[3][c]}, hi = {v[4][c], v[5][c], v[6][c], v[7][c]};
-    bf8 h, m, l;
-    split8(lo, hi, h, m, l);
-    __bf16* d = st + (4 * rg + c) * X6_PITCH + 8 * kg;
-    *reinterpret_cast<bf8*>(d) = h;
-    *reinterpret_cast<bf8*>(d + X6_PLANE) = m;
-    *reinterpret_cast<bf8*>(d + 2 * X6_PLANE) = l;
-  }
-}
-
-__global__ __launch_bounds__(256) void gemm_x6_kernel(const float* __restrict__ A, long lda, int nra,
-                                                      const float* __restrict__ B, long ldb, int nrb, int K, int kps,
-                                                      EpiArgs e) {
-  extern __shared__ __attribute__((aligned(16))) __bf16 xs[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
-  const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.y * X6T, n0 = blockIdx.x * X6T;
-  const int kb = blockIdx.z * kps, ke = min(K, kb + kps);
-  const int M = e.M, N = e.N;
-  // this thread's operand (wave-uniform): waves 0-1 stage A, waves 2-3 stage B
-  const bool isB = threadIdx.x >= 128;
-  const float* P = isB ? B : A;
-  const long ldp = isB ? ldb : lda;
-  const int nrp = isB ? nrb : nra, rp0 = isB ? n0 : m0;
-  f4 acc[4][4];
-  acc_zero(acc);
-  f4 v[8];
-  x6_gload_km(P, ldp, nrp, ke, rp0, kb, v);
-  x6_lstore_km(xs + (isB ? X6_OPER : 0), v);
-  __syncthreads();
-  int cur = 0;
-  for (int k0 = kb; k0 < ke; k0 += 32) {
-    const bool more = k0 + 32 < ke;
-    if (more) x6_gload_km(P, ldp, nrp, ke, rp0, k0 + 32, v);
-    const __bf16* sa = xs + cur * 2 * X6_OPER + (wm * 64 + r) * X6_PITCH + 8 * q;
-    const __bf16* sb = xs + cur * 2 * X6_OPER + X6_OPER + (wn * 64 + r) * X6_PITCH + 8 * q;
-    bf8 b[4][3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) b[j][pl] = *reinterpret_cast<const bf8*>(sb + 16 * j * X6_PITCH + pl * X6_PLANE);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf8 a[3];
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const bf8*>(sa + 16 * i * X6_PITCH + pl * X6_PLANE);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mma_x6(acc[i][j], a[0], a[1], a[2], b[j][0], b[j][1], b[j][2]);
-    }
-    if (more) x6_lstore_km(xs + (cur ^ 1) * 2 * X6_OPER + (isB ? X6_OPER : 0), v);
-    __syncthreads();
-    cur ^= 1;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int row = m0 + wm * 64 + 16 * i + 4 * q + g, col = n0 + wn * 64 + 16 * j + r;
-        if (row < M && col < N) {
-          if (e.slab)
-            e.slab[(long)blockIdx.z * M * N + (long)row * N + col] = acc[i][j][g];
-          else
-            e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, acc[i][j][g]);
-        }
-      }
-}
-
-// opt-in (ABCD_X6GEMM=1): measured on MI355X at the c2 weight-gradient shapes
-// (M = 4H, N = H or Fp, K = L ~ 64k) it is not faster than gemm_tn's fp32
-// MFMA path (300-335 us vs 305 / 200 us): one 120-KiB workgroup per CU leaves
-// too little latency hiding for the staged loads
-static bool lds_nt_disabled() {
-  const char* v = getenv("ABCD_LDSNT");
-  return v && v[0] == '0';
-}
-
-static bool x6_gemm_enabled() {
-  const char* v = getenv("ABCD_X6GEMM");
-  return v && v[0] == '1';
-}
-
-// C = A B^T through gemm_x6_kernel; K split over the grid (fp32 slabs) until
-// ~2 workgroups per CU are in flight
-static int gemm_x6(hipStream_t s, int M, int N, int K, const float* A, long lda, int nra, const float* B, long ldb,
-                   int nrb, EpiArgs e, float* scratch, size_t scratch_floats) {
-  static bool attr = false;
-  if (!attr) {
-    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)X6_LDS));
-    attr = true;
-  }
-  const int tiles = cdiv(M, X6T) * cdiv(N, X6T);
-  int Z = std::max(1, std::min(cdiv(512, tiles), cdiv(K, 32 * 16)));
-  if (scratch) Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)M * N)));
-  else Z = 1;
-  Z = std::max(Z, 1);
-  const int kps = ((cdiv(K, Z) + 31) / 32) * 32;
-  Z = cdiv(K, kps);
-  EpiArgs ek = e;
-  if (Z > 1) ek.slab = scratch;
-  gemm_x6_kernel<<<dim3(cdiv(N, X6T), cdiv(M, X6T), Z), 256, X6_LDS, s>>>(A, lda, nra, B, ldb, nrb, K, kps, ek);
-  ABCD_CHECK_LAUNCH();
-  if (Z > 1) {
-    const long n = (long)M * N;
-    slab_reduce_kernel<<<std::min<long>(2048, cdiv(n, 256)), 256, 0, s>>>(scratch, Z, e);
-    ABCD_CHECK_LAUNCH();
-  }
-  return 0;
-}
-
 template <class OA, class OB>
 static int gemm_launch(hipStream_t s, int M, int N, int K, OA A, OB B, EpiArgs e, float* scratch,
                        size_t scratch_floats) {
@@ -346,14 +194,6 @@ DEV dim3 xcd_tile(bool remap) {
   unsigned i = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
   if (remap && n % 8 == 0) i = (i % 8) * (n / 8) + i / 8;
   return dim3(i % gx, (i / gx) % gy, i / (gx * gy));
-}
-
-static int gxcd_remap() {
-  static const int v = [] {
-    const char* s = getenv("ABCD_GXCD");
-    return (s && s[0] == '0') ? 0 : 1;
-  }();
-  return v;
 }
 
 template <int MR, int NR, bool AKC = false, bool BKC = false>
@@ -504,7 +344,7 @@ static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, lo
   EpiArgs ek = e;
   if (Z > 1) ek.slab = scratch;
   gemm_tn_kernel<MR, NR, AKC, BKC><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek,
-                                                                                   gxcd_remap());
+                                                                                   1);
   ABCD_CHECK_LAUNCH();
   if (Z > 1) {
     const long n = (long)M * N;
@@ -696,7 +536,7 @@ static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, l
   EpiArgs ek = e;
   if (Z > 1) ek.slab = scratch;
   gemm_x6s_kernel<MR, NR, AKC, BKC><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek,
-                                                                                     gxcd_remap());
+                                                                                     1);
   ABCD_CHECK_LAUNCH();
   if (Z > 1) {
     const long n = (long)M * N;
@@ -706,11 +546,6 @@ static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, l
   return 0;
 }
 
-// split-fp32 GEMM routing (default on; ABCD_X6S=0 keeps the f32-MFMA kernels)
-static bool x6s_enabled() {
-  const char* v = getenv("ABCD_X6S");  // read per call: tests flip it in-process
-  return !(v && v[0] == '0');
-}
 
 // both operands K-major with 16-B aligned rows covering roundup(M|N, 4).
 // Tile: 128 rows x 32*NR columns covering N up to 256 per tile.
@@ -720,10 +555,9 @@ static int gemm_tn(hipStream_t s, int M, int N, int K, const Operand& A, const O
   // one 160-wide tile for N in (128, 160] (the decoder's dW_ih, N = F = 129)
   // instead of a second, nearly empty 128-wide one: 38 KB LDS, 142 VGPRs --
   // still one workgroup per CU beside enc_bwd_sk (98 KB, 258 registers)
-  const char* s5 = getenv("ABCD_SIDE5");
-  if (tl_side && N > 128 && N <= 160 && !(s5 && s5[0] == '0')) nr = 5;
+  if (tl_side && N > 128 && N <= 160) nr = 5;
   // the same along M (the emission MLPs' dW2, M = F = 129): one 160-row tile
-  if (tl_side && nr == 4 && M > 128 && M <= 160 && !(s5 && s5[0] == '0'))
+  if (tl_side && nr == 4 && M > 128 && M <= 160)
     return gemm_tn_launch<5, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
 #define TN_CASE(n) \
   case n: return gemm_tn_launch<4, n>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
@@ -752,8 +586,8 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
     // frame-parallel GEMMs (M = packed frames): LDS-staged tiles, 128 x 256 (measured
     // ~1.6x the direct-fragment gemm_big at the input-projection shape)
     if (cdiv(M, 128) * cdiv(N, 128) >= 240 && A.nrows >= M && B.nrows >= N && A.ld % 4 == 0 && B.ld % 4 == 0 &&
-        ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0 && !lds_nt_disabled()) {
-      if (x6s_enabled() && !tl_side) return gemm_x6s_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
+        ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0) {
+      if (!tl_side) return gemm_x6s_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
       if (N >= 256) return gemm_tn_launch<4, 8, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
       return gemm_tn_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
     }
@@ -766,18 +600,12 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
   if (!A.kmajor && B.kmajor)
     return gemm_launch(s, M, N, K, KC{A.p, A.ld, std::min(A.nrows, M)}, KM{B.p, B.ld, std::min(B.nrows, N), K}, e,
                        scratch, scratch_floats);
-  // weight gradients (K = packed frames): split-fp32 on the bf16 matrix cores
-  // when the output has enough tiles to fill the chip with little split-K
-  if (!tl_side && x6_gemm_enabled() && K >= 4096 && M >= 128 && N >= 128 && A.ld % 4 == 0 && B.ld % 4 == 0 &&
-      ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0)
-    return gemm_x6(s, M, N, K, A.p, A.ld, std::min(A.nrows, M), B.p, B.ld, std::min(B.nrows, N), e,
-                               scratch, scratch_floats);
   // gemm_tn for the frame-reduction shapes (K = packed frames); short K (the
   // batch-reduction weight gradients, K = B = 512) goes to gemm_ks, whose
   // 32 x 64 tiles and grid split-K fill the chip (gemm_tn's 128 x 256 tiles
   // leave ~16 workgroups: ~100-170 us per GEMM measured, vs ~10)
   if (K >= 4096 && A.nrows >= M && B.nrows >= N && tn_ok(A, M) && tn_ok(B, N)) {
-    if (x6s_enabled() && !tl_side) {  // 66-76 KB of LDS: not beside a persistent kernel
+    if (!tl_side) {  // 66-76 KB of LDS: not beside a persistent kernel
       if (N > 128 && N <= 160)  // one 160-wide tile (e.g. dW_ih, N = F = 129)
         return gemm_x6s_launch<4, 5, false, false>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
       return gemm_x6s_launch<4, 4, false, false>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);

@@ -23,8 +23,6 @@ struct PFwdDir {
   float *Hprev, *Cprev;          // stashes (Hprev is also the in-launch hand-off)
   float* out; long ldo; int hcol, ccol;  // final state (last_hidden), or null
   int rev;
-  // fused input projection (layer 0, NXC > 0): gates += X W_ih^T + b, X rows x ldx
-  const float *X, *Wih, *bih; long ldx;   // Wih: G*H x ldx (zero-padded), bih: b_ih (+ b_hh for LSTM)
 };
 struct PFwdArgs {
   PFwdDir d[2];
@@ -32,7 +30,6 @@ struct PFwdArgs {
   const int* off;    // device: off[0..T]
   unsigned* sync;    // one 128-B counter line per group, zeroed before the launch
   unsigned long long* prof;  // diagnostics: per-step s_memtime stamps, or null
-  int exp;           // diagnostics (ABCD_PEXP): 1 = recurrent operand reads zero, 2 = no recurrent MMA
 };
 
 // One direction of an encoder layer, backward (BPTT).
@@ -123,14 +120,7 @@ int flush_offsets();
 // (*launched = true); otherwise leave *launched = false (caller runs the
 // per-step kernels).  Returns 0 or a hipError_t.
 int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched);
-// the same with the input projection fused (PFwdDir::X/Wih/bih set; layer 0)
-int persist_encoder_fwd_fused(hipStream_t s, int G, const PFwdArgs& a, bool* launched);
-// zeroed (may be null): recorded on s between the counter reset and the launch
-// (split-K form only; with it set the gather form declines, *launched = false)
-int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched, hipEvent_t zeroed = nullptr);
-// on stream s: wait until the first ngroups group counters of a running
-// persistent launch reach target (call after waiting on its `zeroed` event)
-int gate_persist(hipStream_t s, const unsigned* sync, int ngroups, unsigned target);
+int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched);
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched);
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched);
 

@@ -40,7 +40,6 @@ namespace abcd {
 __device__ unsigned g_persist_status = 0;
 __device__ unsigned g_persist_sticky = 0;       // OR of every status abcd_step_status folded (abcd_device_status)
 __device__ unsigned g_spin_limit = 1u << 22;    // polls before a hand-off wait gives up (ABCD_SPIN_LIMIT, tests)
-__device__ unsigned g_local_wgs = 0;  // diagnostics: workgroups that ran in XCD-local mode
 
 // ---------------------------------------------------------------------------
 // hand-off primitives
@@ -161,7 +160,7 @@ DEV void flags_wait(const unsigned* fl, int M, unsigned epoch) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   __syncthreads();
 }
-// a group's hand-off in either form (flags unless ABCD_FLAGS=0 at launch)
+// a group's hand-off in either form (the launchers pick the per-member flags)
 struct GSync {
   unsigned *cnt, *fl;
   int M, mem, use_flags;
@@ -200,97 +199,31 @@ DEV void group_role(int bid, int ngroups, int nmem, int& grp, int& mem) {
   }
 }
 
-// XCD-local groups.  Every workgroup reads the XCD it actually runs on
-// (HW_REG_XCC_ID), takes a ticket on that XCD's counter, and waits until the
-// whole grid has registered.  If every XCD holds a multiple of nmem
-// workgroups, groups are formed INSIDE XCDs from the tickets ("local" mode):
-// all members of a group then share one L2, so hand-off payloads are stored
-// with plain stores (write-through L1 -> the shared L2, complete at the
-// producer's vmcnt(0) drain) and stay L2-resident for the consumers' L1-
-// bypassing sc1 loads, instead of being written through to the memory side
-// and re-fetched from it by every consumer (sc1 stores drop the L2 line).
-// Otherwise ("fallback" mode) roles come from group_role() and every
-// hand-off store is sc1 (write-through), which is correct under any
-// placement.  Registry: 8 ticket lines + 1 arrival line after the group
-// counters, zeroed with them before the launch.
+// Registry lines after the group counters (kept in the sync layout: 8 + 1
+// lines, zeroed with the counters).  Groups formed INSIDE XCDs from per-XCD
+// tickets, with plain (L2-resident) hand-off stores, measured slower than
+// write-through hand-offs on MI355X (c2: dec_bwd 4.63 vs 4.45 ms, enc_fwd 1.51
+// vs 1.47), so roles come from the block index (group_role) and every
+// hand-off store is write-through (sc1).
 constexpr int PERSIST_REG_LINES = 9;
 struct Role {
   int grp, mem;
-  bool local;
 };
-// `sh`: 3 ints of the kernel's dynamic LDS (no static LDS: the launchers
-// reserve the whole 160 KiB for the dynamic image); free again on return.
-DEV Role assign_role(unsigned* reg, int ngroups, int nmem, int* sh) {
-  if (threadIdx.x == 0) {
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-    xcc &= 7u;
-    const unsigned slot = __hip_atomic_fetch_add(reg + xcc * PERSIST_SYNC_STRIDE, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ticket performed before the arrival
-    unsigned* arrived = reg + 8 * PERSIST_SYNC_STRIDE;
-    __hip_atomic_fetch_add(arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    bool ok = true;
-    const unsigned lim = g_spin_limit;
-    while (__hip_atomic_load(arrived, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > lim) {
-        __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = false;
-        break;
-      }
-    }
-    int grp = 0, mem = 0, local = 0;
-    if (ok) {
-      int base = 0;
-      local = 1;
-      for (unsigned x = 0; x < 8; ++x) {
-        const int c = (int)__hip_atomic_load(reg + x * PERSIST_SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c % nmem) local = 0;
-        if (x < xcc) base += c / nmem;
-      }
-      if (local) {
-        grp = base + (int)slot / nmem;
-        mem = (int)slot % nmem;
-      }
-    }
-    if (!local) group_role(blockIdx.x, ngroups, nmem, grp, mem);
-    else __hip_atomic_fetch_add(&g_local_wgs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sh[0] = grp;
-    sh[1] = mem;
-    sh[2] = local;
-  }
-  __syncthreads();
+DEV Role assign_role(int ngroups, int nmem) {
   Role r;
-  r.grp = __builtin_amdgcn_readfirstlane(sh[0]);
-  r.mem = __builtin_amdgcn_readfirstlane(sh[1]);
-  r.local = __builtin_amdgcn_readfirstlane(sh[2]) != 0;
-  __syncthreads();
+  group_role(blockIdx.x, ngroups, nmem, r.grp, r.mem);
   return r;
 }
-// hand-off payload store: plain inside an XCD-local group, write-through otherwise
-DEV void st_ho(float* p, float v, bool local) {
-  if (local) *p = v;
-  else st_sc1(p, v);
-}
-
 // ---------------------------------------------------------------------------
 // encoder forward: one launch per layer, both directions
 // ---------------------------------------------------------------------------
 // X6 > 0: split-fp32 recurrent MMA with X6 = H / 32 chunks (abcd_x6.h).
-// NXC > 0 (with X6): the input projection x_t W_ih^T + b is fused too, over
-// NXC 32-deep chunks of the padded input row: W_ih's slice sits in LDS next
-// to W_hh's, the x rows of the NEXT step are prefetched into registers at the
-// end of each step, and the x6 MMA runs before the hand-off wait (it does not
-// depend on the recurrence) -- no L x 8H projection GEMM, no GX round trip.
-template <int G, int PD, int X6, int NXC = 0>
+template <int G, int PD, int X6>
 __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, nut = H / 16, nch = H / 16, T = a.T;
-  const Role role = assign_role(a.sync + a.nd * a.nrt * PERSIST_SYNC_STRIDE, a.nd * a.nrt, nut, (int*)smem);
+  const Role role = assign_role(a.nd * a.nrt, nut);
   const int grp = role.grp, mem = role.mem;
-  const bool loc = role.local;
   const int dir = grp / a.nrt, rt = grp % a.nrt;
   const PFwdDir& D = a.d[dir];
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
@@ -300,50 +233,12 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
   unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
   if (X6) stage_x6(smem, D.Whh, H, H, G, H / 32, 0, H / 32, [&](int j, int rr) { return j * H + u0 + rr; });
   else stage_b_frag(smem, D.Whh, H, G, nch, [&](int j) { return j * H + u0; });
-  f4* Bx = smem + (size_t)G * (X6 > 0 ? X6 : 1) * 3 * 64;  // W_ih slice (NXC > 0)
-  if (NXC) stage_x6(Bx, D.Wih, D.ldx, (int)D.ldx, G, NXC, 0, NXC, [&](int j, int rr) { return j * H + u0 + rr; });
-  float bh[G], bx[G];
+  float bh[G];
 #pragma unroll
-  for (int j = 0; j < G; ++j) {
-    bh[j] = (G == 3) ? D.bhh[j * H + unit] : 0.f;
-    bx[j] = NXC ? D.bih[j * H + unit] : 0.f;
-  }
+  for (int j = 0; j < G; ++j) bh[j] = (G == 3) ? D.bhh[j * H + unit] : 0.f;
   __syncthreads();
   float st[4] = {0.f, 0.f, 0.f, 0.f};  // c (LSTM) / h (GRU) of the lane's 4 cells
   const int* off = a.off;
-  // x rows of a step for the fused projection: lane (r, q) holds k = 32c + 8q + 0..7 of row row0 + r
-  f4 xa[NXC > 0 ? NXC : 1][2];
-  auto load_x = [&](int ii) {
-    const int tt = D.rev ? T - 1 - ii : ii;
-    const int oo = off[tt], bb = off[tt + 1] - oo;
-    const BufKC X{make_rsrc(D.X + (size_t)oo * D.ldx, (uint32_t)(bb * D.ldx * 4)), (uint32_t)(D.ldx * 4)};
-#pragma unroll
-    for (int c = 0; c < (NXC > 0 ? NXC : 1); ++c) X.frag8(row0 + r, c, q, xa[c][0], xa[c][1]);
-  };
-  f4 ax[G];  // x projection of the current step (NXC > 0)
-  auto project_x = [&](int ii) {
-    const int tt = D.rev ? T - 1 - ii : ii;
-    const int bb = off[tt + 1] - off[tt];
-#pragma unroll
-    for (int j = 0; j < G; ++j) ax[j] = f4zero();
-    if (row0 < bb) {
-#pragma unroll
-      for (int c = 0; c < (NXC > 0 ? NXC : 1); ++c) {
-        bf8 a0, a1, a2;
-        split8(xa[c][0], xa[c][1], a0, a1, a2);
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const f4* bp = Bx + ((j * NXC + c) * 3) * 64 + lane;
-          ax[j] = mma_x6(ax[j], a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
-                         __builtin_bit_cast(bf8, bp[128]));
-        }
-      }
-    }
-  };
-  if (NXC) {
-    load_x(0);
-    project_x(0);
-  }
   for (int i = 0; i < T; ++i) {
     const int t = D.rev ? T - 1 - i : i;
     const int o = off[t], bs = off[t + 1] - o;
@@ -358,33 +253,23 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
       next_bs = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
     }
     PSTAMP(0);
-    // input projection of this step (independent of the recurrence: issued
+    // input projection of this step (independent of the recurrence: loaded
     // before the wait so its latency hides behind it)
     float gxp[4][G];
-    if (NXC) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const bool live = row0 + 4 * q + g < bs;
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+      const bool live = b < bs;
+      const long rr = o + (live ? b : 0);
 #pragma unroll
-        for (int j = 0; j < G; ++j) gxp[g][j] = live ? ax[j][g] + bx[j] : 0.f;
-      }
-      if (i + 1 < T) load_x(i + 1);  // next step's x rows: in flight across this step's wait and MMA
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int b = row0 + 4 * q + g;
-        const bool live = b < bs;
-        const long rr = o + (live ? b : 0);
-#pragma unroll
-        for (int j = 0; j < G; ++j) gxp[g][j] = live ? D.GX[rr * D.ldgx + j * H + unit] : 0.f;
-      }
+      for (int j = 0; j < G; ++j) gxp[g][j] = live ? D.GX[rr * D.ldgx + j * H + unit] : 0.f;
     }
     if (i > 0) group_wait(cnt, (unsigned)(nut * i));
     PSTAMP(1);
     f4 acc[2][G];
     acc2_zero(acc);
-    if (row0 < bs && prev_valid > 0 && !(a.exp & 2)) {
-      const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (a.exp & 1) ? 0u : (uint32_t)prev_valid * H * 4u),
+    if (row0 < bs && prev_valid > 0) {
+      const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u),
                     (uint32_t)H * 4u};
       if (X6) {
         wave_mma_x6<G, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q);
@@ -419,11 +304,10 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
         cv[g] = 0.f;
         st[g] = hv[g];
       }
-      if (b < bs && b < next_bs) st_ho(D.Hprev + (long)(next_off + b) * H + unit, hv[g], loc);
+      if (b < bs && b < next_bs) st_sc1(D.Hprev + (long)(next_off + b) * H + unit, hv[g]);
     }
     PSTAMP(3);
     group_publish(cnt);
-    if (NXC && i + 1 < T) project_x(i + 1);  // next step's projection, off the hand-off path
     // pass 2: stashes for the backward pass and the outputs (plain stores,
     // drained while the next step waits for its operand)
 #pragma unroll
@@ -459,9 +343,8 @@ template <int G, int PD, int X6>
 __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, GH = G * H, nut = H / 16, nchg = GH / 16, T = a.T;
-  const Role role = assign_role(a.sync + a.nd * a.nrt * PERSIST_SYNC_STRIDE, a.nd * a.nrt, nut, (int*)smem);
+  const Role role = assign_role(a.nd * a.nrt, nut);
   const int grp = role.grp, mem = role.mem;
-  const bool loc = role.local;
   const int dir = grp / a.nrt, rt = grp % a.nrt;
   const PBwdDir& D = a.d[dir];
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
@@ -537,10 +420,10 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
         const float tc = ftanh(pc[g]);
         const float dc = (fin ? pdc[g] : carry[g]) + dh * o_ * (1.f - tc * tc);
         float* dg = D.dGX + rr * GH;
-        st_ho(dg + unit, dc * g_ * i_ * (1.f - i_), loc);
-        st_ho(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_), loc);
-        st_ho(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_), loc);
-        st_ho(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_), loc);
+        st_sc1(dg + unit, dc * g_ * i_ * (1.f - i_));
+        st_sc1(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_));
+        st_sc1(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_));
+        st_sc1(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_));
         carry[g] = dc * f_;
       } else {
         if (!fin) dh += carry[g];
@@ -552,7 +435,7 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
         float* dx = D.dGX + rr * GH;
         float* dhh = D.dGH + rr * GH;
         dx[unit] = drp; dx[H + unit] = dzp; dx[2 * H + unit] = dnp;
-        st_ho(dhh + unit, drp, loc); st_ho(dhh + H + unit, dzp, loc); st_ho(dhh + 2 * H + unit, dnp * r_, loc);
+        st_sc1(dhh + unit, drp); st_sc1(dhh + H + unit, dzp); st_sc1(dhh + 2 * H + unit, dnp * r_);
         carry[g] = dh * z_;
       }
     }
@@ -588,9 +471,8 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   constexpr int H = NSUB * 16, GH = G * H, nut = NSUB;
   const int T = a.T, ng = a.nd * a.nrt;
-  const Role role = assign_role(a.sync + ng * PERSIST_SYNC_STRIDE, ng, nut, (int*)smem);
+  const Role role = assign_role(ng, nut);
   const int grp = role.grp, mem = role.mem;
-  const bool loc = role.local;
   const int dir = grp / a.nrt, rt = grp % a.nrt;
   const PBwdDir& D = a.d[dir];
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
@@ -743,10 +625,8 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
     }
     PSTAMP(3);
     group_publish(cnt);
-    // stashes for the weight-gradient GEMMs, after the publish; write-through
-    // (sc1) so that a gated GEMM running beside this launch (abcd_encoder_
-    // backward_overlap) reads them from memory once the NEXT publish -- whose
-    // vmcnt(0) drains them -- has been counted
+    // stashes for the weight-gradient GEMMs after the launch (plain stores,
+    // after the publish)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int b = row0 + 4 * q + g;
@@ -754,15 +634,14 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
       const long rr = o + b;
       float* dx = D.dGX + rr * GH;
 #pragma unroll
-      for (int j = 0; j < G; ++j) st_sc1(dx + j * H + unit, dgx[g][j]);
+      for (int j = 0; j < G; ++j) dx[j * H + unit] = dgx[g][j];
       if (G == 3) {
         float* dhh = D.dGH + rr * GH;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) st_sc1(dhh + j * H + unit, dgh[g][j]);
+        for (int j = 0; j < 3; ++j) dhh[j * H + unit] = dgh[g][j];
       }
     }
     PSTAMP(4);
-    (void)loc;
   }
 }
 
@@ -832,9 +711,8 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
   const int M = H / 8, nchx = a.feedback ? Fp / 16 : 0, nchh = H / 16, nchm = Hm / 16, nchc = nchx + nchh;
   const int nx32 = a.feedback ? (Fp + 31) / 32 : 0;  // x6: chunks of x
   const int n1t = 2 * Hm / 16, n2t = Fp / 16;
-  const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
+  const Role role = assign_role(a.nrt, M);
   const int grp = role.grp, mem = role.mem;
-  const bool loc = role.local;
   const int rt = grp;
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -914,8 +792,8 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
       hv[g] = go[g] * ftanh(cst[g]);
       const int b = row0 + 4 * q + g;
       if (b < bs) {
-        if (lo) st_ho(a.Hs + (long)(o + b) * H + unit, hv[g], loc);                       // -> mlp
-        else if (b < next_bs) st_ho(a.Hprev + (long)(next_off + b) * H + unit, hv[g], loc);  // -> next cell
+        if (lo) st_sc1(a.Hs + (long)(o + b) * H + unit, hv[g]);                       // -> mlp
+        else if (b < next_bs) st_sc1(a.Hprev + (long)(next_off + b) * H + unit, hv[g]);  // -> next cell
       }
     }
     group_publish(cnt);
@@ -952,7 +830,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int b = row0 + 4 * q + g;
-        if (b < bs) st_ho(a.Aact + (long)(o + b) * 2 * Hm + col, ftanh(acc1[0][0][g] + bb), loc);
+        if (b < bs) st_sc1(a.Aact + (long)(o + b) * 2 * Hm + col, ftanh(acc1[0][0][g] + bb));
       }
     }
     group_publish(cnt);
@@ -1006,7 +884,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
         }
         if (b < bs && a.feedback && b < next_bs) {
           const float m = k == 0 ? mpre[g] : ((a.xmask && col < F) ? a.xmask[(long)(next_off + b) * F + col] : 1.f);
-          st_ho(a.Xin + (long)(next_off + b) * Fp + col, x * m, loc);
+          st_sc1(a.Xin + (long)(next_off + b) * Fp + col, x * m);
         }
         if (k == 0) {
           mu0[g] = mu; lv0[g] = lv; x0[g] = x;
@@ -1062,9 +940,8 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   const int M = H / 8;
   const int nx32 = a.feedback ? (Fp + 31) / 32 : 0;
   const int n1t = 2 * Hm / 16, n2t = Fp / 16;
-  const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
+  const Role role = assign_role(a.nrt, M);
   const int grp = role.grp, mem = role.mem;
-  const bool loc = role.local;
   const int rt = grp;
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1156,8 +1033,8 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       }
       const int b = row0 + 4 * q + g;
       if (b < bs) {
-        if (lo) st_ho(a.Hs + (long)(o + b) * H + unit, hv[g], loc);                       // -> mlp
-        else if (b < next_bs) st_ho(a.Hprev + (long)(next_off + b) * H + unit, hv[g], loc);  // -> next cell
+        if (lo) st_sc1(a.Hs + (long)(o + b) * H + unit, hv[g]);                       // -> mlp
+        else if (b < next_bs) st_sc1(a.Hprev + (long)(next_off + b) * H + unit, hv[g]);  // -> next cell
       }
     }
     gs.publish();
@@ -1198,7 +1075,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int b = row0 + 4 * q + g;
-        if (b < bs) st_ho(a.Aact + (long)(o + b) * 2 * Hm + 16 * mem + r, ftanh(a1[0][g] + b1v), loc);
+        if (b < bs) st_sc1(a.Aact + (long)(o + b) * 2 * Hm + 16 * mem + r, ftanh(a1[0][g] + b1v));
       }
     }
     gs.publish();
@@ -1242,7 +1119,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         const float lv = LVX[((w & 1) * 16 + 4 * q + g) * 16 + r];
         const float x = col2 < F ? ev[g] + __expf(0.5f * lv) * epre[g] : 0.f;
         epre[g] = x;
-        if (b < bs && a.feedback && b < next_bs) st_ho(a.Xin + (long)(next_off + b) * Fp + col2, x * mpre[g], loc);
+        if (b < bs && a.feedback && b < next_bs) st_sc1(a.Xin + (long)(next_off + b) * Fp + col2, x * mpre[g]);
       }
     }
     gs.publish();
@@ -1276,9 +1153,8 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T, GH = 4 * H;
   const int M = H / 8, nchg = GH / 16, nchx = Fp / 16, nchz = 2 * Hm / 16;
   const int nFt = Fp / 16, n0t = nFt + H / 16, n1t = 2 * Hm / 16, n2t = H / 16;
-  const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
+  const Role role = assign_role(a.nrt, M);
   const int grp = role.grp, mem = role.mem;
-  const bool loc = role.local;
   const int rt = grp;
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1341,10 +1217,10 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
             dmu = dx + s_em * (-d) * iv;
             dlv = dx * 0.5f * (ox - mu) + s_em * 0.5f * (1.f - d * d * iv);
           }
-          st_ho(a.dMU + rr * Fp + col, dmu, loc);
-          st_ho(a.dLV + rr * Fp + col, dlv, loc);
+          st_sc1(a.dMU + rr * Fp + col, dmu);
+          st_sc1(a.dLV + rr * Fp + col, dlv);
         } else {
-          st_ho(a.DHR + rr * H + 16 * (j0 - nFt) + r, acc[0][0][g], loc);
+          st_sc1(a.DHR + rr * H + 16 * (j0 - nFt) + r, acc[0][0][g]);
         }
       }
     }
@@ -1380,7 +1256,7 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
         if (b >= bs) continue;
         const long rr = o + b;
         const float z = k == 0 ? zpre[g] : a.Aact[rr * 2 * Hm + col];
-        st_ho(a.dZ + rr * 2 * Hm + col, acc[0][0][g] * (1.f - z * z), loc);
+        st_sc1(a.dZ + rr * 2 * Hm + col, acc[0][0][g] * (1.f - z * z));
       }
     }
     group_publish(cnt);
@@ -1427,10 +1303,10 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
         const float tc = ftanh(pc[g]);
         const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
         float* dg = a.dG + rr * GH;
-        st_ho(dg + unit, dc * g_ * i_ * (1.f - i_), loc);
-        st_ho(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_), loc);
-        st_ho(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_), loc);
-        st_ho(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_), loc);
+        st_sc1(dg + unit, dc * g_ * i_ * (1.f - i_));
+        st_sc1(dg + H + unit, dc * pcp[g] * f_ * (1.f - f_));
+        st_sc1(dg + 2 * H + unit, dc * i_ * (1.f - g_ * g_));
+        st_sc1(dg + 3 * H + unit, dh * tc * o_ * (1.f - o_));
         carry[g] = dc * f_;
         if (t == 0) a.DC0[(long)b * H + unit] = dc * f_;
       }
@@ -1490,9 +1366,8 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
   constexpr int H = NHS * 16, GH = (GRU ? 3 : 4) * H, M = H / 8, NS = NXS + NHS;
   const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
   const int nchx = Fp / 16, nFt = Fp / 16;
-  const Role role = assign_role(a.sync + a.nrt * PERSIST_SYNC_STRIDE, a.nrt, M, (int*)smem);
+  const Role role = assign_role(a.nrt, M);
   const int grp = role.grp, mem = role.mem;
-  const bool loc = role.local;
   const int rt = grp;
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1583,8 +1458,8 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
           dmu = dxv + s_em * (-d) * iv;
           dlv = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);
         }
-        st_ho(a.dMU + rr * Fp + col0, dmu, loc);
-        st_ho(a.dLV + rr * Fp + col0, dlv, loc);
+        st_sc1(a.dMU + rr * Fp + col0, dmu);
+        st_sc1(a.dLV + rr * Fp + col0, dlv);
       }
     }
     gs.publish();
@@ -1625,7 +1500,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       for (int g = 0; g < 4; ++g) {
         const int b = row0 + 4 * q + g;
         if (b >= bs) continue;
-        st_ho(a.dZ + (long)(o + b) * 2 * Hm + 16 * mem + r, acc[0][0][g] * (1.f - zpre[g] * zpre[g]), loc);
+        st_sc1(a.dZ + (long)(o + b) * 2 * Hm + 16 * mem + r, acc[0][0][g] * (1.f - zpre[g] * zpre[g]));
       }
     }
     gs.publish();
@@ -1854,21 +1729,14 @@ static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
   return 0;
 }
 
-// zero the group counters and the role registry.  XCD-local mode is opt-in
-// (ABCD_XCD=1): measured on MI355X it is SLOWER than write-through hand-offs
-// (c2 step 19.05 vs 18.47 ms; the encoder's recurrent MMA 8.7k vs 7.8k
-// cycles per step), so by default XCD 0's ticket count is pre-loaded with 1,
-// the grid never looks evenly spread and every workgroup takes the fallback
-// roles with sc1 hand-off stores.
-// One launch: every sync word zeroed, XCD 0's ticket pre-loaded (unless
-// ABCD_XCD=1) and, when a staged offset table is pending on s, that table
-// read from its pinned host slot into device memory.
-__global__ __launch_bounds__(256) void persist_reset(unsigned* sync, long nwords, long ticket, const int* off_src,
+// One launch before each persistent kernel: every sync word zeroed and, when
+// a staged offset table is pending on s, that table read from its pinned host
+// slot into device memory.
+__global__ __launch_bounds__(256) void persist_reset(unsigned* sync, long nwords, const int* off_src,
                                                      int* off_dst, int noff) {
   const long i0 = (long)blockIdx.x * 256 + threadIdx.x, stride = (long)gridDim.x * 256;
   for (long i = i0; i < nwords / 4; i += stride) {
     uint4 z = make_uint4(0u, 0u, 0u, 0u);
-    if (i == ticket / 4) z.x = 1u;  // ticket is a multiple of PERSIST_SYNC_STRIDE (-1: none)
     reinterpret_cast<uint4*>(sync)[i] = z;
   }
   for (long i = i0; i < noff; i += stride) off_dst[i] = off_src[i];
@@ -1892,13 +1760,11 @@ static int sync_spin_limit(hipStream_t s) {
 static int zero_sync_impl(hipStream_t s, unsigned* sync, int ngroups) {
   ABCD_TRY((hipError_t)sync_spin_limit(s));
   const long nwords = (long)(2 * ngroups + PERSIST_REG_LINES + PERSIST_FLAG_LINES * ngroups) * PERSIST_SYNC_STRIDE;
-  const char* v = getenv("ABCD_XCD");
-  const long ticket = (v && v[0] == '1') ? -1 : (long)ngroups * PERSIST_SYNC_STRIDE;
   const bool take = g_pend.on && g_pend.s == s;
   const int* src = nullptr;
   if (take) ABCD_TRY(hipHostGetDevicePointer((void**)&src, (void*)g_pend.src, 0));
   const int blocks = (int)std::min<long>(64, std::max<long>(1, (nwords / 4 + 255) / 256));
-  persist_reset<<<blocks, 256, 0, s>>>(sync, nwords, ticket, src, take ? g_pend.dst : nullptr, take ? g_pend.n : 0);
+  persist_reset<<<blocks, 256, 0, s>>>(sync, nwords, src, take ? g_pend.dst : nullptr, take ? g_pend.n : 0);
   ABCD_TRY(hipGetLastError());
   if (take) {
     g_pend.on = false;
@@ -1910,39 +1776,28 @@ static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
   return (hipError_t)zero_sync_impl(s, sync, ngroups);
 }
 
-// per-member flag hand-offs unless ABCD_FLAGS=0 (then the group counter)
-static int flags_enabled() {
-  const char* v = getenv("ABCD_FLAGS");
-  return (v && v[0] == '0') ? 0 : 1;
-}
 
 // ring depth: the largest of 16 / 4 / 1 dividing the chunk count
 static int ring_depth(int nch) { return nch % 16 == 0 ? 16 : (nch % 4 == 0 ? 4 : 1); }
 
-// x6 (split-fp32 on the bf16 matrix cores) unless ABCD_X6=0 or the shape
-// is not one of the compiled chunk counts
-static bool x6_enabled(int K) {
-  const char* v = getenv("ABCD_X6");
-  return (K == 64 || K == 128 || K == 256) && !(v && v[0] == '0');
-}
+// x6 (split-fp32 on the bf16 matrix cores) for the compiled chunk counts
+static bool x6_enabled(int K) { return K == 64 || K == 128 || K == 256; }
 
-template <int G, int PD, int X6, int NXC = 0>
+template <int G, int PD, int X6>
 static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * (a.H / 16);
-  const size_t lds = (size_t)G * 16 * a.H * (X6 ? 6 : 4) + (size_t)G * NXC * 3 * 64 * 16;
+  const size_t lds = (size_t)G * 16 * a.H * (X6 ? 6 : 4);
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD, X6, NXC>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD, X6>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PFwdArgs b = a;
   b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
-  const char* ex = getenv("ABCD_PEXP");
-  b.exp = ex ? atoi(ex) : 0;
   {
     TimedScope ts(s, TK_ENC_FWD);
-    enc_fwd_persist<G, PD, X6, NXC><<<grid, 256, lds, s>>>(b);
+    enc_fwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_ENC_FWD, "enc_fwd_persist<%d,%d,%d,%d> grid %d", G, PD, X6, NXC, grid);
+  note_dispatch(TK_ENC_FWD, "enc_fwd_persist<%d,%d,%d> grid %d", G, PD, X6, grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -1974,26 +1829,6 @@ static int launch_fwd_x6(hipStream_t s, const PFwdArgs& a, bool* launched) {
   return launch_fwd<G, 16, 8>(s, a, launched);
 }
 
-// fused input projection (layer 0): H = 256, x6, padded input width <= 160.
-// Opt-in (ABCD_FUSEX=1): measured on MI355X at c2 the fused launch takes
-// ~0.68 ms longer than the unfused one (W_ih's slice fills the LDS next to
-// W_hh's and the extra x6 work sits on the step's critical path), about what
-// the 0.6 ms projection GEMM it replaces costs.
-int persist_encoder_fwd_fused(hipStream_t s, int G, const PFwdArgs& a, bool* launched) {
-  *launched = false;
-  const char* v = getenv("ABCD_FUSEX");
-  if (!persist_enabled() || !(v && v[0] == '1') || !x6_enabled(a.H) || a.H != 256 || !a.d[0].X) return 0;
-  const int nxc = (int)((a.d[0].ldx + 31) / 32);
-  if (G == 4) {
-    if (nxc == 5) return launch_fwd<4, 16, 8, 5>(s, a, launched);
-    if (nxc == 3) return launch_fwd<4, 16, 8, 3>(s, a, launched);
-  } else {
-    if (nxc == 5) return launch_fwd<3, 16, 8, 5>(s, a, launched);
-    if (nxc == 3) return launch_fwd<3, 16, 8, 3>(s, a, launched);
-  }
-  return 0;
-}
-
 int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled()) return 0;
@@ -2010,14 +1845,13 @@ int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched)
 }
 
 template <int G, int NSUB>
-static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched, hipEvent_t zeroed) {
+static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * NSUB;
   const size_t lds = (size_t)NSUB * 2 * 3 * 64 * 16 + (size_t)4 * 16 * SK_PITCH * 4;
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(enc_bwd_sk<G, NSUB>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
-  if (zeroed) ABCD_TRY(hipEventRecord(zeroed, s));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
@@ -2030,51 +1864,20 @@ static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched, hipEv
   return 0;
 }
 
-// split-K form unless ABCD_SPLITK=0 (then the gather form)
-static bool splitk_enabled() {
-  const char* v = getenv("ABCD_SPLITK");
-  return !(v && v[0] == '0');
-}
 
-// gate for work queued beside a persistent launch: one wave polls the first
-// `ngroups` group counters (sc1 loads) until each reaches `target` (bounded)
-__global__ void gate_counters(const unsigned* sync, int ngroups, unsigned target) {
-  const int lane = threadIdx.x;
-  unsigned spins = 0;
-  const unsigned lim = g_spin_limit;
-  for (;;) {
-    bool ok = true;
-    if (lane < ngroups)
-      ok = __hip_atomic_load(sync + lane * PERSIST_SYNC_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
-    if (__all(ok)) break;
-    __builtin_amdgcn_s_sleep(8);
-    if (++spins > lim) {
-      if (lane == 0) __hip_atomic_store(&g_persist_status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-  }
-}
-int gate_persist(hipStream_t s, const unsigned* sync, int ngroups, unsigned target) {
-  if (ngroups > 64) return (int)hipErrorInvalidValue;
-  gate_counters<<<1, 64, 0, s>>>(sync, ngroups, target);
-  ABCD_CHECK_LAUNCH();
-  return 0;
-}
-
-int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched, hipEvent_t zeroed) {
+int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled()) return 0;
-  if (x6_enabled(a.H) && a.part && splitk_enabled()) {
+  if (x6_enabled(a.H) && a.part) {
     if (G == 4) {
-      if (a.H == 64) return launch_bwd_sk<4, 4>(s, a, launched, zeroed);
-      if (a.H == 128) return launch_bwd_sk<4, 8>(s, a, launched, zeroed);
-      return launch_bwd_sk<4, 16>(s, a, launched, zeroed);
+      if (a.H == 64) return launch_bwd_sk<4, 4>(s, a, launched);
+      if (a.H == 128) return launch_bwd_sk<4, 8>(s, a, launched);
+      return launch_bwd_sk<4, 16>(s, a, launched);
     }
-    if (a.H == 64) return launch_bwd_sk<3, 4>(s, a, launched, zeroed);
-    if (a.H == 128) return launch_bwd_sk<3, 8>(s, a, launched, zeroed);
-    return launch_bwd_sk<3, 16>(s, a, launched, zeroed);
+    if (a.H == 64) return launch_bwd_sk<3, 4>(s, a, launched);
+    if (a.H == 128) return launch_bwd_sk<3, 8>(s, a, launched);
+    return launch_bwd_sk<3, 16>(s, a, launched);
   }
-  if (zeroed) return 0;  // the gather-form kernels keep plain stash stores: no gated overlap
   if (x6_enabled(a.H)) {
     if (G == 4) {
       if (a.H == 64) return launch_bwd<4, 16, 8>(s, a, launched);
@@ -2109,7 +1912,7 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
-  b.flags = flags_enabled();
+  b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
@@ -2131,7 +1934,7 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
-  b.flags = flags_enabled();
+  b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
@@ -2146,17 +1949,14 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
 
 template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
-  const char* hp = getenv("ABCD_DECHPRE");
-  if (hp && hp[0] == '0') return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, false>(s, a, launched);
   return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true>(s, a, launched);
 }
 
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled() || a.H % 8) return 0;
-  const char* v6 = getenv("ABCD_DECX6");
   if (G == 3) {  // GRU: the all-x6 form only (a.bias = [b_r | b_z | b_in | b_hn])
-    if (!(x6_enabled(a.H) && a.H == 256 && a.Hm == 256 && 2 * (a.Fp / 16) <= a.H / 8) || (v6 && v6[0] == '0'))
+    if (!(x6_enabled(a.H) && a.H == 256 && a.Hm == 256 && 2 * (a.Fp / 16) <= a.H / 8))
       return 0;
     const int ncc = (a.feedback ? cdiv(a.Fp, 32) : 0) + a.H / 32;
     if (ncc == 13) return launch_dec_fwd_x6<13, 8, 8, true>(s, a, launched);
@@ -2166,7 +1966,7 @@ int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launch
   }
   if (G != 4) return 0;
   // all-x6 form: H = Hm = 256 (one mlp tile per member), 2 Fp/16 emit members
-  if (x6_enabled(a.H) && a.H == 256 && a.Hm == 256 && 2 * (a.Fp / 16) <= a.H / 8 && !(v6 && v6[0] == '0')) {
+  if (x6_enabled(a.H) && a.H == 256 && a.Hm == 256 && 2 * (a.Fp / 16) <= a.H / 8) {
     const int ncc = (a.feedback ? cdiv(a.Fp, 32) : 0) + a.H / 32;
     if (ncc == 13) return launch_dec_fwd_x6<13, 8, 8>(s, a, launched);
     if (ncc == 11) return launch_dec_fwd_x6<11, 8, 8>(s, a, launched);
@@ -2191,7 +1991,7 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
-  b.flags = flags_enabled();
+  b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
@@ -2207,7 +2007,7 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   *launched = false;
   if (!persist_enabled() || a.H % 8) return 0;
   if (G == 3) {  // GRU: the split-K form only
-    if (!(a.part && a.Hprev && a.dGH && x6_enabled(a.H) && splitk_enabled() && a.H == 256 && a.Hm == a.H &&
+    if (!(a.part && a.Hprev && a.dGH && x6_enabled(a.H) && a.H == 256 && a.Hm == a.H &&
           a.Fp / 16 <= a.H / 8))
       return 0;
     const int nxs = a.feedback ? a.Fp / 16 : 0;
@@ -2218,7 +2018,7 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   }
   if (G != 4) return 0;
   // split-K form: H = 256 (32 members), 2Hm/16 == members, Fp/16 <= members
-  if (a.part && x6_enabled(a.H) && splitk_enabled() && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8) {
+  if (a.part && x6_enabled(a.H) && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8) {
     const int nxs = a.feedback ? a.Fp / 16 : 0;
     if (nxs == 9) return launch_dec_bwd_sk<9, 16, 16>(s, a, launched);
     if (nxs == 5) return launch_dec_bwd_sk<5, 16, 16>(s, a, launched);
@@ -2233,7 +2033,7 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
-  b.flags = flags_enabled();
+  b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
@@ -2286,11 +2086,3 @@ extern "C" int abcd_device_status(void) {
   return (int)(v | w);
 }
 
-// diagnostics only: number of persistent workgroups that ran in XCD-local
-// mode since the last call (synchronises the device; resets the count)
-extern "C" int abcd_debug_local_wgs(void) {
-  unsigned v = 0, z = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(abcd::g_local_wgs), sizeof(v)) != hipSuccess) return -1;
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(abcd::g_local_wgs), &z, sizeof(z));
-  return (int)v;
-}

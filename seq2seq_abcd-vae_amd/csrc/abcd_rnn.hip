@@ -38,18 +38,6 @@ int validate_batch(const int64_t* bs, int T, int L, int B) {
   return s == L ? 0 : ABCD_EINVAL;
 }
 
-// diagnostic ablation mask for the recurrent step kernels (ABCD_DIAG env var,
-// timing experiments only; 0 in normal runs): 1 skip GEMM, 2 skip LDS reduce,
-// 4 skip epilogue
-static int diag_mask() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("ABCD_DIAG");
-    m = e ? atoi(e) : 0;
-  }
-  return m;
-}
-
 static std::vector<int> step_offsets(const int64_t* bs, int T) {
   std::vector<int> off(T + 1, 0);
   for (int t = 0; t < T; ++t) off[t + 1] = off[t] + (int)bs[t];
@@ -70,7 +58,7 @@ struct FwdDir {
   float* out; long ldo; int hcol, ccol;       // encoder final state (last_hidden)
   int off, bs, next_off, next_bs, tiles;
 };
-struct FwdArgs { FwdDir d[2]; int H; int nd; int diag; };
+struct FwdArgs { FwdDir d[2]; int H; int nd; };
 
 template <int G>
 __global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
@@ -109,17 +97,17 @@ __global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
 #pragma unroll
   for (int j = 0; j < G; ++j) br[j] = j * H + ut * 16 + r;
   const int nchh = H / 16;
-  if (!(a.diag & 1)) wave_mma<1, G>(accH, KC{D.Ah, H, D.prev_valid}, ar, KC{D.Whh, H, G * H}, br, w, nchh, 4, q);
-  if (D.xrows > 0 && !(a.diag & 1))
+  wave_mma<1, G>(accH, KC{D.Ah, H, D.prev_valid}, ar, KC{D.Whh, H, G * H}, br, w, nchh, 4, q);
+  if (D.xrows > 0)
     wave_mma<1, G>(accX, KC{D.Ax, D.ldx, D.xrows}, ar, KC{D.Wih, D.ldwih, G * H}, br, first_chunk(w, nchh),
                    D.nchx, 4, q);
-  if (!(a.diag & 2)) {
+  {
     reduce_waves_to_lds<1, G>(accH, lds, w, lane);
     reduce_waves_to_lds<1, G>(accX, lds + 4 * TSZ, w, lane);
   }
   const float* tH = lds;
   const float* tX = lds + 4 * TSZ;
-  if (!live || (a.diag & 4)) return;
+  if (!live) return;
   float gx[G], gh[G];
 #pragma unroll
   for (int j = 0; j < G; ++j) {
@@ -309,10 +297,6 @@ __global__ __launch_bounds__(256) void split_wb_kernel(const float* dWx, int row
     }
   }
 }
-static bool bias_col_enabled() {
-  const char* v = getenv("ABCD_BIASCOL");  // read per call: tests flip it in-process
-  return !(v && v[0] == '0');
-}
 
 struct EncWS {
   float* Xp;
@@ -455,25 +439,20 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
         const int base = (l * D + d) * (G == 4 ? 2 * H : H);
         f.hcol = base; f.ccol = G == 4 ? base + H : -1;
         f.rev = d == 1;
-        f.X = X; f.ldx = Inp; f.Wih = w.Wihp[l] + (size_t)d * G * H * Inp; f.bih = w.bcat[l] + d * G * H;
       }
       if (l == 0 && persist_enabled()) ABCD_TRY((hipError_t)stage_offsets(s, off, w.off));
-      // layer 0: input projection fused into the persistent kernel when it fits;
-      // otherwise the L x D*G*H projection GEMM feeds the recurrence
-      if (l == 0) ABCD_TRY((hipError_t)persist_encoder_fwd_fused(s, G, pa, &done));
-      if (!done) {
-        ABCD_TRY((hipError_t)gemm(s, L, D * G * H, Inp, opKC(X, Inp, L), opKC(w.Wihp[l], Inp, D * G * H), w.GX,
-                                  (long)D * G * H, 1.f, 0.f, w.bcat[l], ACT_NONE, w.scratch, w.scratch_floats));
-        ABCD_TRY((hipError_t)persist_encoder_fwd(s, G, pa, &done));
-      }
+      // the L x D*G*H input projection GEMM feeds the recurrence (fusing it into
+      // the persistent kernel measured +0.68 ms on the launch for the 0.6 ms saved)
+      ABCD_TRY((hipError_t)gemm(s, L, D * G * H, Inp, opKC(X, Inp, L), opKC(w.Wihp[l], Inp, D * G * H), w.GX,
+                                (long)D * G * H, 1.f, 0.f, w.bcat[l], ACT_NONE, w.scratch, w.scratch_floats));
+      ABCD_TRY((hipError_t)persist_encoder_fwd(s, G, pa, &done));
       ABCD_TRY((hipError_t)flush_offsets());
     }
     if (!done) note_dispatch(TK_ENC_FWD, "per-step rnn_fwd_step<%d>", G);
-    for (int i = 0; i < T && !done && !(diag_mask() & 8); ++i) {
+    for (int i = 0; i < T && !done; ++i) {
       FwdArgs a{};
       a.H = H;
       a.nd = D;
-      a.diag = diag_mask();
       for (int d = 0; d < D; ++d) {
         const bool rev = d == 1;
         const int t = rev ? T - 1 - i : i;
@@ -542,14 +521,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
   const std::vector<int> off = step_offsets(x->batch_sizes, T);
   const int64_t* bs = x->batch_sizes;
   const int TN = bwd_tn(H);
-  const hipStream_t s2 = (hipStream_t)wgrad_stream;
-  // opt-in (ABCD_ENCGATE=1): measured at c2 it gains nothing -- the side stream
-  // is busy with the decoder's weight gradients until ~1.8 ms into the 2.2 ms
-  // encoder BPTT, and the extra co-running GEMMs slow the BPTT by about what
-  // they hide (14.59 vs 14.59 ms/step)
-  const bool gate_ok = s2 && s2 != s && c->layers == 1 && D == 2 && persist_enabled() && T >= 8 &&
-                       getenv("ABCD_ENCGATE") && getenv("ABCD_ENCGATE")[0] == '1';
-  bool gated = false;
+  (void)wgrad_stream;  // the encoder's weight gradients follow the BPTT on s (a side-stream gate measured no gain)
   for (int l = c->layers - 1; l >= 0; --l) {
     const int In = l == 0 ? F : D * H;
     for (int d = 0; d < D; ++d)
@@ -572,14 +544,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
         b.rev = d == 1;
       }
       if (l == c->layers - 1 && persist_enabled()) ABCD_TRY((hipError_t)stage_offsets(s, off, w.off));
-      // gated overlap (single layer, side stream given): the weight gradients
-      // of the rows the BPTT finishes in its first half run on wgrad_stream
-      // beside the second half (split-K kernel only: write-through stashes)
-      hipEvent_t zeroed = nullptr;
-      if (gate_ok) ABCD_TRY((hipError_t)fork_event(&zeroed, 1));
-      ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done, zeroed));
-      if (gate_ok && !done) ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done));  // gather form
-      else if (gate_ok && done) gated = true;
+      ABCD_TRY((hipError_t)persist_encoder_bwd(s, G, pa, &done));
       ABCD_TRY((hipError_t)flush_offsets());
     }
     if (!done) note_dispatch(TK_ENC_BWD, "per-step launch_bwd_step<%d>", G);
@@ -621,7 +586,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
     }
     // weight gradients: reductions over all L packed frames (K = L, K-major
     // operands), over the row range [r0, r1) into the gradient with weight beta
-    const bool ones_col = l == 0 && F < Fp && !gated && bias_col_enabled();
+    const bool ones_col = l == 0 && F < Fp && true;
     auto wgrad = [&](hipStream_t st, int d, int r0, int r1, float beta, float* scratch, size_t scf) -> int {
       const abcd_rnn_g& gr = g->g[l][d];
       const float* X = l == 0 ? w.Xp : ((noise && noise[l - 1]) ? w.Ydrop[l - 1] : w.Y[l - 1]);  // Xp: padded copy
@@ -658,34 +623,11 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       if (gr.b_hh) ABCD_TRY((hipError_t)colsum(st, dGH, GH, K, GH, nullptr, gr.b_hh, beta, scratch, scf));
       return 0;
     };
-    if (gated) {
-      // rows finished by BPTT step im (both directions): the forward direction
-      // runs t = T-1 .. 0 (rows [off[T-1-im], L) done), the reverse t = 0 ..
-      // (rows [0, off[im+1]) done).  Their stashes are in memory once every
-      // group counter reached 16 * (im + 2) (the next publish drained them).
-      const int im = T / 2, nut = H / 16, ng = 2 * cdiv(x->B, PERSIST_ROWS);
-      const int f0 = off[T - 1 - im], r1 = off[im + 1];
-      hipEvent_t zeroed = nullptr, done_a = nullptr;
-      ABCD_TRY((hipError_t)fork_event(&zeroed, 1));
-      ABCD_TRY((hipError_t)fork_event(&done_a, 2));
-      ABCD_TRY(hipStreamWaitEvent(s2, zeroed, 0));
-      ABCD_TRY((hipError_t)gate_persist(s2, w.sync, ng, (unsigned)(nut * (im + 2))));
-      {
-        GemmSideScope side_tiles(true);
-        ABCD_TRY((hipError_t)wgrad(s2, 0, f0, L, 0.f, w.scratch, w.scratch_floats));
-        ABCD_TRY((hipError_t)wgrad(s2, 1, 0, r1, 0.f, w.scratch, w.scratch_floats));
-      }
-      ABCD_TRY(hipEventRecord(done_a, s2));
-      ABCD_TRY(hipStreamWaitEvent(s, done_a, 0));
-      ABCD_TRY((hipError_t)wgrad(s, 0, 0, f0, 1.f, w.scratch, w.scratch_floats));
-      ABCD_TRY((hipError_t)wgrad(s, 1, r1, L, 1.f, w.scratch, w.scratch_floats));
-    } else {
-      if (ones_col) {
-        set_col_kernel<<<std::max(1, std::min(1024, cdiv(L, 256))), 256, 0, s>>>(w.Xp, Fp, L, F, 1.f);
-        ABCD_CHECK_LAUNCH();
-      }
-      for (int d = 0; d < D; ++d) ABCD_TRY((hipError_t)wgrad(s, d, 0, L, 0.f, w.scratch, w.scratch_floats));
+    if (ones_col) {
+      set_col_kernel<<<std::max(1, std::min(1024, cdiv(L, 256))), 256, 0, s>>>(w.Xp, Fp, L, F, 1.f);
+      ABCD_CHECK_LAUNCH();
     }
+    for (int d = 0; d < D; ++d) ABCD_TRY((hipError_t)wgrad(s, d, 0, L, 0.f, w.scratch, w.scratch_floats));
     if (l > 0) {  // dX of this layer = dh of the layer below (both directions)
       for (int d = 0; d < D; ++d) {
         ABCD_TRY((hipError_t)pack2d(s, p->w[l][d].w_ih, In, In, GH, true, w.WihT[l][d], GH, In, GH));
@@ -1375,7 +1317,7 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
   // set to 1 after the BPTT; the packed W_ih pads are 0, so a later forward
   // that keeps it is unaffected) -- the colsum pass over L x G*H is gone
   const bool same_b = w.dGX == w.dGH;
-  const bool ones = c->feedback && F < Fp && cg.w_ih && cg.b_ih && bias_col_enabled();
+  const bool ones = c->feedback && F < Fp && cg.w_ih && cg.b_ih && true;
   if (ones) {
     set_col_kernel<<<std::max(1, std::min(1024, cdiv(L, 256))), 256, 0, s>>>(w.Xin, Fp, L, F, 1.f);
     ABCD_CHECK_LAUNCH();

@@ -1,7 +1,18 @@
 # coding: utf-8
-"""Post-training encoding (ABCD-VAE/encode.py): encoder -> sampler logits ->
-softmax -> long-format CSV (data_ix, category_ix, prob, annotation columns).
-Runs the encoder and sampler forward on the HIP path."""
+"""Post-training encoding on the HIP path: the drop-in for ABCD-VAE/encode.py
+(and, through ``output=``, encode_logit.py / encode_features.py).
+
+Same command line and the same long-format CSV as the reference
+(encode.py:38-55): one row per (segment, category) with columns
+``data_ix, category_ix, prob`` (``dimension, logit`` / ``dimension,
+feature_value`` for the logit / feature variants) followed by the
+annotation columns, rows ordered category-major within each batch.
+
+How it runs here: every batch goes through the encoder and sampler forward
+kernels once (model.py:60-66, 581-590) and stays on the device; the softmax
+(or nothing, or the to_code_like MLP) is applied there, and the whole table
+is built at the end with numpy index arithmetic -- no per-batch DataFrame
+melt / merge / append cycle."""
 import argparse
 import os
 
@@ -14,110 +25,110 @@ from modules import data_utils
 from modules.data_utils import Compose
 
 OUTPUT = "probs"  # encode_logit.py -> "logits", encode_features.py -> "features"
+COLUMNS = {"probs": ("category_ix", "prob"), "logits": ("dimension", "logit"),
+           "features": ("dimension", "feature_value")}
 
 
 class Encoder(learning.Learner):
-    """encode.py:12-55"""
+    """A trained checkpoint (ours or the reference's: learning.py:317-347 keys)
+    opened for inference: parameters frozen, modules in eval mode."""
 
     def __init__(self, model_config_path, device="cuda"):
         self.device = torch.device(device)
         self.retrieve_model(checkpoint_path=model_config_path, device=device)
-        for param in self.parameters():
-            param.requires_grad = False
-        self.encoder.eval()
-        self.feature_sampler.eval()
-        self.decoder.eval()
+        for m in (self.encoder, self.feature_sampler, self.decoder):
+            m.requires_grad_(False)
+            m.eval()
+
+    def _device_output(self, packed, output):
+        with torch.no_grad():
+            h = self.encoder(packed.to(self.device))
+            if output == "features":
+                return self.feature_sampler.to_code_like(h)
+            logits = self.feature_sampler(h)
+            return torch.softmax(logits, -1) if output == "probs" else logits
 
     def encode(self, data, is_packed=False, to_numpy=True, output=None):
-        output = output or OUTPUT
+        """One batch (a PackedSequence, a tensor or a list of tensors) ->
+        B x K probabilities (or logits / features); with to_numpy, an iterator
+        of per-segment numpy rows as the reference returns."""
         if not is_packed:
-            if not isinstance(data, list):
-                data = [data]
-            data = torch.nn.utils.rnn.pack_sequence(data)
-        with torch.no_grad():
-            data = data.to(self.device)
-            last_hidden = self.encoder(data)
-            if output == "features":
-                out = self.feature_sampler.to_code_like(last_hidden)
-            else:
-                out = self.feature_sampler(last_hidden)
-                if output == "probs":
-                    out = torch.nn.functional.softmax(out, -1)
+            data = torch.nn.utils.rnn.pack_sequence(data if isinstance(data, list) else [data])
+        out = self._device_output(data, output or OUTPUT)
         if to_numpy:
-            out = (p.data.cpu().numpy() for p in out)
+            return iter(out.cpu().numpy())
         return out
 
     def encode_dataset(self, dataset, save_path, to_numpy=True, batch_size=1, output=None):
         output = output or OUTPUT
-        var_name, value_name = {"probs": ("category_ix", "prob"), "logits": ("dimension", "logit"),
-                                "features": ("dimension", "feature_value")}[output]
-        dataloader = data_utils.DataLoader(dataset, batch_size=batch_size)
+        var_name, value_name = COLUMNS[output]
         rename_existing_file(save_path)
+        blocks, ixs = [], []
+        for packed, _, _, ix in data_utils.DataLoader(dataset, batch_size=batch_size):
+            blocks.append(self._device_output(packed, output))
+            ixs.append(np.asarray(ix, dtype=np.int64))
+        ann = None
         if "label" in dataset.df_annotation.columns:
-            df_ann = dataset.df_annotation.drop(columns=["onset_ix", "offset_ix", "length"])
-        else:
-            df_ann = None
-        for data, _, _, ix_in_list in dataloader:
-            vals = self.encode(data, is_packed=True, to_numpy=to_numpy, output=output)
-            df_encoded = pd.DataFrame(vals)
-            df_encoded.loc[:, "data_ix"] = ix_in_list
-            df_encoded = df_encoded.melt(id_vars=["data_ix"], var_name=var_name, value_name=value_name)
-            if df_ann is not None:
-                df_encoded = df_encoded.merge(df_ann, how="left", left_on="data_ix", right_index=True)
-            if os.path.isfile(save_path):
-                df_encoded.to_csv(save_path, index=False, mode="a", header=False)
-            else:
-                df_encoded.to_csv(save_path, index=False)
+            ann = dataset.df_annotation.drop(columns=["onset_ix", "offset_ix", "length"])
+        header = True
+        for vals, ix in zip(blocks, ixs):
+            v = vals.cpu().numpy()
+            n, k = v.shape
+            table = pd.DataFrame({"data_ix": np.tile(ix, k), var_name: np.repeat(np.arange(k), n),
+                                  value_name: v.T.reshape(-1)})
+            if ann is not None:
+                extra = ann.reindex(table["data_ix"].to_numpy()).reset_index(drop=True)
+                table = pd.concat([table, extra], axis=1)
+            table.to_csv(save_path, index=False, mode="w" if header else "a", header=header)
+            header = False
 
 
 def rename_existing_file(filepath):
-    if os.path.isfile(filepath):
-        new_path = filepath + ".prev"
-        rename_existing_file(new_path)
-        os.rename(filepath, new_path)
+    """Keep earlier outputs: path -> path.prev -> path.prev.prev -> ..."""
+    chain = []
+    p = filepath
+    while os.path.isfile(p):
+        chain.append(p)
+        p += ".prev"
+    for src in reversed(chain):
+        os.rename(src, src + ".prev")
 
 
 def get_parameters(argv=None):
-    p = argparse.ArgumentParser()
-    p.add_argument("model_path", type=str, help="Path to the configuration file of a trained model.")
-    p.add_argument("input_root", type=str, help="Path to the root directory under which inputs are located.")
-    p.add_argument("annotation_file", type=str, help="Path to the annotation csv file.")
-    p.add_argument("data_normalizer", type=float, help="Normalizing constant to devide the data.")
-    p.add_argument("--annotation_sep", type=str, default=",", help="Separator symbol of the annotation file.")
-    p.add_argument("-d", "--device", type=str, default="cuda", help="Computing device (GPU only).")
-    p.add_argument("-S", "--save_path", type=str, default=None, help="Path to the file where results are saved.")
-    p.add_argument("--fft_frame_length", type=float, default=0.008, help="FFT frame length in sec.")
-    p.add_argument("--fft_step_size", type=float, default=0.004, help="FFT step size in sec.")
-    p.add_argument("--fft_window_type", type=str, default="hann_window", help="Window type for FFT.")
-    p.add_argument("--fft_no_centering", action="store_true", help="If selected, no centering in FFT.")
-    p.add_argument("--channel", type=int, default=0, help="Channel ID # of multichannel recordings to use.")
-    p.add_argument("-E", "--epsilon", type=float, default=2 ** (-15), help="Added before log.")
-    p.add_argument("-b", "--batch_size", type=int, default=1, help="Batch size.")
+    p = argparse.ArgumentParser(description="Encode annotated segments with a trained ABCD-VAE (MI355X).")
+    p.add_argument("model_path", type=str, help="checkpoint.pt written by learning.py (this package or the reference)")
+    p.add_argument("input_root", type=str, help="directory the annotation's wav paths are relative to")
+    p.add_argument("annotation_file", type=str, help="annotation table (csv) of the segments to encode")
+    p.add_argument("data_normalizer", type=float, help="log-amplitudes are divided by this (training's -N)")
+    p.add_argument("--annotation_sep", type=str, default=",", help="field separator of the annotation table")
+    p.add_argument("-d", "--device", type=str, default="cuda", help="GPU device (there is no CPU path)")
+    p.add_argument("-S", "--save_path", type=str, default=None,
+                   help="output csv (default: <input_root>/autoencoded.csv); an existing file is kept as .prev")
+    p.add_argument("--fft_frame_length", type=float, default=0.008, help="STFT window length, seconds")
+    p.add_argument("--fft_step_size", type=float, default=0.004, help="STFT hop, seconds")
+    p.add_argument("--fft_window_type", type=str, default="hann_window", help="torch window function name")
+    p.add_argument("--fft_no_centering", action="store_true", help="STFT without centre padding")
+    p.add_argument("--channel", type=int, default=0, help="channel (0-based) of multi-channel wav files")
+    p.add_argument("-E", "--epsilon", type=float, default=2 ** (-15), help="offset inside log(|STFT| + eps)")
+    p.add_argument("-b", "--batch_size", type=int, default=1, help="segments per forward pass")
     return p.parse_args(argv)
 
 
 def main(argv=None, output=None):
-    parameters = get_parameters(argv)
-    save_path = parameters.save_path
-    if save_path is None:
-        save_path = os.path.join(parameters.input_root, "autoencoded.csv")
-    save_dir = os.path.dirname(save_path)
-    if save_dir and not os.path.isdir(save_dir):
-        os.makedirs(save_dir)
-    data_parser = data_utils.Data_Parser(parameters.input_root, parameters.annotation_file,
-                                         annotation_sep=parameters.annotation_sep)
-    fs = data_parser.get_sample_freq()
-    fft_frame_length = int(np.floor(parameters.fft_frame_length * fs))
-    fft_step_size = int(np.floor(parameters.fft_step_size * fs))
-    encoder = Encoder(parameters.model_path, device=parameters.device)
-    to_tensor = data_utils.ToTensor()
-    stft = data_utils.STFT(fft_frame_length, fft_step_size, window=parameters.fft_window_type,
-                           centering=not parameters.fft_no_centering)
-    eps, norm = parameters.epsilon, parameters.data_normalizer
-    log_and_normalize = data_utils.Transform(lambda x: (x + eps).log() / norm)
-    dataset = data_parser.get_data(transform=Compose([to_tensor, stft, log_and_normalize]),
-                                   channel=parameters.channel)
-    encoder.encode_dataset(dataset, save_path, batch_size=parameters.batch_size, output=output)
+    a = get_parameters(argv)
+    save_path = a.save_path or os.path.join(a.input_root, "autoencoded.csv")
+    if os.path.dirname(save_path):
+        os.makedirs(os.path.dirname(save_path), exist_ok=True)
+    parser = data_utils.Data_Parser(a.input_root, a.annotation_file, annotation_sep=a.annotation_sep)
+    fs = parser.get_sample_freq()
+    frame, hop = int(np.floor(a.fft_frame_length * fs)), int(np.floor(a.fft_step_size * fs))
+    enc = Encoder(a.model_path, device=a.device)
+    eps, norm = a.epsilon, a.data_normalizer
+    tfm = Compose([data_utils.ToTensor(),
+                   data_utils.STFT(frame, hop, window=a.fft_window_type, centering=not a.fft_no_centering),
+                   data_utils.Transform(lambda x: (x + eps).log() / norm)])
+    enc.encode_dataset(parser.get_data(transform=tfm, channel=a.channel), save_path, batch_size=a.batch_size,
+                       output=output)
     return save_path
 
 

@@ -13,6 +13,7 @@ targets PyTorch 1.2 / pandas 1.x): frame indices are kept as int, and
 `Tensor.stft` is called with `return_complex=True` and turned into the same
 real-pair amplitude.
 """
+import collections
 import os.path
 
 import numpy as np
@@ -68,7 +69,7 @@ class Dataset(torch.utils.data.Dataset):
         self.transform = transform
         self.channel = channel
         self.speaker2ix = speaker2ix
-        self._wav_cache = {}
+        self._wav_cache = collections.OrderedDict()
         self.get_discrete_bounds()
 
     def get_discrete_bounds(self):
@@ -90,12 +91,25 @@ class Dataset(torch.utils.data.Dataset):
     def __len__(self):
         return self.df_annotation.shape[0]
 
+    WAV_CACHE_FILES = 64  # open recordings kept (memory-mapped: the page cache holds the bytes)
+
     def _read(self, input_path):
-        # the reference re-reads the WAV for every item (data_utils.py:91); a per-file cache gives
-        # identical samples without the repeated I/O
-        if input_path not in self._wav_cache:
-            self._wav_cache[input_path] = spw.read(os.path.join(self.input_root, input_path))[1]
-        return self._wav_cache[input_path]
+        # the reference re-reads the WAV for every item (data_utils.py:91); a small LRU of
+        # memory-mapped recordings gives identical samples without the repeated I/O and
+        # without holding whole corpora in process memory
+        cache = self._wav_cache
+        if input_path in cache:
+            cache.move_to_end(input_path)
+            return cache[input_path]
+        path = os.path.join(self.input_root, input_path)
+        try:
+            data = spw.read(path, mmap=True)[1]
+        except ValueError:  # formats scipy cannot map (e.g. 24-bit PCM): read into memory
+            data = spw.read(path)[1]
+        cache[input_path] = data
+        if len(cache) > self.WAV_CACHE_FILES:
+            cache.popitem(last=False)
+        return data
 
     def __getitem__(self, ix):
         row = self.df_annotation.loc[ix]

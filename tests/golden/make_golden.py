@@ -35,8 +35,17 @@ Fixtures written (all small, committed):
 * ``toy_known_answers.json`` loss trajectories of the reference CLI on the toy
   data (config 1 of BASELINE.json and its variants) and the ``encode.py``
   argmax per segment.
+* ``prod_<variant>.npz``    one training step at the production widths of
+  BASELINE.json configs 2/4/5 (F=129, H=Hm=D=256, K=128/1024, speaker 256,
+  LSTM/GRU/plain) with B=72 (two 64-row tile groups): outputs, loss terms,
+  gradient norms / full small gradients / row+column sums of the large ones,
+  post-SGD deltas.  Weights come from the init order, inputs and noise from
+  seeds (``tests/golden_io.py:prod_inputs``).
+* ``ref_ckpt_small.pt`` + ``ref_ckpt_small_encode.npz``  a checkpoint written
+  by the reference CLI (small widths, toy data, 1 epoch) and the reference
+  ``encode.py``'s probabilities for it.
 
-Usage: ``python tests/golden/make_golden.py [--only small|toy|cli]``.
+Usage: ``python tests/golden/make_golden.py [--only small|prod|toy|cli|ckpt]``.
 """
 import argparse
 import hashlib
@@ -536,6 +545,42 @@ def run_cli(only=None):
     print("wrote", path)
 
 
+CKPT_FLAGS = ["-e", "1", "-b", "4", "-R", "LSTM", "-K", "16", "-f", "32", "--encoder_rnn_hidden_size", "32",
+              "--decoder_rnn_hidden_size", "32", "--mlp_hidden_size", "32", "--pretrain_epochs", "0"]
+
+
+def run_ckpt():
+    """A checkpoint.pt WRITTEN BY THE REFERENCE CLI (learning.py:293-314) at
+    small widths on the toy data (weights + optimizer / scheduler state + CPU
+    RNG state only: loadable with torch.load(weights_only=True)), and what the
+    reference's encode.py makes of it: per-segment probabilities over the K
+    categories (the long CSV folded to an 8 x K matrix)."""
+    import shutil
+    import pandas as pd
+    root = os.path.join(REF, "toy_data")
+    ann = os.path.join(root, "annotation_20170806-080002_89.2-94.22.csv")
+    with tempfile.TemporaryDirectory() as tmp:
+        save_root = os.path.join(tmp, "ckpt")
+        subprocess.run([sys.executable, __file__, "--child", "ABCD-VAE", "learning.py", "--", root, ann, "-S",
+                        save_root, "-j", "run"] + CKPT_FLAGS, check=True)
+        ckpt = os.path.join(save_root, "run", "checkpoint.pt")
+        shutil.copy(ckpt, os.path.join(HERE, "ref_ckpt_small.pt"))
+        csv = os.path.join(tmp, "enc.csv")
+        subprocess.run([sys.executable, __file__, "--child", "ABCD-VAE", "encode.py", "--", ckpt, root, ann, "1.0",
+                        "-S", csv, "-b", "4"], check=True)
+        df = pd.read_csv(csv)
+    df["category_ix"] = df["category_ix"].astype(int)
+    n, k = int(df["data_ix"].max()) + 1, int(df["category_ix"].max()) + 1
+    probs = np.zeros((n, k), np.float32)
+    probs[df["data_ix"].to_numpy(), df["category_ix"].to_numpy()] = df["prob"].to_numpy()
+    cols = [c for c in df.columns if c not in ("data_ix", "category_ix", "prob")]
+    np.savez_compressed(os.path.join(HERE, "ref_ckpt_small_encode.npz"), probs=probs,
+                        argmax=probs.argmax(1).astype(np.int64), row_order=df["data_ix"].to_numpy()[:16],
+                        meta=np.frombuffer(json.dumps({"flags": CKPT_FLAGS, "columns": list(df.columns),
+                                                       "annotation_columns": cols}).encode(), dtype=np.uint8))
+    print("wrote ref_ckpt_small.pt / ref_ckpt_small_encode.npz", probs.argmax(1))
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         vdir, script = sys.argv[2], sys.argv[3]
@@ -570,6 +615,8 @@ def main():
                        check=True)
     if a.only in (None, "cli"):
         run_cli(a.case)
+    if a.only in (None, "ckpt"):
+        run_ckpt()
 
 
 if __name__ == "__main__":

@@ -147,41 +147,6 @@ def test_fused_step_persist_vs_stepwise_bench_size(cfg_name):
     assert _rel(g_p, g_s) < 1e-4
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("knob,value", [("ABCD_FUSEX", "1"), ("ABCD_X6GEMM", "1"), ("ABCD_ENCGATE", "1"),
-                                         ("ABCD_DECHPRE", "0"), ("ABCD_X6S", "0"), ("ABCD_BIASCOL", "0"),
-                                         ("ABCD_SIDE5", "0"), ("ABCD_KLSIDE", "0"),
-                                         ("ABCD_LOSSSIDE", "1")])
-def test_opt_in_paths_match_default(knob, value):
-    """The opt-in variants -- input projection fused into the persistent
-    encoder kernel (ABCD_FUSEX=1), split-fp32 weight-gradient GEMMs
-    (ABCD_X6GEMM=1), encoder weight gradients gated beside the BPTT
-    (ABCD_ENCGATE=1), the full-K decoder cell (ABCD_DECHPRE=0), the f32-MFMA
-    GEMMs (ABCD_X6S=0), the encoder bias gradients as colsum passes instead of
-    the ones column of the input weight-gradient GEMM (ABCD_BIASCOL=0), the
-    side-stream GEMMs without the 160-wide tiles (ABCD_SIDE5=0), the KL on the
-    main stream (ABCD_KLSIDE=0), the loss reductions on the side stream
-    (ABCD_LOSSSIDE=1) -- give
-    the default path's losses and gradients at c2."""
-    import bench
-    cfg = bench.CONFIGS["c2"]
-    step = bench.build(cfg, "cuda")
-    batch = bench.make_batch(cfg, 0, "cuda")
-    sc_d, g_d = _fused_run(step, batch, True)
-    old = os.environ.get(knob)
-    os.environ[knob] = value
-    try:
-        sc_o, g_o = _fused_run(step, batch, True)
-    finally:
-        if old is None:
-            os.environ.pop(knob, None)
-        else:
-            os.environ[knob] = old
-    for k in range(4):
-        assert abs(sc_o[k] - sc_d[k]) <= 1e-5 * abs(sc_d[k]) + 1e-6, (k, sc_o[k].item(), sc_d[k].item())
-    assert _rel(g_o, g_d) < 1e-4
-
-
 @pytest.mark.parametrize("rnn", ["LSTM", "GRU"])
 def test_decoder_input_dropout_persist_vs_stepwise(rnn):
     """Decoder input dropout 0 < p < 1 in training (RNN_Cell's nn.Dropout,
@@ -201,29 +166,3 @@ def test_decoder_input_dropout_persist_vs_stepwise(rnn):
         assert abs(sc_p[k] - sc_s[k]) <= 1e-5 * abs(sc_s[k]) + 1e-6, (k, sc_p[k].item(), sc_s[k].item())
     assert _rel(g_p, g_s) < 1e-4
     assert sc_p[0] != sc_0[0] and _rel(g_p, g_0) > 1e-3
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("cfg_name", ["c2", "c4", "c5"])
-@pytest.mark.parametrize("mode", ["1", "2"])
-def test_sampler_wgrad_stream_matches_one_stream(cfg_name, mode):
-    """The sampler's parameter gradients queued on the weight-gradient stream
-    (ABCD_SAMPSPLIT=1) or a third stream (2) beside the d_h chain give the
-    one-stream default's results: losses bit-identical, gradients within 1e-6
-    (the side-stream GEMMs pick a smaller split-K, another summation order)."""
-    import bench
-    cfg = bench.CONFIGS[cfg_name]
-    step = bench.build(cfg, "cuda")
-    batch = bench.make_batch(cfg, 0, "cuda")
-    sc_d, g_d = _fused_run(step, batch, True)
-    old = os.environ.get("ABCD_SAMPSPLIT")
-    os.environ["ABCD_SAMPSPLIT"] = mode
-    try:
-        sc_o, g_o = _fused_run(step, batch, True)
-    finally:
-        if old is None:
-            os.environ.pop("ABCD_SAMPSPLIT", None)
-        else:
-            os.environ["ABCD_SAMPSPLIT"] = old
-    assert torch.equal(sc_o[:4], sc_d[:4])
-    assert _rel(g_o, g_d) < 1e-6

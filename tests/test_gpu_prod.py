@@ -26,9 +26,9 @@ GRAD_TOL = 1e-3
 
 # the kernels bench.py's configs dispatch at H = Hm = 256, F = 129 (Fp = 144)
 EXPECT = {
-    "LSTM": {"enc_fwd": "enc_fwd_persist<4,16,8,0>", "enc_bwd": "enc_bwd_sk<4,16>",
+    "LSTM": {"enc_fwd": "enc_fwd_persist<4,16,8>", "enc_bwd": "enc_bwd_sk<4,16>",
              "dec_fwd": "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd": "dec_bwd_sk<9,16,16,LSTM>"},
-    "GRU": {"enc_fwd": "enc_fwd_persist<3,16,8,0>", "enc_bwd": "enc_bwd_sk<3,16>",
+    "GRU": {"enc_fwd": "enc_fwd_persist<3,16,8>", "enc_bwd": "enc_bwd_sk<3,16>",
             "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_sk<9,16,16,GRU>"},
 }
 

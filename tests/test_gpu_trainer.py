@@ -92,3 +92,25 @@ def test_plain_cli_smoke(tmp_path):
     for e in range(2):
         assert _rel(learner.history[e]["train"]["total"], ka["train_total"][e]) < 1e-4
         assert _rel(learner.history[e]["valid"]["total"], ka["valid_total"][e]) < 1e-4
+
+
+def test_reference_checkpoint_encodes_like_reference(tmp_path):
+    """learning.py:293-347 interop: a checkpoint.pt WRITTEN BY THE REFERENCE CLI
+    (tests/golden/ref_ckpt_small.pt, make_golden.py:run_ckpt) is opened by
+    retrieve_model (torch.load weights_only=True) and encode.py reproduces the
+    reference encode.py's per-segment category probabilities (<= 1e-5) and
+    argmax (exact), in the reference's CSV layout."""
+    import numpy as np
+    import encode
+    z = np.load(os.path.join(GOLDEN, "ref_ckpt_small_encode.npz"), allow_pickle=False)
+    import json
+    meta = json.loads(bytes(z["meta"]).decode())
+    out = encode.main([os.path.join(GOLDEN, "ref_ckpt_small.pt"), TOY, ANN, "1.0", "-S",
+                       os.path.join(str(tmp_path), "enc.csv"), "-b", "4"])
+    df = pd.read_csv(out)
+    assert list(df.columns) == meta["columns"]
+    assert list(df["data_ix"].to_numpy()[:16]) == list(z["row_order"])
+    probs = np.zeros_like(z["probs"])
+    probs[df["data_ix"].to_numpy(), df["category_ix"].to_numpy().astype(int)] = df["prob"].to_numpy()
+    assert np.abs(probs - z["probs"]).max() <= 1e-5
+    assert (probs.argmax(1) == z["argmax"]).all()

@@ -123,3 +123,22 @@ def test_stft_frame_count_matches_torch(n_fft, hop, center):
         z = torch.stft(torch.zeros(length), n_fft, hop_length=hop, window=torch.hann_window(n_fft), center=center,
                        return_complex=True)
         assert lib.abcd_stft_frames(length, n_fft, hop, int(center)) == z.shape[1], length
+
+
+def test_reference_checkpoint_loads_into_product_modules():
+    """A checkpoint written by the reference CLI loads with a loader that
+    executes nothing (weights_only=True), and its *_init_parameters dicts and
+    state dicts rebuild the product's modules exactly (learning.py:317-327)."""
+    from modules import model as M
+    path = os.path.join(REPO, "tests", "golden", "ref_ckpt_small.pt")
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    for k in ("epoch", "encoder", "encoder_init_parameters", "feature_sampler", "feature_sampler_init_parameters",
+              "decoder", "decoder_init_parameters", "optimizer", "lr_scheduler", "gradient_clip", "random_state"):
+        assert k in ck, k
+    enc = M.RNN_Variational_Encoder(**ck["encoder_init_parameters"])
+    samp = M.ABCDSampler(**ck["feature_sampler_init_parameters"])
+    dec = M.RNN_Variational_Decoder(**ck["decoder_init_parameters"])
+    for m, key in ((enc, "encoder"), (samp, "feature_sampler"), (dec, "decoder")):
+        m.load_state_dict(ck[key])
+        for name, v in m.state_dict().items():
+            assert torch.equal(v, ck[key][name]), (key, name)
