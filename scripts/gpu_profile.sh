@@ -1,14 +1,17 @@
-# GPU box: tests, bench, rocprof kernel stats and PMC traffic passes of bench.py c2.
-# usage: bash scripts/gpu_profile.sh [tag]
+# GPU box: bench lines of every config, rocprofv3 kernel stats of c2, PMC traffic passes of c2.
+# usage: bash scripts/gpu_profile.sh <tag>     (outputs under gpurun_out/<tag>/)
 set -e
 TAG=${1:-run}
-mkdir -p gpurun_out
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$TAG -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing > /dev/null 2> gpurun_out/pmc_fetch.err
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$TAG -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing > /dev/null 2> gpurun_out/pmc_write.err
-python scripts/pmc_traffic.py gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG gpurun_out/traffic_$TAG.json > /dev/null
-tail -3 gpurun_out/pytest_gpu.log
-cat gpurun_out/bench.json
+for c in c2 c4 c5 c5gru; do
+  timeout -k 10 400 python -u bench.py --config $c --steps 20 --warmup 3 > $OUT/bench_$c.json 2> $OUT/bench_$c.err
+  echo "bench $c done"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_c2.json 2> $OUT/prof_c2.err
+echo "rocprof c2 done"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing > /dev/null 2> $OUT/pmc_fetch.err
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing > /dev/null 2> $OUT/pmc_write.err
+python scripts/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/traffic.json > /dev/null
+echo "pmc done"

@@ -30,6 +30,7 @@ struct PFwdArgs {
   const int* off;    // device: off[0..T]
   unsigned* sync;    // one 128-B counter line per group, zeroed before the launch
   unsigned long long* prof;  // diagnostics: per-step s_memtime stamps, or null
+  int exp;                   // experiment bits (ABCD_EXP, A/B timing only)
 };
 
 // One direction of an encoder layer, backward (BPTT).
@@ -47,6 +48,7 @@ struct PBwdArgs {
   const int* off;
   unsigned* sync;
   unsigned long long* prof;
+  int exp;
   float* part;       // split-K partials: 2 parity slots x groups x H/16 consumers x 4 waves x H/16 producers x 256
 };
 
@@ -58,6 +60,7 @@ struct PBwdArgs {
 struct PDecFwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
   int flags;                       // hand-off form: 1 per-member flags, 0 group counter
+  int exp;
   const int* off;
   unsigned* sync;
   unsigned long long* prof;
@@ -76,6 +79,7 @@ struct PDecFwdArgs {
 struct PDecBwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
   int flags;                       // hand-off form: 1 per-member flags, 0 group counter
+  int exp;
   const int* off;
   unsigned* sync;
   unsigned long long* prof;

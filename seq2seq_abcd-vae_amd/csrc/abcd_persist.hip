@@ -102,6 +102,30 @@ struct BufKC2x {
   }
 };
 DEV void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// Wave-private LDS transpose of a 16 x 16 accumulator-layout tile (lane
+// (r, q) holds rows 4q + g, column r) into row quads (lane l: row l >> 2,
+// columns 4(l & 3) .. +3), so the tile leaves in ONE 16-B store per lane
+// instead of four 4-B ones: a 4-B write-through store costs ~6x a 16-B one
+// per byte (MI355X_MICROARCH.md), and every publish drains the wave's stores.
+constexpr int TP_PITCH = 20;                    // floats per row: 16-B aligned rows, conflict-free writes
+constexpr int TP_FLOATS = 16 * TP_PITCH;        // per wave
+DEV f4 tp_quad(float* tb, const float (&v)[4], int lane) {
+  const int r = lane & 15, q = lane >> 4;
+  __builtin_amdgcn_wave_barrier();  // the previous quad reads of this buffer are issued (LDS is in order per wave)
+#pragma unroll
+  for (int g = 0; g < 4; ++g) tb[(4 * q + g) * TP_PITCH + r] = v[g];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  return *reinterpret_cast<const f4*>(tb + (lane >> 2) * TP_PITCH + 4 * (lane & 3));
+}
+// 16-B store at byte offset `off` of the buffer `rs` (rows beyond its extent
+// are dropped by the range check); sc1: write-through (hand-off payloads)
+DEV void st4(__amdgpu_buffer_rsrc_t rs, uint32_t off, f4 v, bool wt) {
+  if (wt) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, off, 0, 16);
+  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, off, 0, 0);
+}
 
 // lane 0 of the workgroup polls until *cnt >= target (bounded), then the
 // barrier releases every wave
@@ -272,7 +296,8 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
       const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u),
                     (uint32_t)H * 4u};
       if (X6) {
-        wave_mma_x6<G, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q);
+        wave_mma_x6<G, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q,
+                                             (a.exp & 1) ? mem % (X6 > 0 ? X6 : 1) : 0);
       } else {
         wave_mma_lds<G, PD>(acc, A, row0 + r, smem, nch, lane, q);
       }
@@ -464,7 +489,6 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
 // after all of them consumed step i-1's partials (slot (i-1)&1).
 // G = 3 (GRU) pads the own-column block to 64 with a zero gate.
 // ---------------------------------------------------------------------------
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
 constexpr int SK_PITCH = 68;  // floats per row of the wave-private dG transpose (conflict-free b128 reads)
 template <int G, int NSUB>
 __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
@@ -959,6 +983,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   f4* B1 = BC + 2 * NCC * 3 * 64;       // mlp tile: [NH32][3][64]
   f4* B2 = B1 + NH32 * 3 * 64;          // emit: mu tile, lv tile: [2][NM32][3][64]
   float* LVX = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [2][16][16]
+  float* tb = LVX + 2 * 16 * 16 + w * TP_FLOATS;                   // this wave's transpose tile
   if (nx32)
     stage_x6(BC, a.Wih, Fp, Fp, 2, nx32, 0, NCC,
              [&](int j, int rr) { return GRU ? dec_gru_row(H, u0, j, rr, true) : dec_cell_row(H, u0, j, rr); });
@@ -1004,9 +1029,10 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       if (HPRE && i > 0) {
         acc[0] = acch[0];
         acc[1] = acch[1];
-        if constexpr (NXC > 0) wave_mma_x6<2, (NXC > 0 ? NXC : 1), 8>(acc, A, row0 + r, BC, NCC, lane, q);
+        if constexpr (NXC > 0)
+          wave_mma_x6<2, (NXC > 0 ? NXC : 1), 8>(acc, A, row0 + r, BC, NCC, lane, q, (a.exp & 1) ? mem % NXC : 0);
       } else {
-        wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q);
+        wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q, (a.exp & 1) ? mem % NCC : 0);
       }
     }
     PSTAMP(7);
@@ -1031,26 +1057,36 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         cst[g] = gf[g] * cst[g] + gi[g] * gg[g];
         hv[g] = go[g] * ftanh(cst[g]);
       }
-      const int b = row0 + 4 * q + g;
-      if (b < bs) {
-        if (lo) st_sc1(a.Hs + (long)(o + b) * H + unit, hv[g]);                       // -> mlp
-        else if (b < next_bs) st_sc1(a.Hprev + (long)(next_off + b) * H + unit, hv[g]);  // -> next cell
+    }
+    // row quads of this wave's 16 rows x 8 units: lane l holds row trow, units
+    // u0 + tc .. +3 of the tile's lo half (tcol < 8) or hi half (tcol >= 8)
+    const int trow = lane >> 2, tcol = 4 * (lane & 3), tc = tcol & 7;
+    const bool thi = tcol >= 8;
+    const uint32_t qoff = (uint32_t)((row0 + trow) * H + u0 + tc) * 4u;  // byte offset in an H-pitch step block
+    {  // h -> mlp (lo half) and -> the next cell (hi half, rows < next_bs)
+      const f4 hq = tp_quad(tb, hv, lane);
+      if (row0 < bs) {
+        if (!thi) st4(make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), qoff, hq, true);
+        else st4(make_rsrc(a.Hprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, hq, true);
       }
     }
     gs.publish();
     PSTAMP(1);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-      if (b >= bs) continue;
-      const long rr = o + b;
-      float* Gr = a.Gst + rr * 4 * H;
-      if (lo) {
-        Gr[unit] = gi[g]; Gr[H + unit] = gf[g];
-        if (!GRU) a.Cst[rr * H + unit] = cst[g];
-      } else {
-        Gr[2 * H + unit] = gg[g]; Gr[3 * H + unit] = go[g];
-        if (!GRU && b < next_bs) a.Cprev[(long)(next_off + b) * H + unit] = cst[g];
+    if (row0 < bs) {  // stashes for the backward pass (plain 16-B stores)
+      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
+      const uint32_t goff = (uint32_t)((row0 + trow) * 4 * H + u0 + tc) * 4u;
+      {
+        const float v[4] = {lo ? gi[0] : gg[0], lo ? gi[1] : gg[1], lo ? gi[2] : gg[2], lo ? gi[3] : gg[3]};
+        st4(rg, goff + (uint32_t)(thi ? 2 * H : 0) * 4u, tp_quad(tb, v, lane), false);  // i | g
+      }
+      {
+        const float v[4] = {lo ? gf[0] : go[0], lo ? gf[1] : go[1], lo ? gf[2] : go[2], lo ? gf[3] : go[3]};
+        st4(rg, goff + (uint32_t)(thi ? 3 * H : H) * 4u, tp_quad(tb, v, lane), false);  // f | o
+      }
+      if constexpr (!GRU) {  // c -> Cst (lo half), -> the next step's Cprev row (hi half)
+        const f4 cq = tp_quad(tb, cst, lane);
+        if (!thi) st4(make_rsrc(a.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qoff, cq, false);
+        else st4(make_rsrc(a.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, cq, false);
       }
     }
     // ---------------- mlp ----------------
@@ -1063,20 +1099,20 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
-          wave_mma_x6p<3, NH32, 8>(a3, Hs, row0 + r, bp, lane, q);
+          wave_mma_x6p<3, NH32, 8>(a3, Hs, row0 + r, bp, lane, q, (a.exp & 1) ? mem % NH32 : 0);
           a1[0] = a3[0];
           acch[0] = a3[1];
           acch[1] = a3[2];
         } else {
-          wave_mma_x6<1, NH32, 8>(a1, Hs, row0 + r, B1, NH32, lane, q);
+          wave_mma_x6<1, NH32, 8>(a1, Hs, row0 + r, B1, NH32, lane, q, (a.exp & 1) ? mem % NH32 : 0);
         }
       }
       PSTAMP(6);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int b = row0 + 4 * q + g;
-        if (b < bs) st_sc1(a.Aact + (long)(o + b) * 2 * Hm + 16 * mem + r, ftanh(a1[0][g] + b1v));
-      }
+      const float av[4] = {ftanh(a1[0][0] + b1v), ftanh(a1[0][1] + b1v), ftanh(a1[0][2] + b1v), ftanh(a1[0][3] + b1v)};
+      const f4 aq = tp_quad(tb, av, lane);
+      if (row0 < bs)
+        st4(make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
+            (uint32_t)((row0 + trow) * 2 * Hm + 16 * mem + tcol) * 4u, aq, true);
     }
     gs.publish();
     PSTAMP(3);
@@ -1102,7 +1138,8 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       if (erow0 < bs) {
         const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
                        (uint32_t)2 * Hm * 4u};
-        wave_mma_x6<1, NM32, 8>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q);
+        wave_mma_x6<1, NM32, 8>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
+                                (a.exp & 1) ? mem % NM32 : 0);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) ev[g] = col2 < F ? ae[0][g] + b2v : 0.f;
@@ -1112,29 +1149,29 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       }
     }
     __syncthreads();
+    // this wave's emit rows erow0 + trow, columns 16 j2 + tcol .. +3 (Fp pitch)
+    const uint32_t eoff = (uint32_t)((erow0 + trow) * Fp + 16 * j2 + tcol) * 4u;
     if (has2 && part == 0) {
+      float xm[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int b = erow0 + 4 * q + g;
         const float lv = LVX[((w & 1) * 16 + 4 * q + g) * 16 + r];
         const float x = col2 < F ? ev[g] + __expf(0.5f * lv) * epre[g] : 0.f;
         epre[g] = x;
-        if (b < bs && a.feedback && b < next_bs) st_sc1(a.Xin + (long)(next_off + b) * Fp + col2, x * mpre[g]);
+        xm[g] = x * mpre[g];
       }
+      const f4 xq = tp_quad(tb, xm, lane);
+      if (a.feedback && erow0 < next_bs)
+        st4(make_rsrc(a.Xin + (size_t)next_off * Fp, (uint32_t)next_bs * Fp * 4u), eoff, xq, true);
     }
     gs.publish();
-    if (has2) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int b = erow0 + 4 * q + g;
-        if (b >= bs) continue;
-        const long rr = o + b;
-        if (part == 0) {
-          a.MU[rr * Fp + col2] = ev[g];
-          a.OUT[rr * Fp + col2] = epre[g];
-        } else {
-          a.LV[rr * Fp + col2] = ev[g];
-        }
+    if (has2 && erow0 < bs) {
+      const uint32_t ext = (uint32_t)bs * Fp * 4u;
+      if (part == 0) {
+        st4(make_rsrc(a.MU + (size_t)o * Fp, ext), eoff, tp_quad(tb, ev, lane), false);
+        st4(make_rsrc(a.OUT + (size_t)o * Fp, ext), eoff, tp_quad(tb, epre, lane), false);
+      } else {
+        st4(make_rsrc(a.LV + (size_t)o * Fp, ext), eoff, tp_quad(tb, ev, lane), false);
       }
     }
     PSTAMP(5);
@@ -1342,13 +1379,14 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
 constexpr int DSK_PITCH = 36;  // floats per row of the wave-private dG transpose
 // acc += sum of NP partial f4s at base + p * 1 KiB, NB loads in flight
 template <int NP, int NB = NP>
-DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc) {
+DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc, int rot = 0) {
+  auto pp = [&](int p) { const int x = p + rot; return x >= NP ? x - NP : x; };
 #pragma unroll
   for (int p0 = 0; p0 < NP; p0 += NB) {
     f4 v[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k)
-      v[k] = p0 + k < NP ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (uint32_t)(p0 + k) * 1024u,
+      v[k] = p0 + k < NP ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, base + (uint32_t)pp(p0 + k) * 1024u,
                                                                                         0, 16))
                          : f4zero();
 #pragma unroll
@@ -1445,7 +1483,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     PSTAMP(0);
     if (mem < nFt) {
       f4 dx = f4zero();
-      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx);
+      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx, (a.exp & 1) ? mem % M : 0);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int b = row0 + 4 * q + g;
@@ -1474,7 +1512,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       if (i > 0) group_wait(cnt2, (unsigned)(M * i));  // every wave: it holds a workgroup barrier
       if (has_part) {
         const int pl = q * 16 + (mem & 1) * 8 + (r & 7);
-        sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr);
+        sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr, (a.exp & 1) ? mem % M : 0);
       }
     };
     read_dhr();
@@ -1524,7 +1562,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     f4 acc[1] = {f4zero()};
     if (row0 < bs) {
       const BufKC Az{make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u), (uint32_t)2 * Hm * 4u};
-      wave_mma_x6<1, NZ, 8>(acc, Az, row0 + r, B2, NZ, lane, q);
+      wave_mma_x6<1, NZ, 8>(acc, Az, row0 + r, B2, NZ, lane, q, (a.exp & 1) ? mem % NZ : 0);
     }
     PSTAMP(7);
     float dgh[4][4];
@@ -1745,6 +1783,12 @@ __global__ __launch_bounds__(256) void persist_reset(unsigned* sync, long nwords
 // ABCD_SPIN_LIMIT=<polls> (debug/tests): shrink the hand-off spin bound so a
 // wait times out at once; the device word is only rewritten when the value
 // changes (never in a default run)
+// ABCD_EXP (A/B experiments only): bit 0 rotates each consumer's read order
+static int exp_bits() {
+  const char* v = getenv("ABCD_EXP");
+  return v ? atoi(v) : 0;
+}
+
 static int sync_spin_limit(hipStream_t s) {
   static unsigned cur = 1u << 22, staged;
   const char* v = getenv("ABCD_SPIN_LIMIT");
@@ -1793,6 +1837,7 @@ static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PFwdArgs b = a;
   b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
+  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_ENC_FWD);
     enc_fwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
@@ -1812,6 +1857,7 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
+  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_ENC_BWD);
     enc_bwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
@@ -1854,6 +1900,7 @@ static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
+  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_ENC_BWD);
     enc_bwd_sk<G, NSUB><<<grid, 256, lds, s>>>(b);
@@ -1914,6 +1961,7 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   PDecFwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
+  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_DEC_FWD);
     dec_fwd_persist<NCC><<<grid, 256, lds, s>>>(b);
@@ -1927,7 +1975,7 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
 template <int NCC, int NH32, int NM32, bool GRU, bool HPRE>
 static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
-  const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4;
+  const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE>, grid, lds, &ok));
@@ -1936,6 +1984,7 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
   PDecFwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
+  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_DEC_FWD);
     dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
@@ -1993,6 +2042,7 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   PDecBwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
+  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_DEC_BWD);
     dec_bwd_sk<NXS, NHS, NZ, GRU><<<grid, 256, lds, s>>>(b);
@@ -2035,6 +2085,7 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   PDecBwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
+  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_DEC_BWD);
     dec_bwd_persist<<<grid, 256, lds, s>>>(b);

@@ -130,18 +130,21 @@ DEV void stage_x6(f4* dst, const float* W, long ldw, int kvalid, int nsub, int n
 // image with `nch` chunks per subtile (nch >= NCH; a segment of a wider image
 // starts at Bl + c0 * 3 * 64).
 template <int NR, int NCH, int PD, class OA>
-DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q) {
+DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q, int rot = 0) {
   constexpr int P = PD < NCH ? PD : NCH;
+  // chunk order rotated by `rot` (wave-uniform, < NCH): consumers of one
+  // hand-off tile start on different lines instead of all on chunk 0
+  auto cc = [&](int c) { const int x = c + rot; return x >= NCH ? x - NCH : x; };
   f4 ra[P], rb[P];
 #pragma unroll
-  for (int p = 0; p < P; ++p) A.frag8(arow, p, q, ra[p], rb[p]);
+  for (int p = 0; p < P; ++p) A.frag8(arow, cc(p), q, ra[p], rb[p]);
   // B fragments double-buffered: chunk c + 1's LDS reads are issued before
   // chunk c's MFMAs so their latency hides behind them
   f4 bw[NR][3];
 #pragma unroll
   for (int j = 0; j < NR; ++j)
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bl[((j * nch) * 3 + pl) * 64 + lane];
+    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bl[((j * nch + cc(0)) * 3 + pl) * 64 + lane];
   // pin the whole ring's loads here (the scheduler would sink each next to
   // its use) and keep each chunk's split + refill ahead of its MFMAs
   __builtin_amdgcn_sched_barrier(0);
@@ -153,11 +156,11 @@ DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch
 #pragma unroll
       for (int j = 0; j < NR; ++j)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bl[((j * nch + c + 1) * 3 + pl) * 64 + lane];
+        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bl[((j * nch + cc(c + 1)) * 3 + pl) * 64 + lane];
     }
     bf8 a0, a1, a2;
     split8(ra[p], rb[p], a0, a1, a2);
-    if (c + P < NCH) A.frag8(arow, c + P, q, ra[p], rb[p]);
+    if (c + P < NCH) A.frag8(arow, cc(c + P), q, ra[p], rb[p]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < NR; ++j)
@@ -176,16 +179,18 @@ DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch
 // wave_mma_x6 with one image segment per output tile: chunk c of tile j at
 // Bp[j] + c * 3 * 64 (tiles from different LDS images sharing one A operand)
 template <int NR, int NCH, int PD, class OA>
-DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp)[NR], int lane, int q) {
+DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp)[NR], int lane, int q,
+                      int rot = 0) {
   constexpr int P = PD < NCH ? PD : NCH;
+  auto cc = [&](int c) { const int x = c + rot; return x >= NCH ? x - NCH : x; };
   f4 ra[P], rb[P];
 #pragma unroll
-  for (int p = 0; p < P; ++p) A.frag8(arow, p, q, ra[p], rb[p]);
+  for (int p = 0; p < P; ++p) A.frag8(arow, cc(p), q, ra[p], rb[p]);
   f4 bw[NR][3];
 #pragma unroll
   for (int j = 0; j < NR; ++j)
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bp[j][pl * 64 + lane];
+    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bp[j][(cc(0) * 3 + pl) * 64 + lane];
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -195,11 +200,11 @@ DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp
 #pragma unroll
       for (int j = 0; j < NR; ++j)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bp[j][((c + 1) * 3 + pl) * 64 + lane];
+        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bp[j][(cc(c + 1) * 3 + pl) * 64 + lane];
     }
     bf8 a0, a1, a2;
     split8(ra[p], rb[p], a0, a1, a2);
-    if (c + P < NCH) A.frag8(arow, c + P, q, ra[p], rb[p]);
+    if (c + P < NCH) A.frag8(arow, cc(c + P), q, ra[p], rb[p]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < NR; ++j)
