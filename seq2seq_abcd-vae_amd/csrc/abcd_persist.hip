@@ -260,6 +260,9 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
   float bh[G];
 #pragma unroll
   for (int j = 0; j < G; ++j) bh[j] = (G == 3) ? D.bhh[j * H + unit] : 0.f;
+  // wave-private transpose tile after the weight image (16-B stores, tp_quad)
+  float* tb = reinterpret_cast<float*>(smem) + (size_t)G * 16 * H * (X6 ? 6 : 4) / 4 + w * TP_FLOATS;
+  const int trow = lane >> 2, tcol = 4 * (lane & 3);
   __syncthreads();
   float st[4] = {0.f, 0.f, 0.f, 0.f};  // c (LSTM) / h (GRU) of the lane's 4 cells
   const int* off = a.off;
@@ -329,29 +332,42 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
         cv[g] = 0.f;
         st[g] = hv[g];
       }
-      if (b < bs && b < next_bs) st_sc1(D.Hprev + (long)(next_off + b) * H + unit, hv[g]);
+    }
+    // h -> the next step's operand rows (write-through, 16-B stores; rows
+    // >= next_bs fall outside the buffer's extent)
+    const uint32_t qh = (uint32_t)((row0 + trow) * H + u0 + tcol) * 4u;
+    {
+      const f4 hq = tp_quad(tb, hv, lane);
+      if (row0 < next_bs) st4(make_rsrc(D.Hprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qh, hq, true);
     }
     PSTAMP(3);
     group_publish(cnt);
-    // pass 2: stashes for the backward pass and the outputs (plain stores,
-    // drained while the next step waits for its operand)
+    // pass 2: stashes for the backward pass and the outputs (plain 16-B
+    // stores, drained while the next step waits for its operand)
+    if (row0 < bs) {
+      const __amdgpu_buffer_rsrc_t rg = make_rsrc(D.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
+      const uint32_t go = (uint32_t)((row0 + trow) * 4 * H + u0 + tcol) * 4u;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+      for (int j = 0; j < 4; ++j) {
+        const float v[4] = {gv[0][j], gv[1][j], gv[2][j], gv[3][j]};
+        st4(rg, go + (uint32_t)(j * H) * 4u, tp_quad(tb, v, lane), false);
+      }
+      if (G == 4) st4(make_rsrc(D.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qh, tp_quad(tb, cv, lane), false);
+      st4(make_rsrc(D.Y + (size_t)o * D.ldy, (uint32_t)bs * D.ldy * 4u),
+          (uint32_t)((row0 + trow) * D.ldy + u0 + tcol) * 4u, tp_quad(tb, hv, lane), false);
+      if (G == 4 && row0 < next_bs)
+        st4(make_rsrc(D.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qh, tp_quad(tb, cv, lane), false);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // rows without a predecessor / whose sequence ends here (rare)
       const int b = row0 + 4 * q + g;
       if (b >= bs) continue;
       const long rr = o + b;
-      const bool haspred = b < prev_valid;
-      float* Gr = D.Gst + rr * 4 * H;
-      Gr[unit] = gv[g][0]; Gr[H + unit] = gv[g][1]; Gr[2 * H + unit] = gv[g][2]; Gr[3 * H + unit] = gv[g][3];
-      if (G == 4) D.Cst[rr * H + unit] = cv[g];
-      if (!haspred) {
+      if (b >= prev_valid) {
         if (G == 4) D.Cprev[rr * H + unit] = 0.f;
         D.Hprev[rr * H + unit] = 0.f;
       }
-      D.Y[rr * D.ldy + unit] = hv[g];
-      if (b < next_bs) {
-        if (G == 4) D.Cprev[(long)(next_off + b) * H + unit] = cv[g];
-      } else if (D.out) {
+      if (b >= next_bs && D.out) {
         D.out[(long)b * D.ldo + D.hcol + unit] = hv[g];
         if (G == 4) D.out[(long)b * D.ldo + D.ccol + unit] = cv[g];
       }
@@ -506,6 +522,8 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
   unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
   f4* Bimg = smem;                                         // [NSUB][2][3][64]
   float* Ast = reinterpret_cast<float*>(smem + NSUB * 2 * 3 * 64) + w * 16 * SK_PITCH;
+  float* tb = reinterpret_cast<float*>(smem + NSUB * 2 * 3 * 64) + 4 * 16 * SK_PITCH + w * TP_FLOATS;
+  const int trow = lane >> 2, tcol = 4 * (lane & 3);
   // B image: subtile j = output units 16j..16j+15, chunk c, lane (r, q):
   // kappa = 32c + 8q + 0..7 -> gate kappa/16, own unit kappa%16
   for (int e = threadIdx.x; e < NSUB * 16 * 2 * 4; e += 256) {
@@ -615,14 +633,19 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
       }
     }
     PSTAMP(2);
-    // partials for the next step from this step's own dG columns
-    if (i + 1 < T && row0 < bs) {
+    // the wave's dG tile rows x [gate j][own unit] in LDS: the split-K
+    // operand below and the stash after the publish
+    if (row0 < bs) {
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int j = 0; j < 4; ++j) Ast[(4 * q + g) * SK_PITCH + j * 16 + r] = dgh[g][j];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
+    }
+    // partials for the next step from this step's own dG columns
+    if (i + 1 < T && row0 < bs) {
       f4 acc[NSUB];
 #pragma unroll
       for (int j = 0; j < NSUB; ++j) acc[j] = f4zero();
@@ -649,20 +672,30 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
     }
     PSTAMP(3);
     group_publish(cnt);
-    // stashes for the weight-gradient GEMMs after the launch (plain stores,
-    // after the publish)
+    // stashes for the weight-gradient GEMMs after the launch (plain 16-B
+    // stores after the publish, read back from the dG tile: 16 rows x 4 gates
+    // x 4 quads of own units = 4 quads per lane).  LSTM: dGX = dGH = dG.
+    // GRU: dGH = (dr, dz, dn r) is the tile; dGX = (dr, dz, dn) takes gate 2
+    // from a transpose of dn.
+    if (row0 < bs) {
+      const __amdgpu_buffer_rsrc_t rx = make_rsrc(D.dGX + (size_t)o * GH, (uint32_t)bs * GH * 4u);
+      const __amdgpu_buffer_rsrc_t rh = make_rsrc(D.dGH + (size_t)o * GH, (uint32_t)bs * GH * 4u);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-      if (b >= bs) continue;
-      const long rr = o + b;
-      float* dx = D.dGX + rr * GH;
-#pragma unroll
-      for (int j = 0; j < G; ++j) dx[j * H + unit] = dgx[g][j];
+      for (int k2 = 0; k2 < 4; ++k2) {
+        const int k = lane + 64 * k2, row = k >> 4, gate = (k >> 2) & 3, qd = 4 * (k & 3);
+        if (gate >= G) continue;
+        const f4 v = *reinterpret_cast<const f4*>(Ast + row * SK_PITCH + gate * 16 + qd);
+        const uint32_t so = (uint32_t)((row0 + row) * GH + gate * H + u0 + qd) * 4u;
+        if (G == 3) {
+          st4(rh, so, v, false);
+          if (gate < 2) st4(rx, so, v, false);
+        } else {
+          st4(rx, so, v, false);
+        }
+      }
       if (G == 3) {
-        float* dhh = D.dGH + rr * GH;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) dhh[j * H + unit] = dgh[g][j];
+        const float dn[4] = {dgx[0][2], dgx[1][2], dgx[2][2], dgx[3][2]};
+        st4(rx, (uint32_t)((row0 + trow) * GH + 2 * H + u0 + tcol) * 4u, tp_quad(tb, dn, lane), false);
       }
     }
     PSTAMP(4);
@@ -1377,6 +1410,8 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
 // NXS: Fp/16 with self-feedback, else 0; NHS = H/16; NZ = 2Hm/32 (P2's K chunks).
 // ---------------------------------------------------------------------------
 constexpr int DSK_PITCH = 36;  // floats per row of the wave-private dG transpose
+constexpr int DSK_WAVE_FLOATS = 2 * TP_FLOATS;  // per-wave LDS region: the dG transpose or two tp_quad tiles
+static_assert(16 * DSK_PITCH <= DSK_WAVE_FLOATS, "dG transpose fits the wave's region");
 // acc += sum of NP partial f4s at base + p * 1 KiB, NB loads in flight
 template <int NP, int NB = NP>
 DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc, int rot = 0) {
@@ -1421,7 +1456,9 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
   f4* SK = smem;
   f4* B2 = SK + NS * 3 * 64;
   f4* B1 = B2 + NZ * 3 * 64;
-  float* Ast = reinterpret_cast<float*>(B1 + nchx * 64) + w * 16 * DSK_PITCH;
+  float* Ast = reinterpret_cast<float*>(B1 + nchx * 64) + w * DSK_WAVE_FLOATS;
+  float* tb = Ast;  // the same wave-private region, reused for the 16-B store transposes (tp_quad)
+  const int trow = lane >> 2, tcol = 4 * (lane & 3);
   // split-K image: subtile s, lane (rr, qq) holds rows k = 8qq + 0..7 (gate qq,
   // own units 0..7) of output column 16s + rr: [W_ih | W_hh]^T row (col) ...
   for (int e = threadIdx.x; e < NS * 64; e += 256) {
@@ -1484,20 +1521,22 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     if (mem < nFt) {
       f4 dx = f4zero();
       if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx, (a.exp & 1) ? mem % M : 0);
+      float dmu[4], dlv[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int b = row0 + 4 * q + g;
-        if (b >= bs) continue;
-        const long rr = o + b;
-        float dmu = 0.f, dlv = 0.f;
+        dmu[g] = dlv[g] = 0.f;
         if (col0 < F) {
           const float dxv = dx[g] * emk[g], mu = emu[g], lv = elv[g];
           const float iv = __expf(-lv), d = ey[g] - mu;
-          dmu = dxv + s_em * (-d) * iv;
-          dlv = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);
+          dmu[g] = dxv + s_em * (-d) * iv;
+          dlv[g] = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);
         }
-        st_sc1(a.dMU + rr * Fp + col0, dmu);
-        st_sc1(a.dLV + rr * Fp + col0, dlv);
+      }
+      const f4 mq = tp_quad(tb, dmu, lane), lq = tp_quad(tb + TP_FLOATS, dlv, lane);
+      if (row0 < bs) {  // rows >= bs fall outside the buffers' extent
+        const uint32_t qo = (uint32_t)((row0 + trow) * Fp + 16 * mem + tcol) * 4u;
+        st4(make_rsrc(a.dMU + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, mq, true);
+        st4(make_rsrc(a.dLV + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, lq, true);
       }
     }
     gs.publish();
@@ -1534,12 +1573,13 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
         mma16<1>(acc, A, row0 + r, B1, nchx, lane, q);
       }
       acc2_fold(acc);
+      float dz[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int b = row0 + 4 * q + g;
-        if (b >= bs) continue;
-        st_sc1(a.dZ + (long)(o + b) * 2 * Hm + 16 * mem + r, acc[0][0][g] * (1.f - zpre[g] * zpre[g]));
-      }
+      for (int g = 0; g < 4; ++g) dz[g] = acc[0][0][g] * (1.f - zpre[g] * zpre[g]);
+      const f4 zq = tp_quad(tb, dz, lane);
+      if (row0 < bs)
+        st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
+            (uint32_t)((row0 + trow) * 2 * Hm + 16 * mem + tcol) * 4u, zq, true);
     }
     gs.publish();
     PSTAMP(3);
@@ -1603,7 +1643,8 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     // after it and are drained by the next P0 publish
     const bool mk = i + 1 < T && row0 < bs;
     bf8 a0, a1, a2;
-    if (mk) {
+    if (row0 < bs) {  // dG tile of the wave: rows x [gate j][own unit], read back below for the split and the stash
+      __builtin_amdgcn_wave_barrier();
       if (lo) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -1612,6 +1653,8 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
+    }
+    if (mk) {
       const float* ar = Ast + r * DSK_PITCH + 8 * q;
       split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
     }
@@ -1633,22 +1676,22 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
 #pragma unroll
       for (int s = NXS; s < NS; ++s) partial(s);
     }
-    // stash for the weight-gradient GEMMs and the initial-state gradient (plain stores, after the publish)
-    if (lo) {
+    // stash for the weight-gradient GEMMs (plain 16-B stores, after the
+    // publish), straight from the dG tile in LDS: 16 rows x 4 gates x 2 quads
+    // of own units = 2 quads per lane
+    if (row0 < bs) {
+      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.dG + (size_t)o * GH, (uint32_t)bs * GH * 4u);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int b = row0 + 4 * q + g;
-        if (b >= bs) continue;
-        float* dg = a.dG + (long)(o + b) * GH;
-        if constexpr (GRU) {
-          float* dgr = a.dGH + (long)(o + b) * GH;
-          dg[unit] = dgr[unit] = dgh[g][0];
-          dg[H + unit] = dgr[H + unit] = dgh[g][1];
-          dg[2 * H + unit] = dgh[g][2];
-          dgr[2 * H + unit] = dgh[g][3];
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int k = lane + 64 * k2, row = k >> 3, gate = (k >> 1) & 3, hf = 4 * (k & 1);
+        const f4 v = *reinterpret_cast<const f4*>(Ast + row * DSK_PITCH + 8 * gate + hf);
+        const uint32_t so = (uint32_t)((row0 + row) * GH + u0 + hf) * 4u;
+        if constexpr (GRU) {  // dGX = (dr, dz, dn), dGH = (dr, dz, dn r)
+          const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.dGH + (size_t)o * GH, (uint32_t)bs * GH * 4u);
+          if (gate < 3) st4(rg, so + (uint32_t)(gate * H) * 4u, v, false);
+          if (gate != 2) st4(rh, so + (uint32_t)((gate == 3 ? 2 : gate) * H) * 4u, v, false);
         } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) dg[j * H + unit] = dgh[g][j];
+          st4(rg, so + (uint32_t)(gate * H) * 4u, v, false);
         }
       }
     }
@@ -1830,7 +1873,7 @@ static bool x6_enabled(int K) { return K == 64 || K == 128 || K == 256; }
 template <int G, int PD, int X6>
 static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * (a.H / 16);
-  const size_t lds = (size_t)G * 16 * a.H * (X6 ? 6 : 4);
+  const size_t lds = (size_t)G * 16 * a.H * (X6 ? 6 : 4) + (size_t)4 * TP_FLOATS * 4;
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD, X6>, grid, lds, &ok));
   if (!ok) return 0;
@@ -1893,7 +1936,7 @@ int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched)
 template <int G, int NSUB>
 static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * NSUB;
-  const size_t lds = (size_t)NSUB * 2 * 3 * 64 * 16 + (size_t)4 * 16 * SK_PITCH * 4;
+  const size_t lds = (size_t)NSUB * 2 * 3 * 64 * 16 + (size_t)4 * 16 * SK_PITCH * 4 + (size_t)4 * TP_FLOATS * 4;
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(enc_bwd_sk<G, NSUB>, grid, lds, &ok));
   if (!ok) return 0;
@@ -2033,7 +2076,7 @@ int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launch
 template <int NXS, int NHS, int NZ, bool GRU = false>
 static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   constexpr int NS = NXS + NHS, M = NHS * 2;
-  const size_t lds = (size_t)(NS + NZ) * 3 * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * 16 * DSK_PITCH * 4;
+  const size_t lds = (size_t)(NS + NZ) * 3 * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * DSK_WAVE_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(dec_bwd_sk<NXS, NHS, NZ, GRU>, grid, lds, &ok));
