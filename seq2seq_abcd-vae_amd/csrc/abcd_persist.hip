@@ -1448,8 +1448,6 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
   GSync gs{a.sync + grp * PERSIST_SYNC_STRIDE,
            a.sync + ((size_t)2 * a.nrt + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
            M, mem, a.flags, 0u};
-  // second counter: +1 per member once its dh partials of the previous step are drained
-  unsigned* cnt2 = a.sync + (a.nrt + PERSIST_REG_LINES + grp) * PERSIST_SYNC_STRIDE;
   const int u0 = mem * 8, unit = u0 + (r & 7);
   const bool lo = r < 8;
   // LDS: split-K image [NS][3][64] | P2 image [NZ][3][64] | P1 image [nchx][64] | dG transposes [4][16][PITCH]
@@ -1511,12 +1509,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       ey[g] = live ? a.Y[rr * F + col0] : 0.f;
       emk[g] = (a.xmask && live && b < succ_valid) ? a.xmask[(long)(o + bs + b) * F + col0] : 1.f;
     }
-    if (i > 0) {
-      gs.wait(3u * i);
-      // the dh partials stored after the previous P2 publish have had a whole
-      // hand-off to land: drain and announce them on the second counter
-      group_publish(cnt2);
-    }
+    if (i > 0) gs.wait(3u * i);
     PSTAMP(0);
     if (mem < nFt) {
       f4 dx = f4zero();
@@ -1541,20 +1534,6 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     }
     gs.publish();
     PSTAMP(1);
-    // dh_rec of the own units from step t+1's partials (lane takes column
-    // (mem & 1) * 8 + (r & 7) of subtile NXS + mem / 2 from each producer):
-    // members without P0 work overlap it with the P0 members' work, the P0
-    // members with the hand-off latency into P1 (measured: reading it after
-    // the P1 publish instead is no faster)
-    f4 dhr = f4zero();
-    auto read_dhr = [&]() {
-      if (i > 0) group_wait(cnt2, (unsigned)(M * i));  // every wave: it holds a workgroup barrier
-      if (has_part) {
-        const int pl = q * 16 + (mem & 1) * 8 + (r & 7);
-        sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr, (a.exp & 1) ? mem % M : 0);
-      }
-    };
-    read_dhr();
     PSTAMP(6);
     // ---------------- P1: dZ tile ----------------
     float zpre[4];
@@ -1583,6 +1562,16 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     }
     gs.publish();
     PSTAMP(3);
+    // dh_rec of the own units from step t+1's partials (lane takes column
+    // (mem & 1) * 8 + (r & 7) of subtile NXS + mem / 2 from each producer),
+    // loaded across the P1 -> P2 hand-off.  The producers stored them after
+    // their P2 publish of step t+1; their P0 publish of this step drained them
+    // (vmcnt(0)), and the P1 wait above saw every member's P0 publish.
+    f4 dhr = f4zero();
+    if (has_part) {
+      const int pl = q * 16 + (mem & 1) * 8 + (r & 7);
+      sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr, (a.exp & 1) ? mem % M : 0);
+    }
     // ---------------- P2: dh -> cell backward -> dG_t -> partials ----------------
     float pg[4][4], pc[4], pcp[4], pdho[4];
 #pragma unroll
