@@ -135,6 +135,17 @@ int abcd_sampler_sample(const abcd_sampler_cfg* cfg, const abcd_sampler_params* 
 /* replaces ABCDSampler.kl_divergence (model.py:608-639) / plain kl: writes a device scalar */
 int abcd_sampler_kl(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* logits, int B,
                     double entire_data_size, float* kl_out, void* ws, size_t ws_bytes, void* stream);
+/* forward + sample + kl of one training step (learning.py:149-153 calls
+ * feature_sampler(h), .sample(logits), .kl_divergence(logits, N) in turn):
+ * logits B x K, feats B x D and the KL scalar (kl_out may be NULL), the same
+ * values and backward stash as the three calls above.  ABCD: two launches --
+ * the split-K h W1^T GEMM and one row-tiled sampler-head kernel (MLP tail,
+ * logits, Gumbel-softmax, y C^T and the KL row terms per 16-row tile, the KL
+ * scalar reduced by the last tile).  plain: the three calls in turn. */
+int abcd_sampler_forward_fused(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
+                               int mode, float temperature, const float* noise, uint64_t seed, uint64_t offset,
+                               double entire_data_size, float* logits, float* feats, float* kl_out, void* ws,
+                               size_t ws_bytes, void* stream);
 /* backward of forward+sample+kl.  d_feats: B x D (may be NULL); d_kl: device
  * scalar upstream grad of kl (may be NULL); d_h: B x E (may be NULL). */
 int abcd_sampler_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
@@ -144,6 +155,10 @@ int abcd_sampler_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params
 /* the same, with the parameter gradients (codebook, posterior_shape_logits,
  * MLP weights and biases) queued on wgrad_stream (NULL or == stream: one
  * stream) after an event on `stream`; only the d_h chain stays on `stream`.
+ * ABCD with d_feats and d_kl: one row-tiled sampler-head backward kernel
+ * (d_logits, dU, dZ1, the bias / prior column sums and d posterior_shape_logits
+ * in its last tile) + the d_h GEMM on `stream`; codebook / W2 / W1 GEMMs on
+ * wgrad_stream.
  * The caller joins wgrad_stream before reading the gradients. */
 int abcd_sampler_backward_split(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
                                 int mode, float temperature, double entire_data_size, const float* d_feats,

@@ -175,6 +175,18 @@ DEV float philox_gumbel(uint64_t seed, uint64_t idx) {
   return -__logf(fmaxf(e, 1e-30f));
 }
 
+// Buffer resource over [p, p + bytes): loads beyond it return 0.
+// The descriptor must live in SGPRs: its inputs are wave-uniform, but when
+// divergence analysis cannot prove it the compiler wraps every load in a
+// readfirstlane "waterfall" loop -- so make the uniformity explicit.
+DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 inline int rup16(int x) { return (x + 15) & ~15; }
 

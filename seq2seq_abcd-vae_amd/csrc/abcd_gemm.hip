@@ -616,6 +616,28 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
                      e, scratch, scratch_floats);
 }
 
+// A B^T as raw split-K partial slabs (no epilogue): slab[z][m*N + n] for
+// z < *zout, K split the way gemm() splits a small-M product; the consumer
+// sums the slabs (the sampler head fuses that reduce into its prologue).
+int gemm_slabs(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* slab, size_t slab_floats, int* zout) {
+  ABCD_REQUIRE(M > 0 && N > 0 && K > 0 && K % 16 == 0 && !A.kmajor && !B.kmajor && slab && zout);
+  ABCD_REQUIRE(A.ld % 4 == 0 && B.ld % 4 == 0 && ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0);
+  const long per = (long)M * N;
+  ABCD_REQUIRE((long)slab_floats >= per);
+  const int nch = K / 16, tiles = cdiv(M, 32) * cdiv(N, 64);
+  int Z = std::min(cdiv(1024, tiles), std::max(1, nch / 8));
+  Z = (int)std::max<long>(1, std::min<long>(Z, (long)slab_floats / per));
+  const int cps = cdiv(nch, Z);
+  Z = cdiv(nch, cps);
+  EpiArgs e{nullptr, N, M, N, 1.f, 0.f, nullptr, ACT_NONE, slab};
+  dim3 grid(cdiv(N, 64), cdiv(M, 32), Z);
+  gemm_ks_kernel<2, 4, KC, KC><<<grid, 256, 0, s>>>(KC{A.p, A.ld, std::min(A.nrows, M)},
+                                                    KC{B.p, B.ld, std::min(B.nrows, N)}, nch, cps, e);
+  ABCD_CHECK_LAUNCH();
+  *zout = Z;
+  return 0;
+}
+
 size_t gemm_scratch_floats_hint(int M, int N, int K) { return (size_t)M * N * 16; }
 
 // ---------------------------------------------------------------------------

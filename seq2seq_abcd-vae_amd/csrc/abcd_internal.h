@@ -38,6 +38,9 @@ inline Operand opKM(const float* p, long ld, int nrows) { return Operand{p, ld, 
 int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, long ldc, float alpha,
          float beta, const float* bias, int act, float* scratch, size_t scratch_floats);
 
+// A B^T (both K-contiguous) as raw split-K slabs slab[z][m*N + n], z < *zout.
+int gemm_slabs(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* slab, size_t slab_floats, int* zout);
+
 // out[j] (+)= sum_r w[r] * Z[r*ldz + j]  (w == null -> 1), j < ncols, r < nrows; deterministic.
 // out2 (optional) receives the same sum with the same beta (e.g. b_ih and b_hh of an LSTM).
 int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const float* w, float* out,
@@ -122,7 +125,11 @@ namespace abcd {
 // Optional live timing of the recurrent kernel family (bench.py roofline):
 // when enabled, a HIP event pair brackets every launch inside TimedScope,
 // tagged with the kernel id (TK_*) so one kernel can be read back alone.
-enum TimedKernel { TK_STEP = 0, TK_ENC_FWD = 1, TK_ENC_BWD = 2, TK_DEC_FWD = 3, TK_DEC_BWD = 4, TK_N = 5 };
+enum TimedKernel {
+  TK_STEP = 0, TK_ENC_FWD = 1, TK_ENC_BWD = 2, TK_DEC_FWD = 3, TK_DEC_BWD = 4,
+  TK_SAMP_FWD = 5, TK_SAMP_BWD = 6,  // dispatch records only (no live timing)
+  TK_N = 7
+};
 bool timing_on();
 void timing_mark(hipStream_t s, int kid);
 // records which kernel (template instance) a role's last launch ran, so the

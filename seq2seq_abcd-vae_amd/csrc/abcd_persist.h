@@ -30,7 +30,6 @@ struct PFwdArgs {
   const int* off;    // device: off[0..T]
   unsigned* sync;    // one 128-B counter line per group, zeroed before the launch
   unsigned long long* prof;  // diagnostics: per-step s_memtime stamps, or null
-  int exp;                   // experiment bits (ABCD_EXP, A/B timing only)
 };
 
 // One direction of an encoder layer, backward (BPTT).
@@ -48,7 +47,6 @@ struct PBwdArgs {
   const int* off;
   unsigned* sync;
   unsigned long long* prof;
-  int exp;
   float* part;       // split-K partials: 2 parity slots x groups x H/16 consumers x 4 waves x H/16 producers x 256
 };
 
@@ -60,7 +58,6 @@ struct PBwdArgs {
 struct PDecFwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
   int flags;                       // hand-off form: 1 per-member flags, 0 group counter
-  int exp;
   const int* off;
   unsigned* sync;
   unsigned long long* prof;
@@ -79,7 +76,6 @@ struct PDecFwdArgs {
 struct PDecBwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
   int flags;                       // hand-off form: 1 per-member flags, 0 group counter
-  int exp;
   const int* off;
   unsigned* sync;
   unsigned long long* prof;

@@ -44,16 +44,6 @@ __device__ unsigned g_spin_limit = 1u << 22;    // polls before a hand-off wait 
 // ---------------------------------------------------------------------------
 // hand-off primitives
 // ---------------------------------------------------------------------------
-// The descriptor must live in SGPRs: its inputs are wave-uniform, but when
-// divergence analysis cannot prove it the compiler wraps every load in a
-// readfirstlane "waterfall" loop -- so make the uniformity explicit.
-DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
-  const uint64_t v = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
-}
 // K-contiguous operand read through a buffer resource with `sc1` (bypasses
 // this CU's L1, so it sees other workgroups' write-through stores); rows at
 // or beyond the resource's extent read as zero (hardware range check).
@@ -299,8 +289,7 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
       const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u),
                     (uint32_t)H * 4u};
       if (X6) {
-        wave_mma_x6<G, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q,
-                                             (a.exp & 1) ? mem % (X6 > 0 ? X6 : 1) : 0);
+        wave_mma_x6<G, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q);
       } else {
         wave_mma_lds<G, PD>(acc, A, row0 + r, smem, nch, lane, q);
       }
@@ -1063,9 +1052,9 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         acc[0] = acch[0];
         acc[1] = acch[1];
         if constexpr (NXC > 0)
-          wave_mma_x6<2, (NXC > 0 ? NXC : 1), 8>(acc, A, row0 + r, BC, NCC, lane, q, (a.exp & 1) ? mem % NXC : 0);
+          wave_mma_x6<2, (NXC > 0 ? NXC : 1), 8>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC);
       } else {
-        wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q, (a.exp & 1) ? mem % NCC : 0);
+        wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q, mem % NCC);
       }
     }
     PSTAMP(7);
@@ -1132,12 +1121,12 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
-          wave_mma_x6p<3, NH32, 8>(a3, Hs, row0 + r, bp, lane, q, (a.exp & 1) ? mem % NH32 : 0);
+          wave_mma_x6p<3, NH32, 8>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
           a1[0] = a3[0];
           acch[0] = a3[1];
           acch[1] = a3[2];
         } else {
-          wave_mma_x6<1, NH32, 8>(a1, Hs, row0 + r, B1, NH32, lane, q, (a.exp & 1) ? mem % NH32 : 0);
+          wave_mma_x6<1, NH32, 8>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32);
         }
       }
       PSTAMP(6);
@@ -1172,7 +1161,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
                        (uint32_t)2 * Hm * 4u};
         wave_mma_x6<1, NM32, 8>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
-                                (a.exp & 1) ? mem % NM32 : 0);
+                                mem % NM32);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) ev[g] = col2 < F ? ae[0][g] + b2v : 0.f;
@@ -1513,7 +1502,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     PSTAMP(0);
     if (mem < nFt) {
       f4 dx = f4zero();
-      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx, (a.exp & 1) ? mem % M : 0);
+      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx, mem % M);
       float dmu[4], dlv[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1570,7 +1559,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     f4 dhr = f4zero();
     if (has_part) {
       const int pl = q * 16 + (mem & 1) * 8 + (r & 7);
-      sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr, (a.exp & 1) ? mem % M : 0);
+      sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr, mem % M);
     }
     // ---------------- P2: dh -> cell backward -> dG_t -> partials ----------------
     float pg[4][4], pc[4], pcp[4], pdho[4];
@@ -1591,7 +1580,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     f4 acc[1] = {f4zero()};
     if (row0 < bs) {
       const BufKC Az{make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u), (uint32_t)2 * Hm * 4u};
-      wave_mma_x6<1, NZ, 8>(acc, Az, row0 + r, B2, NZ, lane, q, (a.exp & 1) ? mem % NZ : 0);
+      wave_mma_x6<1, NZ, 8>(acc, Az, row0 + r, B2, NZ, lane, q, mem % NZ);
     }
     PSTAMP(7);
     float dgh[4][4];
@@ -1815,12 +1804,6 @@ __global__ __launch_bounds__(256) void persist_reset(unsigned* sync, long nwords
 // ABCD_SPIN_LIMIT=<polls> (debug/tests): shrink the hand-off spin bound so a
 // wait times out at once; the device word is only rewritten when the value
 // changes (never in a default run)
-// ABCD_EXP (A/B experiments only): bit 0 rotates each consumer's read order
-static int exp_bits() {
-  const char* v = getenv("ABCD_EXP");
-  return v ? atoi(v) : 0;
-}
-
 static int sync_spin_limit(hipStream_t s) {
   static unsigned cur = 1u << 22, staged;
   const char* v = getenv("ABCD_SPIN_LIMIT");
@@ -1869,7 +1852,6 @@ static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PFwdArgs b = a;
   b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
-  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_ENC_FWD);
     enc_fwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
@@ -1889,7 +1871,6 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
-  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_ENC_BWD);
     enc_bwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
@@ -1932,7 +1913,6 @@ static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
-  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_ENC_BWD);
     enc_bwd_sk<G, NSUB><<<grid, 256, lds, s>>>(b);
@@ -1993,7 +1973,6 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   PDecFwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
-  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_DEC_FWD);
     dec_fwd_persist<NCC><<<grid, 256, lds, s>>>(b);
@@ -2016,7 +1995,6 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
   PDecFwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
-  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_DEC_FWD);
     dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
@@ -2074,7 +2052,6 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   PDecBwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
-  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_DEC_BWD);
     dec_bwd_sk<NXS, NHS, NZ, GRU><<<grid, 256, lds, s>>>(b);
@@ -2117,7 +2094,6 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   PDecBwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
-  b.exp = exp_bits();
   {
     TimedScope ts(s, TK_DEC_BWD);
     dec_bwd_persist<<<grid, 256, lds, s>>>(b);

@@ -9,6 +9,8 @@
 #include "abcd_common.h"
 #include "abcd_internal.h"
 
+#include <mutex>
+
 namespace abcd {
 
 // ---- special functions (fp64, x > 0) --------------------------------------
@@ -68,67 +70,82 @@ __global__ void sample_softmax_rows(const float* logits, int B, int K, int gumbe
   for (int k = lane; k < K; k += 64) y[k] *= is;
 }
 
-// KL prior part (one block): p = softmax(psl), alpha = p N + a0, elog = psi(alpha) - psi(S)
-// kl_small: [0] = (Eq log q(pi) - Eq log p(pi)), [1] = psi'(S), [2] = S
+// Block reductions (blockDim = 64 x nw, nw <= 16); `sh` holds 16 doubles.
+// Every thread returns the block-wide value.
+DEV double block_sum_dd(double v, double* sh) {
+  const int nw = blockDim.x >> 6;
+  v = wave_sum_d(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < nw; ++i) t += sh[i];
+  return t;
+}
+DEV double block_max_dd(double v, double* sh) {
+  const int nw = blockDim.x >> 6;
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double t = sh[0];
+  for (int i = 1; i < nw; ++i) t = fmax(t, sh[i]);
+  return t;
+}
+
+// KL prior part (model.py:620-633), one block: p = softmax(psl),
+// alpha = p N + a0, elog = psi(alpha) - psi(S).  alphaL / elogL: K floats of
+// block-shared scratch receiving alpha and elog (as fp32, the values the row
+// terms use).  stash: also p / alpha / elog / tri to global and
+// kl_small = [Eq log q(pi) - Eq log p(pi), psi'(S), S].
+DEV void prior_block(const float* psl, int K, double N, float a0, float* alphaL, float* elogL, double* sh,
+                     bool stash, float* p_out, float* alpha_out, float* elog_out, float* tri_out,
+                     double* kl_small) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  double m = -1e300;
+  for (int k = tid; k < K; k += nt) m = fmax(m, (double)psl[k]);
+  m = block_max_dd(m, sh);
+  double se = 0.0;
+  for (int k = tid; k < K; k += nt) se += exp((double)psl[k] - m);
+  se = block_sum_dd(se, sh);
+  double sa = 0.0;
+  for (int k = tid; k < K; k += nt) {
+    const double p = exp((double)psl[k] - m) / se;
+    const double al = (double)(float)((float)p * (float)N) + (double)a0;  // the product in fp32 like the reference
+    alphaL[k] = (float)al;
+    if (stash) { p_out[k] = (float)p; alpha_out[k] = (float)al; }
+    sa += al;
+  }
+  sa = block_sum_dd(sa, sh);
+  const double S = sa, psiS = digamma_d(S);
+  double acc = 0.0;  // -sum lgamma(alpha) + sum (alpha-1) elog - (a0-1) sum elog
+  for (int k = tid; k < K; k += nt) {
+    const double al = alphaL[k];
+    const double el = digamma_d(al) - psiS;
+    elogL[k] = (float)el;
+    if (stash) {
+      elog_out[k] = (float)el;
+      tri_out[k] = (float)trigamma_d(al);
+      acc += -lgamma(al) + (al - 1.0) * el - ((double)a0 - 1.0) * el;
+    }
+  }
+  if (stash) {
+    acc = block_sum_dd(acc, sh);
+    if (tid == 0) {
+      const double a0d = a0;
+      kl_small[0] = lgamma(S) + acc - (lgamma(a0d * K) - K * lgamma(a0d));
+      kl_small[1] = trigamma_d(S);
+      kl_small[2] = S;
+    }
+  }
+  __syncthreads();
+}
+
+// standalone form (abcd_sampler_kl): alpha / elog land in the global stash
 __global__ void kl_prior(const float* psl, int K, double N, float a0, float* p_out, float* alpha_out,
                          float* elog_out, float* tri_out, double* kl_small) {
   __shared__ double sh[16];
-  __shared__ double bc[4];
-  const int tid = threadIdx.x;
-  // softmax(psl) in double
-  double m = -1e300;
-  for (int k = tid; k < K; k += blockDim.x) m = fmax(m, (double)psl[k]);
-  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
-  if ((tid & 63) == 0) sh[tid >> 6] = m;
-  __syncthreads();
-  if (tid == 0) { double t = sh[0]; for (int i = 1; i < (int)(blockDim.x >> 6); ++i) t = fmax(t, sh[i]); bc[0] = t; }
-  __syncthreads();
-  m = bc[0];
-  double se = 0.0;
-  for (int k = tid; k < K; k += blockDim.x) se += exp((double)psl[k] - m);
-  se = wave_sum_d(se);
-  __syncthreads();
-  if ((tid & 63) == 0) sh[tid >> 6] = se;
-  __syncthreads();
-  if (tid == 0) { double t = 0; for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i]; bc[1] = t; }
-  __syncthreads();
-  se = bc[1];
-  double sa = 0.0;
-  for (int k = tid; k < K; k += blockDim.x) {
-    const double p = exp((double)psl[k] - m) / se;
-    const double al = (double)(float)((float)p * (float)N) + (double)a0;  // fp32 like the reference
-    p_out[k] = (float)p;
-    alpha_out[k] = (float)al;
-    sa += al;
-  }
-  sa = wave_sum_d(sa);
-  __syncthreads();
-  if ((tid & 63) == 0) sh[tid >> 6] = sa;
-  __syncthreads();
-  if (tid == 0) { double t = 0; for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i]; bc[2] = t; }
-  __syncthreads();
-  const double S = bc[2];
-  const double psiS = digamma_d(S);
-  double acc = 0.0;  // -sum lgamma(alpha) + sum (alpha-1) elog - (a0-1) sum elog
-  for (int k = tid; k < K; k += blockDim.x) {
-    const double al = alpha_out[k];
-    const double el = digamma_d(al) - psiS;
-    elog_out[k] = (float)el;
-    tri_out[k] = (float)trigamma_d(al);
-    acc += -lgamma(al) + (al - 1.0) * el - ((double)a0 - 1.0) * el;
-  }
-  acc = wave_sum_d(acc);
-  __syncthreads();
-  if ((tid & 63) == 0) sh[tid >> 6] = acc;
-  __syncthreads();
-  if (tid == 0) {
-    double t = 0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
-    const double a0d = a0;
-    kl_small[0] = lgamma(S) + t - (lgamma(a0d * K) - K * lgamma(a0d));
-    kl_small[1] = trigamma_d(S);
-    kl_small[2] = S;
-  }
+  prior_block(psl, K, N, a0, alpha_out, elog_out, sh, true, p_out, alpha_out, elog_out, tri_out, kl_small);
 }
 
 // per row: Q = softmax(l); v_b = sum_k Q (log Q - elog)
@@ -200,41 +217,34 @@ __global__ void kl_rows_bwd(const float* Q, const float* elog, const float* v, i
   }
 }
 
-// d posterior_shape_logits (one block)
-__global__ void kl_prior_bwd(const float* p, const float* alpha, const float* tri, const double* kl_small,
-                             const float* Qsum, int K, int B, double N, float a0, const float* dkl, float* dpsl) {
-  __shared__ double sh[16];
-  __shared__ double bc[2];
-  const int tid = threadIdx.x;
-  const double s = *dkl;
+// d posterior_shape_logits (model.py:620-633 backward), one block; Qsum[k] =
+// sum_b Q(b, k) (global or block-shared)
+DEV void prior_bwd_block(const float* p, const float* alpha, const float* tri, const double* kl_small,
+                         const float* Qsum, int K, int B, double N, float a0, float dkl, float* dpsl, double* sh) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const double s = dkl;
   const double r = (double)B / N;
   double sde = 0.0;
-  for (int k = tid; k < K; k += blockDim.x) sde += r * ((double)alpha[k] - a0) - Qsum[k];
-  sde = wave_sum_d(sde);
-  if ((tid & 63) == 0) sh[tid >> 6] = sde;
-  __syncthreads();
-  if (tid == 0) { double t = 0; for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i]; bc[0] = t; }
-  __syncthreads();
-  sde = bc[0];
+  for (int k = tid; k < K; k += nt) sde += r * ((double)alpha[k] - a0) - Qsum[k];
+  sde = block_sum_dd(sde, sh);
   const double triS = kl_small[1];
   double spd = 0.0;
-  for (int k = tid; k < K; k += blockDim.x) {
+  for (int k = tid; k < K; k += nt) {
     const double de = r * ((double)alpha[k] - a0) - Qsum[k];
     const double da = s * (de * tri[k] - triS * sde);
     spd += (double)p[k] * da * N;
   }
-  spd = wave_sum_d(spd);
-  __syncthreads();
-  if ((tid & 63) == 0) sh[tid >> 6] = spd;
-  __syncthreads();
-  if (tid == 0) { double t = 0; for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i]; bc[1] = t; }
-  __syncthreads();
-  spd = bc[1];
-  for (int k = tid; k < K; k += blockDim.x) {
+  spd = block_sum_dd(spd, sh);
+  for (int k = tid; k < K; k += nt) {
     const double de = r * ((double)alpha[k] - a0) - Qsum[k];
     const double da = s * (de * tri[k] - triS * sde);
     dpsl[k] = (float)((double)p[k] * (da * N - spd));
   }
+}
+__global__ void kl_prior_bwd(const float* p, const float* alpha, const float* tri, const double* kl_small,
+                             const float* Qsum, int K, int B, double N, float a0, const float* dkl, float* dpsl) {
+  __shared__ double sh[16];
+  prior_bwd_block(p, alpha, tri, kl_small, Qsum, K, B, N, a0, *dkl, dpsl, sh);
 }
 
 __global__ void tanh_bwd_inplace(float* dz, const float* z, long n) {
@@ -286,11 +296,590 @@ __global__ void plain_dparams(const float* MV, const float* EPS, int B, int f, c
   }
 }
 
+// ---------------------------------------------------------------------------
+// Sampler head: the ABCD sampler's forward (model.py:581-606 + the KL row
+// terms of 608-639) and its backward as ONE row-tiled kernel each.  A
+// workgroup owns 16 rows of the batch; every intermediate of those rows
+// (Z1 -> U -> logits -> Q, Y -> feats) stays in LDS between the four
+// products, which run on the exact-fp32 16x16x4 MFMA with the weights /
+// codebook streamed from L2 as B operands (4 waves split the output columns,
+// a 4-chunk register ring per wave).  The only grid-wide results -- the KL
+// scalar and (backward) the bias / Qsum column sums feeding the Dirichlet
+// prior gradient -- are reduced by the last workgroup to finish, over the
+// per-tile partials in tile order (deterministic, no float atomics).
+// Forward = the split-K h W1^T GEMM (raw slabs) + samp_head_fwd; backward =
+// samp_head_bwd + the d_h GEMM, with the parameter-gradient GEMMs on the
+// side stream.
+// ---------------------------------------------------------------------------
+constexpr int HEAD_ROWS = 16;
+// "last workgroup" tickets (self-resetting): [0] forward KL, [1] backward
+// column sums.  Launches on one device are serialised on the engine's stream.
+__device__ unsigned g_head_ticket[2];
+
+struct LdsRows {  // A operand: 16 rows resident in LDS, row pitch ld floats
+  const float* p; int ld;
+  DEV f4 frag(int row, int kc, int q) const { return *reinterpret_cast<const f4*>(p + row * ld + kc * 16 + 4 * q); }
+};
+
+// B operands of the tile products, read through buffer resources so every
+// load is unconditional (out-of-range lanes / chunks read 0): a load under a
+// divergent or conditional branch leaves the wait-count pass unsure of the
+// in-order count and it falls back to vmcnt(0) before every chunk, which
+// serialises the register ring behind one memory round trip per chunk.
+struct BKC {  // B(n, k) at p[n * ld + k] (16-B loads along k); rsrc covers ncols rows
+  __amdgpu_buffer_rsrc_t rs; uint32_t ld4;
+  DEV f4 frag(int n, int kc, int q, bool ok) const {
+    const uint32_t o = ok ? (uint32_t)n * ld4 + (uint32_t)(kc * 16 + 4 * q) * 4u : 0x80000000u;
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+  }
+};
+struct BKM {  // B(n, k) at p[k * ld + n] (4-B loads, 16 lanes over 16 consecutive n)
+  __amdgpu_buffer_rsrc_t rs; uint32_t ld4;
+  DEV f4 frag(int n, int kc, int q, bool ok) const {
+    f4 v;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t o = ok ? (uint32_t)(kc * 16 + 4 * q + t) * ld4 + (uint32_t)n * 4u : 0x80000000u;
+      v[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0));
+    }
+    return v;
+  }
+};
+DEV BKC bkc(const float* p, int ld, int nrows) { return BKC{make_rsrc(p, (uint32_t)nrows * ld * 4u), (uint32_t)ld * 4u}; }
+DEV BKM bkm(const float* p, int ld, int nk) { return BKM{make_rsrc(p, (uint32_t)nk * ld * 4u), (uint32_t)ld * 4u}; }
+
+// out(r, n) = sum_k A(r, k) B(n, k) for the tile's 16 rows, n < ncols
+// (multiple of 16), k < nk (multiple of 16); A: the 16 rows in LDS (pitch
+// lda floats).  Wave w takes the 16-column subtiles w*NR.., (w+4)*NR..;
+// epi(c0, acc): lane (r, q) holds rows 4q+g of column c0 + r.  PD chunks of
+// A and B fragments in flight per wave, branch-free.
+template <int NR, int PD, class OB, class Epi>
+DEV void tile_mma(const float* Al, int lda, int nk, const OB& B, int ncols, int w, int lane, Epi&& epi) {
+  const int r = lane & 15, q = lane >> 4;
+  const int nsub = ncols >> 4, nch = nk >> 4;
+  for (int j0 = w * NR; j0 < nsub; j0 += 4 * NR) {
+    f4 acc[NR];
+    int bn[NR];
+    bool bok[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      acc[j] = f4zero();
+      bn[j] = (j0 + j) * 16 + r;
+      bok[j] = bn[j] < ncols;
+    }
+    f4 a[PD], b[PD][NR];
+    auto fetch = [&](int p, int kc) {
+      const bool ok = kc < nch;
+      const f4 av = *reinterpret_cast<const f4*>(Al + r * lda + (ok ? kc : 0) * 16 + 4 * q);
+      a[p] = ok ? av : f4zero();
+#pragma unroll
+      for (int j = 0; j < NR; ++j) b[p][j] = B.frag(bn[j], kc, q, ok && bok[j]);
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) fetch(p, p);
+    for (int base = 0; base < nch; base += PD) {
+#pragma unroll
+      for (int p = 0; p < PD; ++p) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < NR; ++j) acc[j] = mfma4(a[p][t], b[p][j][t], acc[j]);
+        fetch(p, base + p + PD);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      if (j0 + j < nsub) epi((j0 + j) * 16, acc[j]);
+  }
+}
+template <class OB, class Epi>
+DEV void tile_mma_any(const float* Al, int lda, int nk, const OB& B, int ncols, int w, int lane, Epi&& epi) {
+  tile_mma<2, 4>(Al, lda, nk, B, ncols, w, lane, epi);
+}
+// sum over the 16 rows a lane group holds (rows 4q+g): every lane of the
+// column gets the column's tile sum
+DEV float tile_colsum(f4 v) {
+  float c = (v[0] + v[1]) + (v[2] + v[3]);
+  c += __shfl_xor(c, 16, 64);
+  c += __shfl_xor(c, 32, 64);
+  return c;
+}
+// true in every thread of the last workgroup to call it (after this
+// workgroup's global stores); that workgroup then reads the others' partials
+// with agent-scope loads
+DEV bool last_workgroup(unsigned* ticket, int* flag_sh) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned n = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = n == gridDim.x - 1;
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_sh = last;
+  }
+  __syncthreads();
+  const bool last = *flag_sh != 0;
+  if (last) __threadfence();
+  return last;
+}
+template <class T>
+DEV T ld_agent(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <class T>
+DEV void st_agent(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+constexpr int HEAD_MAX_SLABS = 8;  // split-K slabs the forward head sums (gemm_slabs' cap)
+
+struct HeadFwdArgs {
+  int B, Hm, D, K, nslab;
+  const float *slab, *b1, *W2, *b2, *C, *psl;  // slab: nslab x B x Hm raw partials of h W1^T
+  double N; float a0;
+  int gumbel; float tau; const float* noise; uint64_t seed, offset;
+  float *Z1, *U, *logits, *Y, *Q, *v, *feats;
+  float *p, *alpha, *elog, *tri; double* kl_small;  // prior stash (written by workgroup 0)
+  double* klpart;                                   // per-tile sum_b v_b
+  float* kl_out;
+  float *CT, *W2T;   // K x D and Hm x D transposed copies for the backward (each tile writes a slice)
+};
+inline size_t head_fwd_lds(int Hm, int D, int K) {
+  return ((size_t)HEAD_ROWS * (std::max(Hm, K) + 4) + (size_t)HEAD_ROWS * (std::max(D, K) + 4) + 2 * (size_t)K) * 4 +
+         16 * sizeof(double) + 16;
+}
+
+// KPL: categories per lane, ceil(K / 64) rounded up to a power of two
+template <int KPL>
+__global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  const int Hm = a.Hm, D = a.D, K = a.K;
+  const int ld1 = max(Hm, K) + 4, ld2 = max(D, K) + 4;
+  float* R1 = hsm;                   // Z1, then logits
+  float* R2 = R1 + HEAD_ROWS * ld1;  // U, then Y
+  float* alphaL = R2 + HEAD_ROWS * ld2;
+  float* elogL = alphaL + K;
+  double* sh = reinterpret_cast<double*>(elogL + K);
+  int* flag = reinterpret_cast<int*>(sh + 16);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
+  const int row0 = blockIdx.x * HEAD_ROWS, nr = min(HEAD_ROWS, a.B - row0);
+  // Prologue, one memory round trip per iteration: (a) this tile's slice of
+  // the transposed codebook / W2 (the backward's K-contiguous operands):
+  // CT[k][d] = C[d][k], W2T[j][d] = W2[d][j]; (b) Z1 = tanh(sum of the
+  // split-K slabs + b1) (the slab-reduce epilogue), every slab of two f4
+  // columns in flight (slabs >= nslab lie beyond the buffer resource: 0).
+  // All loads are unconditional buffer loads (out-of-range offsets read 0).
+  {
+    const int nC = K * D, nW = Hm * D, nT = nC + nW;
+    const int per = (nT + gridDim.x - 1) / gridDim.x, t0 = blockIdx.x * per, t1 = min(nT, t0 + per);
+    const __amdgpu_buffer_rsrc_t rC = make_rsrc(a.C, (uint32_t)nC * 4u), rW = make_rsrc(a.W2, (uint32_t)nW * 4u);
+    const uint32_t BH4 = (uint32_t)a.B * Hm * 4u;
+    const __amdgpu_buffer_rsrc_t rS = make_rsrc(a.slab, (uint32_t)a.nslab * BH4);
+    const __amdgpu_buffer_rsrc_t rB = make_rsrc(a.b1, (uint32_t)Hm * 4u);
+    const int h4 = Hm >> 2, nZ = HEAD_ROWS * h4;
+    constexpr int UT = 8, UZ = 2;
+    const int itT = (t1 - t0 + 256 * UT - 1) / (256 * UT), itZ = (nZ + 256 * UZ - 1) / (256 * UZ);
+    for (int it = 0; it < max(itT, itZ); ++it) {
+      float tv[UT];
+#pragma unroll
+      for (int u = 0; u < UT; ++u) {
+        const int e = t0 + (it * UT + u) * 256 + tid;
+        const bool inC = e < nC;
+        const int k = e / D, d = e - k * D, f = e - nC, jj = f / D, dd = f - jj * D;
+        const uint32_t oc = (e < t1 && inC) ? ((uint32_t)d * K + k) * 4u : 0x80000000u;
+        const uint32_t ow = (e < t1 && !inC) ? ((uint32_t)dd * Hm + jj) * 4u : 0x80000000u;
+        tv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(inC ? rC : rW, inC ? oc : ow, 0, 0));
+      }
+      f4 v[UZ][HEAD_MAX_SLABS + 1];  // [.][HEAD_MAX_SLABS]: b1
+#pragma unroll
+      for (int u = 0; u < UZ; ++u) {
+        const int e = (it * UZ + u) * 256 + tid, rr = e / h4, c = (e - rr * h4) * 4;
+        const bool ok = e < nZ && rr < nr;
+        const uint32_t o = ok ? ((uint32_t)(row0 + rr) * Hm + c) * 4u : 0x80000000u;
+#pragma unroll
+        for (int k = 0; k < HEAD_MAX_SLABS; ++k)
+          v[u][k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rS, o + k * BH4, 0, 0));
+        v[u][HEAD_MAX_SLABS] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rB, ok ? (uint32_t)c * 4u : 0x80000000u, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < UT; ++u) {
+        const int e = t0 + (it * UT + u) * 256 + tid;
+        if (e < t1) { if (e < nC) a.CT[e] = tv[u]; else a.W2T[e - nC] = tv[u]; }
+      }
+#pragma unroll
+      for (int u = 0; u < UZ; ++u) {
+        const int e = (it * UZ + u) * 256 + tid, rr = e / h4, c = (e - rr * h4) * 4;
+        if (e >= nZ) continue;
+        f4 z = f4zero();
+        if (rr < nr) {
+          f4 sacc = f4zero();
+#pragma unroll
+          for (int k = 0; k < HEAD_MAX_SLABS; ++k) sacc += v[u][k];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) z[i] = tanhf(sacc[i] + v[u][HEAD_MAX_SLABS][i]);
+          *reinterpret_cast<f4*>(a.Z1 + (long)(row0 + rr) * Hm + c) = z;
+        }
+        *reinterpret_cast<f4*>(R1 + rr * ld1 + c) = z;
+      }
+    }
+  }
+  __syncthreads();
+  // U = Z1 W2^T + b2
+  tile_mma_any(R1, ld1, Hm, bkc(a.W2, Hm, D), D, w, lane, [&](int c0, f4 acc) {
+    const int col = c0 + r;
+    const float bb = a.b2[col];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row = 4 * q + g;
+      const float v = acc[g] + bb;
+      R2[row * ld2 + col] = v;
+      if (row < nr) a.U[(long)(row0 + row) * D + col] = v;
+    }
+  });
+  __syncthreads();
+  // logits = U C / sqrt(D)   (C: D x K, the K-major operand)
+  const float rs = 1.f / sqrtf((float)D);
+  tile_mma_any(R2, ld2, D, bkm(a.C, K, D), K, w, lane, [&](int c0, f4 acc) {
+    const int col = c0 + r;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row = 4 * q + g;
+      const float v = rs * acc[g];
+      R1[row * ld1 + col] = v;
+      if (row < nr) a.logits[(long)(row0 + row) * K + col] = v;
+    }
+  });
+  // Dirichlet posterior: elog for the row terms (every tile), the stash once
+  prior_block(a.psl, K, a.N, a.a0, alphaL, elogL, sh, blockIdx.x == 0, a.p, a.alpha, a.elog, a.tri, a.kl_small);
+  // rows: KL row term v_b = sum_k Q (log Q - elog) (kl_rows) and the sample
+  // Y = softmax((logits + g) / tau) (sample_softmax_rows), one wave per row,
+  // the row's KPL logits per lane in registers
+  const float it = 1.f / a.tau;
+  double klsum = 0.0;
+  for (int rr = 0; rr < HEAD_ROWS / 4; ++rr) {
+    const int row = w * (HEAD_ROWS / 4) + rr;
+    float* y = R2 + row * ld2;
+    if (row >= nr) {
+      for (int k = lane; k < K; k += 64) y[k] = 0.f;
+      continue;
+    }
+    const float* l = R1 + row * ld1;
+    const long g0 = (long)(row0 + row) * K;
+    float lv[KPL], gv[KPL];
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const int k = lane + 64 * u;
+      lv[u] = k < K ? l[k] : -INFINITY;
+      gv[u] = (a.gumbel && a.noise && k < K) ? a.noise[g0 + k] : 0.f;
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) m = fmaxf(m, lv[u]);
+    m = wave_max(m);
+    float se = 0.f;
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) se += lane + 64 * u < K ? __expf(lv[u] - m) : 0.f;
+    se = wave_sum(se);
+    const float ls = __logf(se);
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const int k = lane + 64 * u;
+      if (k < K) {
+        const float lq = lv[u] - m - ls;
+        const float qv = __expf(lq);
+        a.Q[g0 + k] = qv;
+        acc += qv * (lq - elogL[k]);
+      }
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) a.v[row0 + row] = acc;
+    klsum += acc;
+    float m2 = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const int k = lane + 64 * u;
+      if (k < K && a.gumbel) {
+        const float g = a.noise ? gv[u] : philox_gumbel(a.seed, a.offset + (uint64_t)g0 + k);
+        lv[u] = (lv[u] + g) * it;
+      }
+      m2 = fmaxf(m2, lv[u]);
+    }
+    m2 = wave_max(m2);
+    float s2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      lv[u] = lane + 64 * u < K ? __expf(lv[u] - m2) : 0.f;
+      s2 += lv[u];
+    }
+    s2 = wave_sum(s2);
+    const float is = 1.f / s2;
+#pragma unroll
+    for (int u = 0; u < KPL; ++u) {
+      const int k = lane + 64 * u;
+      if (k < K) {
+        const float yv = lv[u] * is;
+        y[k] = yv;
+        a.Y[g0 + k] = yv;
+      }
+    }
+  }
+  if (lane == 0) sh[w] = klsum;
+  __syncthreads();
+  // feats = Y C^T
+  tile_mma_any(R2, ld2, K, bkc(a.C, K, D), D, w, lane, [&](int c0, f4 acc) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row = 4 * q + g;
+      if (row < nr) a.feats[(long)(row0 + row) * D + c0 + r] = acc[g];
+    }
+  });
+  if (!a.kl_out) return;
+  if (tid == 0) st_agent(a.klpart + blockIdx.x, (sh[0] + sh[1]) + (sh[2] + sh[3]));
+  if (last_workgroup(&g_head_ticket[0], flag) && w == 0) {
+    double t = 0.0;  // lane-strided partial sums, then a fixed shuffle tree: deterministic
+    for (int i = lane; i < (int)gridDim.x; i += 64) t += a.klpart[i];
+    t = wave_sum_d(t);
+    if (lane == 0) *a.kl_out = (float)(a.kl_small[0] * ((double)a.B / a.N) + t);
+  }
+}
+
+struct HeadBwdArgs {
+  int B, Hm, D, K; float it;                // it: 1 / tau (Gumbel mode), else 1
+  const float *dfeat, *dkl, *Y, *Q, *v, *elog, *Z1, *C, *W2;
+  const float *p, *alpha, *tri; const double* kl_small; double N; float a0;
+  float* dfeat_copy;                       // the stacked [d_feats; U] operand of dC (top half), or null
+  float *dLs, *dU, *dZ1;                   // dLs = d_logits / sqrt(D)
+  float* colpart;                          // tiles x (D + Hm + K)
+  float *db2, *db1, *dpsl;                 // last workgroup's outputs (each may be null)
+  const float *CT, *W2T;                   // transposed copies written by the forward head
+};
+inline size_t head_bwd_lds(int Hm, int D, int K) {
+  return ((size_t)HEAD_ROWS * (K + 4) + (size_t)HEAD_ROWS * (D + 4) + (size_t)HEAD_ROWS * (Hm + 4) + 6 * (size_t)K) *
+             4 + 16 * sizeof(double) + 16;
+}
+
+template <int KPL>
+struct HeadRow {  // one row's backward inputs, KPL per lane
+  float y[KPL], q[KPL], vb;
+};
+template <int KPL>
+DEV HeadRow<KPL> head_row_load(const HeadBwdArgs& a, int brow, bool valid, int lane) {
+  HeadRow<KPL> h;
+  const long g0 = (long)brow * a.K;
+#pragma unroll
+  for (int u = 0; u < KPL; ++u) {
+    const int k = lane + 64 * u;
+    const bool ok = valid && k < a.K;
+    h.y[u] = ok ? a.Y[g0 + k] : 0.f;
+    h.q[u] = ok ? a.Q[g0 + k] : 0.f;
+  }
+  h.vb = valid ? a.v[brow] : 0.f;
+  return h;
+}
+
+template <int KPL>
+__global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  const int Hm = a.Hm, D = a.D, K = a.K;
+  const int ld1 = K + 4, ld2 = D + 4, ldz = Hm + 4;
+  float* R1 = hsm;                    // dY, then dL
+  float* R2 = R1 + HEAD_ROWS * ld1;   // d_feats, then dU
+  float* ZL = R2 + HEAD_ROWS * ld2;   // Z1 tile
+  float* QcL = ZL + HEAD_ROWS * ldz;  // per-wave Q column sums (4 x K); the last workgroup's Qsum
+  float* elogL = QcL + 4 * K;
+  double* sh = reinterpret_cast<double*>(elogL + K);
+  int* flag = reinterpret_cast<int*>(sh + 16);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
+  const int row0 = blockIdx.x * HEAD_ROWS, nr = min(HEAD_ROWS, a.B - row0);
+  const int NC = D + Hm + K;
+  float* part = a.colpart + (long)blockIdx.x * NC;
+  // stage d_feats, Z1 and elog; zero the Q column sums
+  {  // one round trip per iteration: d_feats, Z1 and elog loads all in flight
+    const __amdgpu_buffer_rsrc_t rF = make_rsrc(a.dfeat + (long)row0 * D, (uint32_t)nr * D * 4u);
+    const __amdgpu_buffer_rsrc_t rZ = make_rsrc(a.Z1 + (long)row0 * Hm, (uint32_t)nr * Hm * 4u);
+    const __amdgpu_buffer_rsrc_t rE = make_rsrc(a.elog, (uint32_t)K * 4u);
+    const int nF = HEAD_ROWS * D / 4, nZ = HEAD_ROWS * Hm / 4, nE = K / 4;
+    const int nAll = nF + nZ + nE;
+    constexpr int U = 4;
+    for (int e0 = tid; e0 < nAll; e0 += 256 * U) {
+      f4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + 256 * u;
+        const int ez = e - nF, ee = ez - nZ;
+        // rows >= nr lie beyond the d_feats / Z1 resources and read 0
+        const uint32_t o = e < nF ? (uint32_t)e * 16u : ez < nZ ? (uint32_t)ez * 16u : ee < nE ? (uint32_t)ee * 16u : 0x80000000u;
+        v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(e < nF ? rF : ez < nZ ? rZ : rE, o, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + 256 * u;
+        if (e < nF) {
+          const int rr = e / (D / 4), c = (e - rr * (D / 4)) * 4;
+          *reinterpret_cast<f4*>(R2 + rr * ld2 + c) = v[u];
+        } else if (e < nF + nZ) {
+          const int ez = e - nF, rr = ez / (Hm / 4), c = (ez - rr * (Hm / 4)) * 4;
+          *reinterpret_cast<f4*>(ZL + rr * ldz + c) = v[u];
+        } else if (e < nAll) {
+          *reinterpret_cast<f4*>(elogL + (e - nF - nZ) * 4) = v[u];
+        }
+      }
+    }
+  }
+  for (int k = tid; k < 4 * K; k += 256) QcL[k] = 0.f;
+  __syncthreads();
+  if (a.dfeat_copy) {
+    const int d4 = D >> 2;
+    for (int e = tid; e < nr * d4; e += 256) {
+      const int rr = e / d4, c = (e - rr * d4) * 4;
+      *reinterpret_cast<f4*>(a.dfeat_copy + (long)(row0 + rr) * D + c) = *reinterpret_cast<const f4*>(R2 + rr * ld2 + c);
+    }
+  }
+  // dY = d_feats C
+  tile_mma_any(R2, ld2, D, bkc(a.CT, D, K), K, w, lane, [&](int c0, f4 acc) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) R1[(4 * q + g) * ld1 + c0 + r] = acc[g];
+  });
+  __syncthreads();
+  // dL = Y (dY - sum Y dY) / tau  +  s Q ((log Q - elog) - v_b)
+  // (sample_softmax_bwd + kl_rows_bwd), one wave per row; the next row's
+  // Y / Q / v_b loads are in flight while this row is reduced
+  const float s = *a.dkl, rs = 1.f / sqrtf((float)D);
+  {
+    const int rbase = w * (HEAD_ROWS / 4);
+    float* qc = QcL + w * K;
+    HeadRow<KPL> cur = head_row_load<KPL>(a, row0 + rbase, rbase < nr, lane);
+    for (int rr = 0; rr < HEAD_ROWS / 4; ++rr) {
+      const int row = rbase + rr;
+      HeadRow<KPL> nxt = cur;
+      if (rr + 1 < HEAD_ROWS / 4) nxt = head_row_load<KPL>(a, row0 + row + 1, row + 1 < nr, lane);
+      float* d = R1 + row * ld1;
+      if (row < nr) {
+        const long g0 = (long)(row0 + row) * K;
+        float sdy = 0.f;
+#pragma unroll
+        for (int u = 0; u < KPL; ++u)
+          if (lane + 64 * u < K) sdy += cur.y[u] * d[lane + 64 * u];
+        sdy = wave_sum(sdy);
+#pragma unroll
+        for (int u = 0; u < KPL; ++u) {
+          const int k = lane + 64 * u;
+          if (k < K) {
+            const float g1 = cur.y[u] * (d[k] - sdy) * a.it;
+            const float qv = cur.q[u];
+            const float g2 = s * qv * ((__logf(fmaxf(qv, 1e-38f)) - elogL[k]) - cur.vb);
+            const float dl = g1 + g2;
+            d[k] = dl;
+            a.dLs[g0 + k] = dl * rs;
+            qc[k] += qv;
+          }
+        }
+      } else {
+        for (int k = lane; k < K; k += 64) d[k] = 0.f;
+      }
+      cur = nxt;
+    }
+  }
+  __syncthreads();
+  // Qsum partial of this tile (the prior gradient's column sums)
+  for (int k = tid; k < K; k += 256) st_agent(part + D + Hm + k, (QcL[k] + QcL[K + k]) + (QcL[2 * K + k] + QcL[3 * K + k]));
+  // dU = dL C^T / sqrt(D)  (+ the db2 partial)
+  tile_mma_any(R1, ld1, K, bkc(a.C, K, D), D, w, lane, [&](int c0, f4 acc) {
+    const int col = c0 + r;
+    f4 v;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row = 4 * q + g;
+      v[g] = rs * acc[g];
+      R2[row * ld2 + col] = v[g];
+      if (row < nr) a.dU[(long)(row0 + row) * D + col] = v[g];
+    }
+    const float cs = tile_colsum(v);  // rows >= nr are zero (dL rows zeroed)
+    if (q == 0) st_agent(part + col, cs);
+  });
+  __syncthreads();
+  // dZ1 = (dU W2) (1 - Z1^2)  (+ the db1 partial)
+  tile_mma_any(R2, ld2, D, bkc(a.W2T, D, Hm), Hm, w, lane, [&](int c0, f4 acc) {
+    const int col = c0 + r;
+    f4 v;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row = 4 * q + g;
+      const float z = ZL[row * ldz + col];
+      v[g] = row < nr ? acc[g] * (1.f - z * z) : 0.f;
+      if (row < nr) a.dZ1[(long)(row0 + row) * Hm + col] = v[g];
+    }
+    const float cs = tile_colsum(v);
+    if (q == 0) st_agent(part + D + col, cs);
+  });
+  if (!last_workgroup(&g_head_ticket[1], flag)) return;
+  // last workgroup: column sums over the tiles (tile order) -> db2, db1,
+  // Qsum; then the Dirichlet prior's gradient
+  const int nt = gridDim.x;
+  for (int c = tid; c < NC; c += 256) {
+    float t = 0.f;  // tile order; 8 tiles' loads in flight
+    int i = 0;
+    for (; i + 8 <= nt; i += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = a.colpart[(long)(i + u) * NC + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t += v[u];
+    }
+    for (; i < nt; ++i) t += a.colpart[(long)i * NC + c];
+    if (c < D) { if (a.db2) a.db2[c] = t; }
+    else if (c < D + Hm) { if (a.db1) a.db1[c - D] = t; }
+    else QcL[c - D - Hm] = t;
+  }
+  __syncthreads();
+  if (a.dpsl) prior_bwd_block(a.p, a.alpha, a.tri, a.kl_small, QcL, K, a.B, a.N, a.a0, s, a.dpsl, sh);
+}
+
+// KPL dispatch: K <= 64 * KPL
+template <template <int> class F, class... Args>
+static int head_dispatch(int K, Args&&... args) {
+  if (K <= 64) return F<1>::run(args...);
+  if (K <= 128) return F<2>::run(args...);
+  if (K <= 256) return F<4>::run(args...);
+  if (K <= 512) return F<8>::run(args...);
+  if (K <= 1024) return F<16>::run(args...);
+  return ABCD_EINVAL;
+}
+static std::mutex g_head_attr_mu;
+static int head_lds_attr(const void* fn, size_t lds) {  // once per kernel instance needing > 64 KiB
+  if (lds <= 64 * 1024) return 0;
+  static const void* done[16];
+  std::lock_guard<std::mutex> lk(g_head_attr_mu);
+  int i = 0;
+  for (; i < 16 && done[i]; ++i)
+    if (done[i] == fn) return 0;
+  ABCD_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  if (i < 16) done[i] = fn;
+  return 0;
+}
+template <int KPL>
+struct HeadFwdLaunch {
+  static int run(const HeadFwdArgs& a, int grid, size_t lds, hipStream_t s) {
+    ABCD_TRY((hipError_t)head_lds_attr((const void*)samp_head_fwd<KPL>, lds));
+    samp_head_fwd<KPL><<<grid, 256, lds, s>>>(a);
+    ABCD_CHECK_LAUNCH();
+    return 0;
+  }
+};
+template <int KPL>
+struct HeadBwdLaunch {
+  static int run(const HeadBwdArgs& a, int grid, size_t lds, hipStream_t s) {
+    ABCD_TRY((hipError_t)head_lds_attr((const void*)samp_head_bwd<KPL>, lds));
+    samp_head_bwd<KPL><<<grid, 256, lds, s>>>(a);
+    ABCD_CHECK_LAUNCH();
+    return 0;
+  }
+};
+
 struct SampWS {
   float *W1T[2], *W2T[2], *CT;
   float *Z1[2], *U, *Y, *Q, *v, *p, *alpha, *elog, *tri, *Qsum, *MV, *EPS;
   double* kl_small;
   float *dY, *dL, *dU, *dZ1[2], *dMV, *dh2;
+  float *FU, *YdL;     // stacked dC operands: [d_feats; U] (2B x D), [Y; dL / sqrt(D)] (2B x K)
+  float* colpart;      // sampler head backward: per-tile column sums
+  double* klpart;      // sampler head forward: per-tile KL row sums
   float* scratch;
   size_t scratch_floats;
 };
@@ -314,7 +903,11 @@ static SampWS carve_sampler(Arena& A, const abcd_sampler_cfg* c, int B) {
     w.dZ1[k] = A.f((size_t)B * Hm);
   }
   w.CT = A.f((size_t)K * D);
-  w.U = A.f((size_t)B * D); w.Y = A.f((size_t)B * K); w.Q = A.f((size_t)B * K); w.v = A.f(B);
+  w.FU = A.f((size_t)2 * B * D); w.YdL = A.f((size_t)2 * B * K);
+  w.U = w.FU ? w.FU + (size_t)B * D : nullptr; w.Y = w.YdL;
+  w.Q = A.f((size_t)B * K); w.v = A.f(B);
+  const int ntile = cdiv(B, HEAD_ROWS);
+  w.colpart = A.f((size_t)ntile * (D + Hm + K)); w.klpart = A.d(ntile);
   w.p = A.f(K); w.alpha = A.f(K); w.elog = A.f(K); w.tri = A.f(K); w.Qsum = A.f(K);
   w.MV = A.f((size_t)B * 2 * D); w.EPS = A.f((size_t)B * D);
   w.kl_small = A.d(8);
@@ -366,7 +959,9 @@ extern "C" int abcd_sampler_forward(const abcd_sampler_cfg* c, const abcd_sample
   // logits = U @ codebook / sqrt(D)   (codebook D x K used as a K-major operand)
   ABCD_TRY((hipError_t)gemm(s, B, K, D, opKC(w.U, D, B), opKM(p->codebook, K, K), logits, K,
                             1.f / sqrtf((float)D), 0.f, nullptr, ACT_NONE, nullptr, 0));
-  return 0;
+  // the transposed codebook / W2 the fused backward reads (the fused forward writes them in-kernel)
+  ABCD_TRY((hipError_t)pack2d(s, p->codebook, K, K, D, true, w.CT, D, K, D));
+  return pack2d(s, m.w2, Hm, Hm, D, true, w.W2T[0], D, Hm, D);
 }
 
 extern "C" int abcd_sampler_sample(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* logits,
@@ -418,6 +1013,48 @@ extern "C" int abcd_sampler_kl(const abcd_sampler_cfg* c, const abcd_sampler_par
   ABCD_CHECK_LAUNCH();
   kl_final<<<1, 256, 0, s>>>(w.kl_small, w.v, B, N, kl_out);
   ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- the fused training-step forward: forward + sample + kl in two launches ----
+constexpr size_t HEAD_LDS_MAX = 160 * 1024;
+
+extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
+                                          int B, int mode, float temperature, const float* noise, uint64_t seed,
+                                          uint64_t offset, double N, float* logits, float* feats, float* kl_out,
+                                          void* ws, size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(samp_check(c) == 0 && p && h && logits && feats && ws && B > 0);
+  const int E = c->input_size, Hm = c->mlp_hidden, D = c->feature_dim, K = c->num_categories;
+  const size_t lds = c->plain ? 0 : head_fwd_lds(Hm, D, K);
+  if (c->plain || lds > HEAD_LDS_MAX || K > 1024) {  // the three reference methods in turn
+    ABCD_TRY((hipError_t)abcd_sampler_forward(c, p, h, B, logits, ws, ws_bytes, stream));
+    ABCD_TRY((hipError_t)abcd_sampler_sample(c, p, logits, B, mode, temperature, noise, seed, offset, feats, ws,
+                                             ws_bytes, stream));
+    return kl_out ? abcd_sampler_kl(c, p, logits, B, N, kl_out, ws, ws_bytes, stream) : 0;
+  }
+  ABCD_REQUIRE(mode == ABCD_SAMPLE_SOFTMAX || temperature > 0.f);
+  ABCD_REQUIRE(!kl_out || N > 0);
+  hipStream_t s = (hipStream_t)stream;
+  Arena A(ws, ws_bytes);
+  SampWS w = carve_sampler(A, c, B);
+  ABCD_REQUIRE(A.ok);
+  const abcd_mlp_w& m = p->mlp[0];
+  int Z = 0;
+  ABCD_TRY((hipError_t)gemm_slabs(s, B, Hm, E, opKC(h, E, B), opKC(m.w1, E, Hm), w.scratch,
+                                        std::min(w.scratch_floats, (size_t)HEAD_MAX_SLABS * B * Hm), &Z));
+  HeadFwdArgs a{};
+  a.B = B; a.Hm = Hm; a.D = D; a.K = K; a.nslab = Z;
+  a.slab = w.scratch; a.b1 = m.b1; a.W2 = m.w2; a.b2 = m.b2; a.C = p->codebook; a.psl = p->posterior_shape_logits;
+  a.N = N > 0 ? N : 1.0; a.a0 = p->prior_concentration;
+  a.gumbel = mode == ABCD_SAMPLE_GUMBEL; a.tau = a.gumbel ? temperature : 1.f;
+  a.noise = noise; a.seed = seed; a.offset = offset;
+  a.Z1 = w.Z1[0]; a.U = w.U; a.logits = logits; a.Y = w.Y; a.Q = w.Q; a.v = w.v; a.feats = feats;
+  a.p = w.p; a.alpha = w.alpha; a.elog = w.elog; a.tri = w.tri; a.kl_small = w.kl_small;
+  a.klpart = w.klpart; a.kl_out = kl_out;
+  a.CT = w.CT; a.W2T = w.W2T[0];
+  const int grid = cdiv(B, HEAD_ROWS);
+  ABCD_TRY((hipError_t)head_dispatch<HeadFwdLaunch>(K, a, grid, lds, s));
+  note_dispatch(TK_SAMP_FWD, "gemm_slabs[%d] + samp_head_fwd grid %d", Z, grid);
   return 0;
 }
 
@@ -547,6 +1184,50 @@ static int samp_fwd_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p,
   return 0;
 }
 
+// the fused training-step backward (ABCD, d_feats and d_kl both present):
+// samp_head_bwd + the d_h GEMM on `s`; codebook / W2 / W1 gradients on `sw`
+static int samp_fused_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h, int B, int mode,
+                          float temperature, double N, const float* d_feats, const float* d_kl, float* d_h,
+                          const abcd_sampler_grads* g, const SampWS& w, hipStream_t s, hipStream_t sw) {
+  const int E = c->input_size, Hm = c->mlp_hidden, D = c->feature_dim, K = c->num_categories;
+  const abcd_mlp_w& m = p->mlp[0];
+  const abcd_mlp_g& mg = g->mlp[0];
+  HeadBwdArgs a{};
+  a.B = B; a.Hm = Hm; a.D = D; a.K = K;
+  a.it = 1.f / (mode == ABCD_SAMPLE_GUMBEL ? temperature : 1.f);
+  a.dfeat = d_feats; a.dkl = d_kl; a.Y = w.Y; a.Q = w.Q; a.v = w.v; a.elog = w.elog; a.Z1 = w.Z1[0];
+  a.C = p->codebook; a.W2 = m.w2;
+  a.p = w.p; a.alpha = w.alpha; a.tri = w.tri; a.kl_small = w.kl_small; a.N = N; a.a0 = p->prior_concentration;
+  a.dfeat_copy = g->codebook ? w.FU : nullptr;
+  a.dLs = w.YdL + (size_t)B * K; a.dU = w.dU; a.dZ1 = w.dZ1[0];
+  a.colpart = w.colpart; a.db2 = mg.b2; a.db1 = mg.b1; a.dpsl = g->posterior_shape_logits;
+  a.CT = w.CT; a.W2T = w.W2T[0];
+  const size_t lds = head_bwd_lds(Hm, D, K);
+  const int grid = cdiv(B, HEAD_ROWS);
+  ABCD_TRY((hipError_t)head_dispatch<HeadBwdLaunch>(K, a, grid, lds, s));
+  note_dispatch(TK_SAMP_BWD, "samp_head_bwd grid %d + d_h gemm", grid);
+  ABCD_TRY((hipError_t)stream_fork(s, sw, 1));
+  {
+    SideWork side(s, sw);
+    float* sc = w.scratch;
+    const size_t scf = w.scratch_floats;
+    // dC = [d_feats; U]^T [Y; dL / sqrt(D)]  (the sample and the logits products in one reduction)
+    if (g->codebook)
+      ABCD_TRY((hipError_t)gemm(sw, D, K, 2 * B, opKM(w.FU, D, D), opKM(w.YdL, K, K), g->codebook, K, 1.f, 0.f,
+                                nullptr, ACT_NONE, sc, scf));
+    if (mg.w2)
+      ABCD_TRY((hipError_t)gemm(sw, D, Hm, B, opKM(w.dU, D, D), opKM(w.Z1[0], Hm, Hm), mg.w2, Hm, 1.f, 0.f, nullptr,
+                                ACT_NONE, sc, scf));
+    if (mg.w1)
+      ABCD_TRY((hipError_t)gemm(sw, Hm, E, B, opKM(w.dZ1[0], Hm, Hm), opKM(h, E, E), mg.w1, E, 1.f, 0.f, nullptr,
+                                ACT_NONE, sc, scf));
+  }
+  if (d_h)
+    ABCD_TRY((hipError_t)gemm(s, B, E, Hm, opKC(w.dZ1[0], Hm, B), opKM(m.w1, E, E), d_h, E, 1.f, 0.f, nullptr,
+                              ACT_NONE, nullptr, 0));
+  return 0;
+}
+
 static int samp_ws(const abcd_sampler_cfg* c, int B, void* ws, size_t ws_bytes, SampWS* w) {
   Arena A(ws, ws_bytes);
   *w = carve_sampler(A, c, B);
@@ -606,6 +1287,8 @@ extern "C" int abcd_sampler_backward_split(const abcd_sampler_cfg* c, const abcd
     ABCD_CHECK_LAUNCH();
     dL = w.dL;
     have = 1;
+  } else if (d_feats && d_kl && K <= 1024 && head_bwd_lds(c->mlp_hidden, D, K) <= HEAD_LDS_MAX) {
+    return samp_fused_bwd(c, p, h, B, mode, temperature, N, d_feats, d_kl, d_h, g, w, s, sw);
   } else {
     if (d_feats) {
       ABCD_TRY((hipError_t)samp_sample_bwd(c, p, B, mode, temperature, d_feats, dL, g->codebook, w, s, sw));

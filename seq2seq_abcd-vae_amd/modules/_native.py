@@ -97,6 +97,9 @@ _SIGS = {
                                     c_uint64, c_uint64, c_void_p, c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_kl": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_double, c_void_p, c_void_p,
                                 c_size_t, c_void_p]),
+    "abcd_sampler_forward_fused": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float,
+                                           c_void_p, c_uint64, c_uint64, c_double, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float, c_double,
                                       c_void_p, c_void_p, c_void_p, _P(SamplerGrads), c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_backward_split": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float,
@@ -216,14 +219,15 @@ def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
-ENC_FWD, ENC_BWD, DEC_FWD, DEC_BWD = 1, 2, 3, 4
+ENC_FWD, ENC_BWD, DEC_FWD, DEC_BWD, SAMP_FWD, SAMP_BWD = 1, 2, 3, 4, 5, 6
 
 
 def dispatch():
     """{role: (kernel name of its last launch, launches since reset)}"""
     L = lib()
     return {r: (L.abcd_dispatch_name(k).decode(), int(L.abcd_dispatch_count(k)))
-            for r, k in (("enc_fwd", ENC_FWD), ("enc_bwd", ENC_BWD), ("dec_fwd", DEC_FWD), ("dec_bwd", DEC_BWD))}
+            for r, k in (("enc_fwd", ENC_FWD), ("enc_bwd", ENC_BWD), ("dec_fwd", DEC_FWD), ("dec_bwd", DEC_BWD),
+                                ("samp_fwd", SAMP_FWD), ("samp_bwd", SAMP_BWD))}
 
 
 def ptr_array(tensors):

@@ -150,8 +150,6 @@ class FusedStep:
                                                 N.ptr(ws_e), ws_e.numel(), st), "encoder forward")
         W = self.sampler._logit_width()
         logits = torch.empty(B, W, device=dev)
-        N.check(L_.abcd_sampler_forward(self.samp_cfg, self.samp_p, N.ptr(h), B, N.ptr(logits), N.ptr(ws_s),
-                                        ws_s.numel(), st), "sampler forward")
         feats = torch.empty(B, self.Dfeat, device=dev)
         self.last_hidden, self.feats = h, feats  # kept for inspection (encode paths, parity tests)
         if self.plain:
@@ -162,19 +160,12 @@ class FusedStep:
         else:
             mode, tau = N.SAMPLE_GUMBEL, float(self.sampler.temperature)
             nt, seed, off = _noise.gumbel(B, W, dev)
-        N.check(L_.abcd_sampler_sample(self.samp_cfg, self.samp_p, N.ptr(logits), B, mode, tau, N.ptr(nt), seed, off,
-                                       N.ptr(feats), N.ptr(ws_s), ws_s.numel(), st), "sampler sample")
-        # the Dirichlet KL (three small kernels) only feeds the loss scalar and
-        # the backward: on the idle side stream beside the decoder's setup
-        # (ABCD flavour only: plain KL and sample share the MV stash copy);
-        # measured ~30 us/step at c2
-        kl_side = None
-        if not self.plain:
-            kl_side = self._side_stream()
-            kl_side.wait_stream(torch.cuda.current_stream(dev))
-        N.check(L_.abcd_sampler_kl(self.samp_cfg, self.samp_p, N.ptr(logits), B, float(entire_data_size),
-                                   N.ptr(sc[KL:KL + 1]), N.ptr(ws_s), ws_s.numel(),
-                                   st if kl_side is None else N.c_void_p(kl_side.cuda_stream)), "sampler kl")
+        # feature_sampler(h) -> .sample(logits) -> .kl_divergence(logits, N)
+        # (learning.py:149-153): ABCD = the split-K MLP GEMM + one row-tiled
+        # sampler-head kernel (logits, Gumbel-softmax, y C^T, KL) per step
+        N.check(L_.abcd_sampler_forward_fused(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, N.ptr(nt), seed,
+                                              off, float(entire_data_size), N.ptr(logits), N.ptr(feats),
+                                              N.ptr(sc[KL:KL + 1]), N.ptr(ws_s), ws_s.numel(), st), "sampler")
         F = self.decoder.rnn_cell.cell.input_size
         pdrop = self.decoder._input_dropout_p() if train else 0.0
         eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
@@ -186,8 +177,6 @@ class FusedStep:
                                               N.ptr(eps), N.ptr(xmask), eseed, eoff, None, None, None, None,
                                               N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st, None),
                 "decoder forward")
-        if kl_side is not None:
-            torch.cuda.current_stream(dev).wait_stream(kl_side)
         N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), Bn, N.ptr(sc[LOSS:LOSS + 1]), st),
                 "total loss")
         if not train:
@@ -206,7 +195,8 @@ class FusedStep:
         d_h = torch.empty(B, self.E, device=dev)
         N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
                                                float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
-                                               self.samp_g, N.ptr(ws_s), ws_s.numel(), st, None), "sampler backward")
+                                               self.samp_g, N.ptr(ws_s), ws_s.numel(), st, None),
+                "sampler backward")  # one stream: its parameter GEMMs beside enc_bwd only slow the BPTT (DESIGN s3)
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
                                                  self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
                                                  N.c_void_p(side.cuda_stream)), "encoder backward")

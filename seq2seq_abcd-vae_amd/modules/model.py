@@ -9,8 +9,9 @@ dicts follow the reference (file:line cited per class) so that ``learning.py``,
 created with the same torch init calls in the same order as the reference, so
 ``torch.manual_seed(seed)`` gives bit-identical initial weights.
 
-Every forward/backward runs on the GPU through the C ABI (``_native``); there is
-no CPU fallback -- a CPU tensor raises.
+Every forward/backward runs on the GPU through the ``abcd::`` custom operators
+of ``ops.py`` (the C ABI registered with ``torch.library``, autograd formulas
+included); there is no CPU fallback -- a CPU tensor raises.
 """
 import math
 
@@ -18,6 +19,7 @@ import torch
 
 from . import _native as N
 from . import noise as _noise
+from . import ops
 
 
 # ----------------------------------------------------------------------------
@@ -183,22 +185,6 @@ class RNN_Cell(torch.nn.Module):
 # ----------------------------------------------------------------------------
 # Encoder (model.py:40-79)
 # ----------------------------------------------------------------------------
-class _EncoderFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, enc, data, batch_sizes, *params):
-        noise = enc.draw_dropout_noise(int(data.shape[0]), data.device)
-        out, ws, keep = enc._run_forward(data, batch_sizes, noise=noise)
-        ctx.enc, ctx.ws, ctx.keep, ctx.noise = enc, ws, keep, noise
-        ctx.data, ctx.batch_sizes = data, batch_sizes
-        return out
-
-    @staticmethod
-    @torch.autograd.function.once_differentiable
-    def backward(ctx, d_out):
-        grads = ctx.enc._run_backward(ctx.data, ctx.batch_sizes, d_out.contiguous(), ctx.ws, noise=ctx.noise)
-        return (None, None, None) + tuple(grads)
-
-
 class RNN_Variational_Encoder(torch.nn.Module):
     """Bi-directional LSTM/GRU over a PackedSequence; returns the last (h, c)
     of every layer/direction flattened to (B, hidden_size_total)."""
@@ -242,46 +228,20 @@ class RNN_Variational_Encoder(torch.nn.Module):
         return [_noise.dropout_noise((L, dirs * self.rnn.hidden_size), p, device)
                 for _ in range(self.rnn.num_layers - 1)]
 
-    def _run_forward(self, data, batch_sizes, ws=None, noise=None):
-        data = _f32c(data)
-        N.require_gpu(data)
-        cfg = self._cfg()
-        pk, bs = _packed_struct(data, batch_sizes, cfg.input_size)
-        L = N.lib()
-        nbytes = L.abcd_encoder_workspace_bytes(cfg, pk.T, pk.L, pk.B)
-        if nbytes == 0:
-            raise N.HipError("encoder: unsupported configuration (hidden size must be a multiple of 16)")
-        if ws is None or ws.numel() < nbytes:
-            ws = N.workspace(nbytes, data.device)
-        out = torch.empty(pk.B, self.hidden_size_total, device=data.device)
-        N.check(L.abcd_encoder_forward_dropout(cfg, self._params(), pk, N.ptr_array(noise), N.ptr(out), N.ptr(ws),
-                                               ws.numel(), N.stream()), "encoder forward")
-        return out, ws, (bs, data)
+    def _cfg_list(self):
+        return [self.rnn.input_size, self.rnn.hidden_size, N.LSTM if self.rnn.mode == "LSTM" else N.GRU,
+                self.rnn.num_layers, int(self.rnn.bidirectional)]
 
-    def _run_backward(self, data, batch_sizes, d_out, ws, grad_views=None, noise=None):
-        cfg = self._cfg()
-        pk, bs = _packed_struct(data, batch_sizes, cfg.input_size)
+    def _weights(self):
         dirs = 2 if self.rnn.bidirectional else 1
-        if grad_views is None:
-            grad_views = {}
-            for l in range(self.rnn.num_layers):
-                for d in range(dirs):
-                    grad_views[(l, d)] = [torch.empty_like(p) for p in self.rnn.layer_weights(l, d)]
-        N.check(N.lib().abcd_encoder_backward_dropout(cfg, self._params(), pk, N.ptr_array(noise), N.ptr(d_out),
-                                                      self._params(grad_views), N.ptr(ws), ws.numel(), N.stream(),
-                                                      None), "encoder backward")
-        out = []
-        for l in range(self.rnn.num_layers):
-            for d in range(dirs):
-                out.extend(grad_views[(l, d)])
-        return out
+        return [t for l in range(self.rnn.num_layers) for d in range(dirs) for t in self.rnn.layer_weights(l, d)]
 
     def forward(self, packed_input):
-        data, bsz = packed_input.data, packed_input.batch_sizes
-        params = list(self.rnn.parameters())
-        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
-            return _EncoderFn.apply(self, data, bsz, *params)
-        return self._run_forward(data, bsz, noise=self.draw_dropout_noise(int(data.shape[0]), data.device))[0]
+        data = _f32c(packed_input.data)
+        N.require_gpu(data)
+        noise = self.draw_dropout_noise(int(data.shape[0]), data.device)
+        out, _ws = ops.encoder(data, packed_input.batch_sizes, self._weights(), noise or [], self._cfg_list())
+        return out
 
     def pack_init_parameters(self):
         return {"input_size": self.rnn.input_size, "rnn_hidden_size": self.rnn.hidden_size,
@@ -333,98 +293,12 @@ class _SamplerBase(torch.nn.Module):
             ws = N.workspace(nbytes, device)
         return ws
 
-    def _run_forward(self, h, ws=None):
-        h = _f32c(h)
-        N.require_gpu(h)
-        B = h.shape[0]
-        ws = self._ws_for(B, h.device, ws)
-        out = torch.empty(B, self._logit_width(), device=h.device)
-        N.check(N.lib().abcd_sampler_forward(self._scfg(), self._sparams(), N.ptr(h), B, N.ptr(out), N.ptr(ws),
-                                             ws.numel(), N.stream()), "sampler forward")
-        return out, ws
+    def _cfg_list(self):
+        c = self._scfg()
+        return [c.input_size, c.mlp_hidden, c.num_categories, c.feature_dim, c.plain]
 
-
-class _SamplerForwardFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, samp, h, *params):
-        out, ws = samp._run_forward(h)
-        ctx.samp, ctx.ws, ctx.h = samp, ws, h
-        out._abcd_ws = ws
-        return out
-
-    @staticmethod
-    @torch.autograd.function.once_differentiable
-    def backward(ctx, d_logits):
-        samp = ctx.samp
-        views = samp._grad_views_forward()
-        d_h = torch.empty_like(ctx.h) if ctx.needs_input_grad[1] else None
-        N.check(N.lib().abcd_sampler_forward_backward(
-            samp._scfg(), samp._sparams(), N.ptr(ctx.h), ctx.h.shape[0], N.ptr(d_logits.contiguous()), N.ptr(d_h),
-            samp._sgrads(views), 0, N.ptr(ctx.ws), ctx.ws.numel(), N.stream()), "sampler forward backward")
-        return (None, d_h) + samp._order_grads(views)
-
-
-class _SampleFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, samp, logits, mode, tau, ws, noise_t, seed, offset, *params):
-        B = logits.shape[0]
-        feats = torch.empty(B, samp._feat_dim(), device=logits.device)
-        N.check(N.lib().abcd_sampler_sample(samp._scfg(), samp._sparams(), N.ptr(logits), B, mode, tau,
-                                            N.ptr(noise_t), seed, offset, N.ptr(feats), N.ptr(ws), ws.numel(),
-                                            N.stream()), "sampler sample")
-        ctx.samp, ctx.ws, ctx.mode, ctx.tau, ctx.B = samp, ws, mode, tau, B
-        return feats
-
-    @staticmethod
-    @torch.autograd.function.once_differentiable
-    def backward(ctx, d_feats):
-        samp = ctx.samp
-        d_logits = torch.empty(ctx.B, samp._logit_width(), device=d_feats.device)
-        d_cb = torch.empty_like(samp.codebook) if isinstance(samp, ABCDSampler) else None
-        N.check(N.lib().abcd_sampler_sample_backward(samp._scfg(), samp._sparams(), ctx.B, ctx.mode, ctx.tau,
-                                                     N.ptr(d_feats.contiguous()), N.ptr(d_logits), N.ptr(d_cb),
-                                                     N.ptr(ctx.ws), ctx.ws.numel(), N.stream()),
-                "sampler sample backward")
-        grads = [None] * len(samp._sample_params())
-        if d_cb is not None:
-            grads[0] = d_cb
-        return (None, d_logits, None, None, None, None, None, None) + tuple(grads)
-
-
-class _KLFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, samp, logits, Ntot, ws, *params):
-        B = logits.shape[0]
-        kl = torch.empty((), device=logits.device)
-        N.check(N.lib().abcd_sampler_kl(samp._scfg(), samp._sparams(), N.ptr(logits), B, float(Ntot), N.ptr(kl),
-                                        N.ptr(ws), ws.numel(), N.stream()), "sampler kl")
-        ctx.samp, ctx.ws, ctx.B, ctx.N = samp, ws, B, float(Ntot)
-        return kl
-
-    @staticmethod
-    @torch.autograd.function.once_differentiable
-    def backward(ctx, d_kl):
-        samp = ctx.samp
-        d_logits = torch.empty(ctx.B, samp._logit_width(), device=d_kl.device)
-        d_psl = torch.empty_like(samp.posterior_shape_logits) if isinstance(samp, ABCDSampler) else None
-        N.check(N.lib().abcd_sampler_kl_backward(samp._scfg(), samp._sparams(), ctx.B, ctx.N,
-                                                 N.ptr(d_kl.contiguous()), 0, N.ptr(d_logits), N.ptr(d_psl),
-                                                 N.ptr(ctx.ws), ctx.ws.numel(), N.stream()), "sampler kl backward")
-        grads = [None] * len(samp._kl_params())
-        if d_psl is not None:
-            grads[0] = d_psl
-        return (None, d_logits, None, None) + tuple(grads)
-
-
-def _ws_of(samp, logits):
-    ws = getattr(logits, "_abcd_ws", None)
-    if ws is None:
-        ws = samp._ws_for(logits.shape[0], logits.device)
-        try:
-            logits._abcd_ws = ws
-        except Exception:
-            pass
-    return ws
+    def _mlp_weights(self):
+        return [t for m in self._mlps() for t in m.weights()]
 
 
 class ABCDSampler(_SamplerBase):
@@ -471,59 +345,27 @@ class ABCDSampler(_SamplerBase):
     def _feat_dim(self):
         return self.to_code_like.output_size
 
-    def _sample_params(self):
-        return [self.codebook]
-
-    def _kl_params(self):
-        return [self.posterior_shape_logits]
-
-    def _grad_views_forward(self):
-        w1, b1, w2, b2 = self.to_code_like.weights()
-        return {"mlp0.w1": torch.empty_like(w1), "mlp0.b1": torch.empty_like(b1), "mlp0.w2": torch.empty_like(w2),
-                "mlp0.b2": torch.empty_like(b2), "codebook": torch.empty_like(self.codebook)}
-
-    def _order_grads(self, views):
-        # parameter order of the Function call: to_code_like (w1,b1,w2,b2), codebook
-        return (views["mlp0.w1"], views["mlp0.b1"], views["mlp0.w2"], views["mlp0.b2"], views["codebook"])
-
     # -- reference API --
     def forward(self, x):
-        params = list(self.to_code_like.weights()) + [self.codebook]
-        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
-            return _SamplerForwardFn.apply(self, x, *params)
-        out, ws = self._run_forward(x)
-        out._abcd_ws = ws
-        return out
+        return ops.sampler(_f32c(x), self._mlp_weights(), self.codebook, self._cfg_list())[0]
 
     def sample(self, logits, no_sample=False):
         logits = _f32c(logits)
         N.require_gpu(logits)
-        ws = _ws_of(self, logits)
         B, K = logits.shape
         if no_sample:
             mode, tau, nt, seed, off = N.SAMPLE_SOFTMAX, 1.0, None, 0, 0
         else:
             mode, tau = N.SAMPLE_GUMBEL, float(self.temperature)
             nt, seed, off = _noise.gumbel(B, K, logits.device)
-        if torch.is_grad_enabled() and (logits.requires_grad or self.codebook.requires_grad):
-            return _SampleFn.apply(self, logits, mode, tau, ws, nt, seed, off, self.codebook)
-        feats = torch.empty(B, self._feat_dim(), device=logits.device)
-        N.check(N.lib().abcd_sampler_sample(self._scfg(), self._sparams(), N.ptr(logits), B, mode, tau, N.ptr(nt),
-                                            seed, off, N.ptr(feats), N.ptr(ws), ws.numel(), N.stream()),
-                "sampler sample")
-        return feats
+        return ops.sampler_sample(logits, self.codebook, self._cfg_list(), mode, tau, nt, ops._i64(seed),
+                                  ops._i64(off))[0]
 
     def kl_divergence(self, logits, entire_data_size):
         logits = _f32c(logits)
         N.require_gpu(logits)
-        ws = _ws_of(self, logits)
-        if torch.is_grad_enabled() and (logits.requires_grad or self.posterior_shape_logits.requires_grad):
-            return _KLFn.apply(self, logits, entire_data_size, ws, self.posterior_shape_logits)
-        kl = torch.empty((), device=logits.device)
-        N.check(N.lib().abcd_sampler_kl(self._scfg(), self._sparams(), N.ptr(logits), logits.shape[0],
-                                        float(entire_data_size), N.ptr(kl), N.ptr(ws), ws.numel(), N.stream()),
-                "sampler kl")
-        return kl
+        return ops.sampler_kl(logits, self.posterior_shape_logits, self._cfg_list(), self._prior_value(),
+                              float(entire_data_size))[0]
 
     def log_pmf(self, targets, logits):
         return torch.nn.functional.cross_entropy(logits, targets, reduction="sum")
@@ -577,30 +419,9 @@ class Sampler(_SamplerBase):
     def _feat_dim(self):
         return self.to_parameters.output_size
 
-    def _sample_params(self):
-        return []
-
-    def _kl_params(self):
-        return []
-
-    def _grad_views_forward(self):
-        v = {}
-        for k, m in enumerate(self._mlps()):
-            for f, t in zip(("w1", "b1", "w2", "b2"), m.weights()):
-                v[f"mlp{k}.{f}"] = torch.empty_like(t)
-        return v
-
-    def _order_grads(self, views):
-        return tuple(views[f"mlp{k}.{f}"] for k in range(2) for f in ("w1", "b1", "w2", "b2"))
-
     def forward(self, parameter_seed):
-        params = [t for m in self._mlps() for t in m.weights()]
         f = self.to_parameters.output_size
-        if torch.is_grad_enabled() and (parameter_seed.requires_grad or any(p.requires_grad for p in params)):
-            mv = _SamplerForwardFn.apply(self, parameter_seed, *params)
-        else:
-            mv, ws = self._run_forward(parameter_seed)
-            mv._abcd_ws = ws
+        mv = ops.sampler(_f32c(parameter_seed), self._mlp_weights(), None, self._cfg_list())[0]
         mu, lv = mv[:, :f], mv[:, f:]
         mu._abcd_mv = mv
         return [mu, lv]
@@ -610,28 +431,16 @@ class Sampler(_SamplerBase):
         mv = getattr(mu, "_abcd_mv", None)
         if mv is None:  # parameters not produced by this module's forward: reference torch formula
             return self._sampler(*parameters)
-        ws = _ws_of(self, mv)
         B, f = mu.shape
         nt, seed, off = _noise.normal(B, f, mu.device)
-        if torch.is_grad_enabled() and mv.requires_grad:
-            return _SampleFn.apply(self, mv, 0, 1.0, ws, nt, seed, off)
-        feats = torch.empty(B, f, device=mu.device)
-        N.check(N.lib().abcd_sampler_sample(self._scfg(), self._sparams(), N.ptr(mv), B, 0, 1.0, N.ptr(nt), seed,
-                                            off, N.ptr(feats), N.ptr(ws), ws.numel(), N.stream()), "plain sample")
-        return feats
+        return ops.sampler_sample(mv, None, self._cfg_list(), 0, 1.0, nt, ops._i64(seed), ops._i64(off))[0]
 
     def kl_divergence(self, parameters):
         mu, lv = parameters
         mv = getattr(mu, "_abcd_mv", None)
         if mv is None:
             return self._kl_divergence(*parameters)
-        ws = _ws_of(self, mv)
-        if torch.is_grad_enabled() and mv.requires_grad:
-            return _KLFn.apply(self, mv, 1.0, ws)
-        kl = torch.empty((), device=mu.device)
-        N.check(N.lib().abcd_sampler_kl(self._scfg(), self._sparams(), N.ptr(mv), mu.shape[0], 1.0, N.ptr(kl),
-                                        N.ptr(ws), ws.numel(), N.stream()), "plain kl")
-        return kl
+        return ops.sampler_kl(mv, None, self._cfg_list(), 1.0, 1.0)[0]
 
     def log_pdf(self, samples, parameters):
         return self._log_pdf(samples, *parameters)
@@ -644,33 +453,6 @@ class Sampler(_SamplerBase):
 # ----------------------------------------------------------------------------
 # Decoder (model.py:84-285)
 # ----------------------------------------------------------------------------
-class _DecoderFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, dec, features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, xmask, *params):
-        res = dec._run_forward(features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, xmask=xmask)
-        em, off, flat, mu, lv, offl, ws = res
-        ctx.dec, ctx.ws = dec, ws
-        ctx.saved = (features, batch_sizes, speaker, gt, gt_off, xmask)
-        ctx.feedback = dec._feedback()
-        ctx.mark_non_differentiable(flat, mu, lv, offl)
-        ctx.set_materialize_grads(False)
-        return em, off, flat, mu, lv, offl
-
-    @staticmethod
-    @torch.autograd.function.once_differentiable
-    def backward(ctx, d_em, d_off, d_flat, d_mu, d_lv, d_offl):
-        if any(g is not None for g in (d_flat, d_mu, d_lv, d_offl)):
-            raise NotImplementedError("decoder backward supports gradients of the emission and offset losses only")
-        features, batch_sizes, speaker, gt, gt_off, xmask = ctx.saved
-        dev = features.device
-        z = torch.zeros((), device=dev)
-        d_em = z if d_em is None else d_em.reshape(()).contiguous()
-        d_off = z if d_off is None else d_off.reshape(()).contiguous()
-        d_feat, grads = ctx.dec._run_backward(features, batch_sizes, speaker, gt, gt_off, d_em, d_off, ctx.ws,
-                                              feedback=ctx.feedback, xmask=xmask)
-        return (None, d_feat, None, None, None, None, None, None, None, None) + tuple(grads)
-
-
 class RNN_Variational_Decoder(torch.nn.Module):
     """Self-feedback LSTM/GRU decoder with isotropic-Gaussian emission and an
     end-of-segment (offset) predictor, unidirectional (model.py:84-196)."""
@@ -756,55 +538,10 @@ class RNN_Variational_Decoder(torch.nn.Module):
     def workspace_bytes(self, T, L, B):
         return N.lib().abcd_decoder_workspace_bytes(self._dcfg(1), T, L, B)
 
-    def _run_forward(self, features, batch_sizes, speaker, gt, gt_off, eps, seed, offset, ws=None,
-                     want_outputs=True, xmask=None):
-        features = _f32c(features)
-        N.require_gpu(features)
-        cfg = self._dcfg()
-        pk, bs = _packed_struct(gt, batch_sizes, cfg.output_size)
-        L = N.lib()
-        nbytes = L.abcd_decoder_workspace_bytes(cfg, pk.T, pk.L, pk.B)
-        if nbytes == 0:
-            raise N.HipError("decoder: unsupported configuration (sizes must be multiples of 16)")
-        if ws is None or ws.numel() < nbytes:
-            ws = N.workspace(nbytes, features.device)
-        dev = features.device
-        F = cfg.output_size
-        spk = None
-        if self.embed_speaker is not None:
-            spk = speaker.to(dev, torch.int64).contiguous()
-        flat = mu = lv = None
-        if want_outputs:
-            flat = torch.empty(pk.L, F, device=dev)
-            mu = torch.empty(pk.L, F, device=dev)
-            lv = torch.empty(pk.L, F, device=dev)
-        offl = torch.empty(pk.L, device=dev)
-        losses = torch.zeros(2, device=dev)
-        N.check(L.abcd_decoder_forward_dropout(cfg, self._dparams(), pk, N.ptr(features), N.ptr(spk),
-                                               N.ptr(None if gt_off is None else _f32c(gt_off)), N.ptr(eps),
-                                               N.ptr(xmask), seed, offset, N.ptr(flat), N.ptr(mu), N.ptr(lv),
-                                               N.ptr(offl), N.ptr(losses), N.ptr(ws), ws.numel(), N.stream()),
-                "decoder forward")
-        em = losses[0] if gt is not None else None
-        off = losses[1] if gt_off is not None else None
-        return em, off, flat, mu, lv, offl, ws
-
-    def _run_backward(self, features, batch_sizes, speaker, gt, gt_off, d_em, d_off, ws, grad_tensors=None,
-                      feedback=None, d_features=None, xmask=None):
-        cfg = self._dcfg(feedback)
-        pk, bs = _packed_struct(gt, batch_sizes, cfg.output_size)
-        dev = features.device
-        spk = speaker.to(dev, torch.int64).contiguous() if self.embed_speaker is not None else None
-        if grad_tensors is None:
-            grad_tensors = [torch.empty_like(p) for p in self._param_list()]
-        if d_features is None:
-            d_features = torch.empty_like(features)
-        N.check(N.lib().abcd_decoder_backward_dropout(cfg, self._dparams(), pk, N.ptr(features), N.ptr(spk),
-                                                      N.ptr(_f32c(gt_off)), N.ptr(xmask), N.ptr(d_em), N.ptr(d_off),
-                                                      N.ptr(d_features), self._dparams(grad_tensors), N.ptr(ws),
-                                                      ws.numel(), N.stream(), None),
-                "decoder backward")
-        return d_features, grad_tensors
+    def _cfg_list(self, feedback=None):
+        c = self._dcfg(feedback)
+        return [c.output_size, c.hidden_size, c.mlp_hidden, c.feature_size, c.rnn_type, c.feedback, c.num_speakers,
+                c.speaker_dim]
 
     # -- reference API --
     def forward(self, features, lengths=None, batch_sizes=None, speaker=None, ground_truth_out=None,
@@ -816,18 +553,13 @@ class RNN_Variational_Decoder(torch.nn.Module):
             batch_sizes = torch.tensor([int(b) for b in batch_sizes], dtype=torch.int64)
         F = self.rnn_cell.cell.input_size
         eps, seed, offset, xmask = _noise.decoder_noise(batch_sizes, F, self._input_dropout_p(), features.device)
-        params = self._param_list()
-        gt = ground_truth_out
-        gt_off = ground_truth_offset
-        if (gt is not None and gt_off is not None and torch.is_grad_enabled()
-                and (features.requires_grad or any(p.requires_grad for p in params))):
-            em, off, flat, mu, lv, offl = _DecoderFn.apply(self, features, batch_sizes, speaker, _f32c(gt),
-                                                           gt_off, eps, seed, offset, xmask, *params)
-        else:
-            em, off, flat, mu, lv, offl, _ = self._run_forward(features, batch_sizes, speaker,
-                                                               None if gt is None else _f32c(gt), gt_off, eps,
-                                                               seed, offset, xmask=xmask)
-        return em, off, flat, (mu, lv), offl
+        gt = None if ground_truth_out is None else _f32c(ground_truth_out)
+        gt_off = None if ground_truth_offset is None else _f32c(ground_truth_offset)
+        spk = speaker if self.embed_speaker is not None else None
+        em, off, flat, mu, lv, offl, _ws = ops.decoder(_f32c(features), batch_sizes, spk, gt, gt_off, eps,
+                                                       ops._i64(seed), ops._i64(offset), xmask, self._param_list(),
+                                                       self._cfg_list())
+        return (em if gt is not None else None), (off if gt_off is not None else None), flat, (mu, lv), offl
 
     def _length_to_batch_sizes(self, lengths):
         lengths = torch.as_tensor(lengths).cpu()

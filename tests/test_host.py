@@ -142,3 +142,17 @@ def test_reference_checkpoint_loads_into_product_modules():
         m.load_state_dict(ck[key])
         for name, v in m.state_dict().items():
             assert torch.equal(v, ck[key][name]), (key, name)
+
+
+def test_custom_ops_registered():
+    """The module classes call the C ABI through torch.library custom
+    operators (modules/ops.py): every forward op has an autograd formula and a
+    fake (meta) implementation, and takes no Python objects."""
+    import torch
+    from modules import ops
+    assert list(ops.registered()) == list(ops.OPS)
+    for name in ops.OPS:
+        schema = str(getattr(torch.ops.abcd, name).default._schema)
+        assert schema.startswith(f"abcd::{name}("), schema
+        assert "(a!)" not in schema and "(a1!)" not in schema, schema  # functional: no mutated inputs
+    assert ops._u64(ops._i64(0xF00DF00DF00DF00D)) == 0xF00DF00DF00DF00D
