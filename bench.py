@@ -67,12 +67,9 @@ def flops_per_step(cfg, L, B):
     return 3 * ((enc + dec) * L + seg * B)
 
 
-# persistent recurrent kernels: id (abcd_timing_read_kernel), rocprof symbol
-# timing ids of the persistent-kernel roles (abcd_timing_*); at c2 the library
-# dispatches them to the kernels named in ROLE_KERNELS
+# timing ids of the persistent-kernel roles (abcd_timing_*); the kernel each
+# role dispatched is read back from the library (abcd_dispatch_name)
 KERNELS = {1: "enc_fwd", 2: "enc_bwd", 3: "dec_fwd", 4: "dec_bwd"}
-ROLE_KERNELS = {"enc_fwd": "abcd::enc_fwd_persist<4,16,8>", "enc_bwd": "abcd::enc_bwd_sk<4,16>",
-                "dec_fwd": "abcd::dec_fwd_x6<13,8,8>", "dec_bwd": "abcd::dec_bwd_sk<9,16,16>"}
 
 
 def kernel_flops_per_frame(cfg, kid):
@@ -277,7 +274,7 @@ def main():
         "step_tflops": round(fl / (elapsed / args.steps) / 1e12, 3),
     }
     if not args.no_kernel_timing:
-        out["roofline"] = kernel_roofline(step, batches, cfg, run)
+        out["roofline"] = kernel_roofline(step, batches, cfg, run, args.config)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], parity = cpu_baseline(cfg, args.config, device)
         out["recon_loss_rel_delta"] = parity["recon_loss_rel_delta"]
@@ -288,21 +285,24 @@ def main():
         dist.destroy_process_group()
 
 
-def load_traffic(kernel):
+def load_traffic(kernel, cfg_name):
     """HBM bytes per launch of `kernel` from the rocprofv3 PMC passes committed
     under profiles/ (scripts/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, the
-    gfx950 correction of MI355X_MICROARCH.md), or None."""
+    gfx950 correction of MI355X_MICROARCH.md) for this configuration, or None
+    (no PMC pass of this configuration is committed)."""
     path = os.path.join(REPO, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
+        if t.get("config", "c2") != cfg_name:
+            return None
         e = t["kernels"][kernel]
         return int(e["hbm_bytes_per_launch"])
     except (OSError, KeyError, ValueError):
         return None
 
 
-def kernel_roofline(step, batches, cfg, run):
+def kernel_roofline(step, batches, cfg, run, cfg_name):
     """Roofline of the dominant kernel: the persistent recurrent kernel with
     the largest device time.  Its launches are bracketed live with HIP events
     on the launch stream by the library (abcd_timing_*); `achieved` =
@@ -334,8 +334,10 @@ def kernel_roofline(step, batches, cfg, run):
     dom = max(per, key=lambda k: per[k]["avg_launch_us"] * per[k]["launches"])
     d = per[dom]
     achieved = d["tflops"]
-    traffic = load_traffic(dom)
-    return {"bound": "mfma", "kernel": dom, "kernel_symbol": ROLE_KERNELS.get(dom), "achieved": achieved,
+    traffic = load_traffic(dom, cfg_name)
+    symbol = N.dispatch().get(dom, ("", 0))[0]
+    return {"bound": "mfma", "kernel": dom, "kernel_symbol": "abcd::" + symbol if symbol else None,
+            "achieved": achieved,
             "peak": PEAK_FP32_MFMA_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
             "avg_launch_us": d["avg_launch_us"], "launches": d["launches"],

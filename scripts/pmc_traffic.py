@@ -46,9 +46,11 @@ def read_pass(d, counter):
 
 def main():
     fetch_dir, write_dir, out = sys.argv[1:4]
+    cfg = sys.argv[4] if len(sys.argv) > 4 else "c2"
     fetch, nf = read_pass(fetch_dir, "FETCH_SIZE")
     write, nw = read_pass(write_dir, "WRITE_SIZE")
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py c2",
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py --config {cfg}",
+           "config": cfg,
            "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts 1/2)",
            "kernels": {}}
     for k in KERNELS:
