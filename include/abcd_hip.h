@@ -141,11 +141,15 @@ int abcd_sampler_kl(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, c
  * values and backward stash as the three calls above.  ABCD: two launches --
  * the split-K h W1^T GEMM and one row-tiled sampler-head kernel (MLP tail,
  * logits, Gumbel-softmax, y C^T and the KL row terms per 16-row tile, the KL
- * scalar reduced by the last tile).  plain: the three calls in turn. */
+ * scalar reduced by the last tile).  plain: the three calls in turn.
+ * ppl_out (ABCD, may be NULL): ppl_out[0..1] = the cluster and batch
+ * perplexities of abcd_perplexities on these logits (reduced by the same
+ * last tile); ppl_out[2] is left to abcd_shape_perplexity (it reads
+ * posterior_shape_logits after the SGD step, learning.py:171-178). */
 int abcd_sampler_forward_fused(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
                                int mode, float temperature, const float* noise, uint64_t seed, uint64_t offset,
-                               double entire_data_size, float* logits, float* feats, float* kl_out, void* ws,
-                               size_t ws_bytes, void* stream);
+                               double entire_data_size, float* logits, float* feats, float* kl_out, float* ppl_out,
+                               void* ws, size_t ws_bytes, void* stream);
 /* backward of forward+sample+kl.  d_feats: B x D (may be NULL); d_kl: device
  * scalar upstream grad of kl (may be NULL); d_h: B x E (may be NULL). */
 int abcd_sampler_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
@@ -183,6 +187,8 @@ int abcd_sampler_forward_backward(const abcd_sampler_cfg* cfg, const abcd_sample
  * batch-mean / Dirichlet-shape perplexities (device floats) */
 int abcd_perplexities(const float* logits, int B, int K, const float* posterior_shape_logits, float* out,
                       void* stream);
+/* out[0] = exp(entropy of softmax(posterior_shape_logits)) (abcd_perplexities' out[2]) */
+int abcd_shape_perplexity(const float* posterior_shape_logits, int K, float* out, void* stream);
 
 /* ------------------------------------------------------------------------
  * Decoder: RNN_Variational_Decoder (model.py:84-196, unidirectional)

@@ -522,6 +522,155 @@ __global__ __launch_bounds__(256, 2) void gemm_x6s_kernel(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// gemm_x6f: split-fp32 GEMM for two K-contiguous operands (element (row, k)
+// at P[row * ld + k]: the frame-parallel projections).  gemm_x6s keeps fp32
+// slabs in LDS and every wave splits the fragments it reads (8 fragment
+// splits per wave and chunk, each fragment split by two waves); here each
+// 32-deep chunk of the A and B tiles is read from global once per workgroup
+// (two f4 per 8 k), split once into the three bf16 planes and stored in
+// fragment order ([subtile][plane][lane] x 16 B), so a wave reads each
+// fragment plane with one conflict-free ds_read_b128 and issues only MFMAs.
+// Per chunk and thread: 4 splits of 8 values (the tile's 2 x 128 x 32
+// values over 256 threads), 12 16-B LDS writes; per wave 24 ds_read_b128 and
+// 96 MFMAs.  Loads go through buffer resources (rows >= M / N and k >= K read
+// 0), so the staging is branch-free.  Input projection at c2: 458 us
+// against gemm_x6s's 515 us (VALU per MFMA 7.4 -> 4.4, PMC); offset head
+// 100 vs 110 us.
+// ---------------------------------------------------------------------------
+template <int MR, int NR>
+__global__ __launch_bounds__(256, 2) void gemm_x6f_kernel(const float* __restrict__ A, long lda,
+                                                       const float* __restrict__ B, long ldb, int K, EpiArgs e,
+                                                       int remap) {
+  extern __shared__ __attribute__((aligned(16))) f4 fsm[];
+  constexpr int BM = 32 * MR, BN = 32 * NR, SA = BM / 16, SB = BN / 16;
+  constexpr int STAGE = (SA + SB) * 3 * 64;  // f4 per stage
+  constexpr int GA = BM * 4, GT = (BM + BN) * 4;  // groups of 8 k per chunk: A, A + B
+  constexpr int UPT = GT / 256;                   // groups per thread
+  static_assert(GT % 256 == 0 && GA % 256 == 0, "whole groups per thread");
+  const dim3 bid = xcd_tile(remap != 0);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = bid.y * BM, n0 = bid.x * BN;
+  const int M = e.M, N = e.N, nch = (K + 31) / 32;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A, (uint32_t)((size_t)M * lda * 4));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(B, (uint32_t)((size_t)N * ldb * 4));
+  auto gload = [&](int c, f4 (&v)[UPT][2]) {
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      const int g = threadIdx.x + 256 * u;
+      const bool isB = g >= GA;  // uniform per u
+      // group gi -> fragment slot: lane ln = gi & 63 of subtile gi >> 6 (row 16 sub + (ln & 15), k 8 (ln >> 4))
+      const int gi = isB ? g - GA : g, ln = gi & 63, row = ((gi >> 6) << 4) + (ln & 15), qq = ln >> 4;
+      const int k = c * 32 + 8 * qq;
+      const bool ok = (isB ? n0 + row < N : m0 + row < M) && k < K;
+      const uint32_t o = ok ? (uint32_t)(((isB ? (long)(n0 + row) * ldb : (long)(m0 + row) * lda) + k) * 4)
+                            : 0x80000000u;
+      const __amdgpu_buffer_rsrc_t rs = isB ? rb : ra;
+      v[u][0] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+      v[u][1] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? o + 16u : o, 0, 0));
+    }
+  };
+  auto lstore = [&](int buf, const f4 (&v)[UPT][2]) {
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      const int g = threadIdx.x + 256 * u;
+      const bool isB = g >= GA;
+      const int gi = isB ? g - GA : g, ln = gi & 63;
+      const int sub = (isB ? SA : 0) + (gi >> 6);
+      bf8 h, m, l;
+      split8(v[u][0], v[u][1], h, m, l);
+      f4* dst = fsm + buf * STAGE + sub * 3 * 64 + ln;  // consecutive lanes, consecutive 16-B slots
+      dst[0] = __builtin_bit_cast(f4, h);
+      dst[64] = __builtin_bit_cast(f4, m);
+      dst[128] = __builtin_bit_cast(f4, l);
+    }
+  };
+  f4 acc[MR][NR];
+  acc_zero(acc);
+  auto compute = [&](int buf) {
+    const f4* st = fsm + buf * STAGE;
+    bf8 bp[NR][3];
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bp[j][p] = __builtin_bit_cast(bf8, st[((SA + wn * NR + j) * 3 + p) * 64 + lane]);
+    constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      bf8 ap[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) ap[p] = __builtin_bit_cast(bf8, st[((wm * MR + i) * 3 + p) * 64 + lane]);
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = mfma_bf(ap[TA[t]], bp[j][TB[t]], acc[i][j]);
+    }
+  };
+  // one LDS stage (48 KiB: two workgroups per CU); the next chunk's global
+  // loads are in flight during this chunk's MFMAs.  Measured at the input
+  // projection shape: 458 us against 685 us for a double-buffered stage at
+  // one workgroup per CU and 475 us with two chunks of loads in flight
+  f4 v[UPT][2];
+  gload(0, v);
+  lstore(0, v);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+    if (more) gload(c + 1, v);
+    compute(0);
+    __syncthreads();  // every wave is done reading the stage
+    if (more) lstore(0, v);
+    __syncthreads();
+  }
+  // epilogue: wave-private LDS transpose, whole-row 16-B stores (as gemm_x6s_kernel)
+  const int r = lane & 15, q = lane >> 4;
+  constexpr int SW = 16 * NR, SP = SW + 4;
+  float* stg = reinterpret_cast<float*>(fsm) + w * 16 * SP;
+  float* const dst = e.C;
+  const long ldd = e.ldc;
+  const bool vec = (ldd % 4 == 0) && (((uintptr_t)dst & 15) == 0);
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int pp = 0; pp < NR; ++pp) {
+      const int lr = (lane + 64 * pp) / (4 * NR), c4 = (lane + 64 * pp) % (4 * NR);
+      const int gcol = n0 + wn * SW + 4 * c4;
+      const int row = m0 + wm * 16 * MR + 16 * i + lr;
+      f4 val = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
+      if (row < M) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (gcol + t < N) val[t] = apply_epi(e, row, gcol + t, val[t]);
+        float* d = dst + (long)row * ldd + gcol;
+        if (vec && gcol + 4 <= N) *reinterpret_cast<f4*>(d) = val;
+        else
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (gcol + t < N) d[t] = val[t];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int MR, int NR>
+static int gemm_x6f_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                           EpiArgs e) {
+  constexpr int BM = 32 * MR, BN = 32 * NR;
+  const size_t lds = (size_t)(BM / 16 + BN / 16) * 3 * 64 * 16;
+  gemm_x6f_kernel<MR, NR><<<dim3(cdiv(N, BN), cdiv(M, BM), 1), 256, lds, s>>>(A, lda, B, ldb, K, e, 1);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int MR, int NR, bool AKC, bool BKC>
 static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
                            EpiArgs e, float* scratch, size_t scratch_floats) {
@@ -571,6 +720,7 @@ static bool tn_ok(const Operand& o, int rows) {
   return o.kmajor && o.ld % 4 == 0 && ((uintptr_t)o.p % 16) == 0 && o.ld >= ((rows + 3) & ~3);
 }
 
+
 int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, long ldc, float alpha,
          float beta, const float* bias, int act, float* scratch, size_t scratch_floats) {
   if (M <= 0 || N <= 0) return 0;
@@ -587,7 +737,12 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
     // ~1.6x the direct-fragment gemm_big at the input-projection shape)
     if (cdiv(M, 128) * cdiv(N, 128) >= 240 && A.nrows >= M && B.nrows >= N && A.ld % 4 == 0 && B.ld % 4 == 0 &&
         ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0) {
-      if (!tl_side) return gemm_x6s_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
+      if (!tl_side) {
+        // fragment-staged form (one split per workgroup) when both operands fit a buffer resource
+        if (K % 8 == 0 && (size_t)M * A.ld * 4 < (1ull << 31) && (size_t)N * B.ld * 4 < (1ull << 31))
+          return gemm_x6f_launch<4, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
+        return gemm_x6s_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
+      }
       if (N >= 256) return gemm_tn_launch<4, 8, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
       return gemm_tn_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
     }

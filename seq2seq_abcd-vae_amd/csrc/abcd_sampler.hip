@@ -438,6 +438,10 @@ struct HeadFwdArgs {
   double* klpart;                                   // per-tile sum_b v_b
   float* kl_out;
   float *CT, *W2T;   // K x D and Hm x D transposed copies for the backward (each tile writes a slice)
+  // learning.py:171-178 cluster / batch perplexities of this forward (null: skipped)
+  float* ppl;        // [exp(mean row entropy of Q), exp(entropy of the batch-mean Q)]
+  double* entpart;   // per-tile sum of row entropies
+  float* qcolpart;   // tiles x K column sums of Q
 };
 inline size_t head_fwd_lds(int Hm, int D, int K) {
   return ((size_t)HEAD_ROWS * (std::max(Hm, K) + 4) + (size_t)HEAD_ROWS * (std::max(D, K) + 4) + 2 * (size_t)K) * 4 +
@@ -550,7 +554,10 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
   // Y = softmax((logits + g) / tau) (sample_softmax_rows), one wave per row,
   // the row's KPL logits per lane in registers
   const float it = 1.f / a.tau;
-  double klsum = 0.0;
+  double klsum = 0.0, entsum = 0.0;
+  float qcol[KPL];
+#pragma unroll
+  for (int u = 0; u < KPL; ++u) qcol[u] = 0.f;
   for (int rr = 0; rr < HEAD_ROWS / 4; ++rr) {
     const int row = w * (HEAD_ROWS / 4) + rr;
     float* y = R2 + row * ld2;
@@ -576,7 +583,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     for (int u = 0; u < KPL; ++u) se += lane + 64 * u < K ? __expf(lv[u] - m) : 0.f;
     se = wave_sum(se);
     const float ls = __logf(se);
-    float acc = 0.f;
+    float acc = 0.f, ent = 0.f;
 #pragma unroll
     for (int u = 0; u < KPL; ++u) {
       const int k = lane + 64 * u;
@@ -585,11 +592,15 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
         const float qv = __expf(lq);
         a.Q[g0 + k] = qv;
         acc += qv * (lq - elogL[k]);
+        ent += -qv * lq;
+        qcol[u] += qv;
       }
     }
     acc = wave_sum(acc);
+    ent = wave_sum(ent);
     if (lane == 0) a.v[row0 + row] = acc;
     klsum += acc;
+    entsum += ent;
     float m2 = -INFINITY;
 #pragma unroll
     for (int u = 0; u < KPL; ++u) {
@@ -619,8 +630,16 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
       }
     }
   }
-  if (lane == 0) sh[w] = klsum;
+  if (lane == 0) {
+    sh[w] = klsum;
+    sh[4 + w] = entsum;
+  }
   __syncthreads();
+  if (a.ppl) {  // the waves' Q column sums into the (now free) logits region
+#pragma unroll
+    for (int u = 0; u < KPL; ++u)
+      if (lane + 64 * u < K) R1[w * K + lane + 64 * u] = qcol[u];
+  }
   // feats = Y C^T
   tile_mma_any(R2, ld2, K, bkc(a.C, K, D), D, w, lane, [&](int c0, f4 acc) {
 #pragma unroll
@@ -629,13 +648,55 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
       if (row < nr) a.feats[(long)(row0 + row) * D + c0 + r] = acc[g];
     }
   });
-  if (!a.kl_out) return;
-  if (tid == 0) st_agent(a.klpart + blockIdx.x, (sh[0] + sh[1]) + (sh[2] + sh[3]));
-  if (last_workgroup(&g_head_ticket[0], flag) && w == 0) {
+  if (!a.kl_out && !a.ppl) return;
+  if (a.ppl) {
+    __syncthreads();
+    for (int k = tid; k < K; k += 256)
+      st_agent(a.qcolpart + (long)blockIdx.x * K + k, (R1[k] + R1[K + k]) + (R1[2 * K + k] + R1[3 * K + k]));
+  }
+  if (tid == 0) {
+    st_agent(a.klpart + blockIdx.x, (sh[0] + sh[1]) + (sh[2] + sh[3]));
+    st_agent(a.entpart + blockIdx.x, (sh[4] + sh[5]) + (sh[6] + sh[7]));
+  }
+  if (!last_workgroup(&g_head_ticket[0], flag)) return;
+  const int nt = gridDim.x;
+  if (a.kl_out && w == 0) {
     double t = 0.0;  // lane-strided partial sums, then a fixed shuffle tree: deterministic
-    for (int i = lane; i < (int)gridDim.x; i += 64) t += a.klpart[i];
+    for (int i = lane; i < nt; i += 64) t += a.klpart[i];
     t = wave_sum_d(t);
     if (lane == 0) *a.kl_out = (float)(a.kl_small[0] * ((double)a.B / a.N) + t);
+  }
+  if (!a.ppl) return;
+  // perplexities (perplex_kernel's formulas): exp(sum of row entropies / B),
+  // exp(entropy of the column sums normalised by their total)
+  double te = 0.0;
+  for (int i = tid; i < nt; i += 256) te += a.entpart[i];
+  te = block_sum_dd(te, sh);
+  double tot = 0.0;
+  for (int k = tid; k < K; k += 256) {
+    float c = 0.f;  // tile order, 8 tiles' loads in flight
+    int i = 0;
+    for (; i + 8 <= nt; i += 8) {
+      float v8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v8[u] = a.qcolpart[(long)(i + u) * K + k];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) c += v8[u];
+    }
+    for (; i < nt; ++i) c += a.qcolpart[(long)i * K + k];
+    R1[k] = c;
+    tot += c;
+  }
+  tot = block_sum_dd(tot, sh);
+  double be = 0.0;
+  for (int k = tid; k < K; k += 256) {
+    const double bm = R1[k] / tot;
+    if (bm > 0) be += -bm * log(bm);
+  }
+  be = block_sum_dd(be, sh);
+  if (tid == 0) {
+    a.ppl[0] = (float)exp(te / a.B);
+    a.ppl[1] = (float)exp(be);
   }
 }
 
@@ -880,6 +941,9 @@ struct SampWS {
   float *FU, *YdL;     // stacked dC operands: [d_feats; U] (2B x D), [Y; dL / sqrt(D)] (2B x K)
   float* colpart;      // sampler head backward: per-tile column sums
   double* klpart;      // sampler head forward: per-tile KL row sums
+  double* entpart;     // ... per-tile row-entropy sums (perplexities)
+  float* qcolpart;     // ... per-tile Q column sums (perplexities)
+  float* ppl3;         // per-method perplexities (fused entry's fallback)
   float* scratch;
   size_t scratch_floats;
 };
@@ -908,6 +972,7 @@ static SampWS carve_sampler(Arena& A, const abcd_sampler_cfg* c, int B) {
   w.Q = A.f((size_t)B * K); w.v = A.f(B);
   const int ntile = cdiv(B, HEAD_ROWS);
   w.colpart = A.f((size_t)ntile * (D + Hm + K)); w.klpart = A.d(ntile);
+  w.entpart = A.d(ntile); w.qcolpart = A.f((size_t)ntile * K); w.ppl3 = A.f(4);
   w.p = A.f(K); w.alpha = A.f(K); w.elog = A.f(K); w.tri = A.f(K); w.Qsum = A.f(K);
   w.MV = A.f((size_t)B * 2 * D); w.EPS = A.f((size_t)B * D);
   w.kl_small = A.d(8);
@@ -1022,7 +1087,7 @@ constexpr size_t HEAD_LDS_MAX = 160 * 1024;
 extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
                                           int B, int mode, float temperature, const float* noise, uint64_t seed,
                                           uint64_t offset, double N, float* logits, float* feats, float* kl_out,
-                                          void* ws, size_t ws_bytes, void* stream) {
+                                          float* ppl_out, void* ws, size_t ws_bytes, void* stream) {
   ABCD_REQUIRE(samp_check(c) == 0 && p && h && logits && feats && ws && B > 0);
   const int E = c->input_size, Hm = c->mlp_hidden, D = c->feature_dim, K = c->num_categories;
   const size_t lds = c->plain ? 0 : head_fwd_lds(Hm, D, K);
@@ -1030,7 +1095,15 @@ extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_
     ABCD_TRY((hipError_t)abcd_sampler_forward(c, p, h, B, logits, ws, ws_bytes, stream));
     ABCD_TRY((hipError_t)abcd_sampler_sample(c, p, logits, B, mode, temperature, noise, seed, offset, feats, ws,
                                              ws_bytes, stream));
-    return kl_out ? abcd_sampler_kl(c, p, logits, B, N, kl_out, ws, ws_bytes, stream) : 0;
+    if (kl_out) ABCD_TRY((hipError_t)abcd_sampler_kl(c, p, logits, B, N, kl_out, ws, ws_bytes, stream));
+    if (ppl_out && !c->plain) {  // the first two of abcd_perplexities' three values
+      Arena A(ws, ws_bytes);
+      SampWS w = carve_sampler(A, c, B);
+      ABCD_REQUIRE(A.ok);
+      ABCD_TRY((hipError_t)abcd_perplexities(logits, B, K, p->posterior_shape_logits, w.ppl3, stream));
+      ABCD_TRY(hipMemcpyAsync(ppl_out, w.ppl3, 2 * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    }
+    return 0;
   }
   ABCD_REQUIRE(mode == ABCD_SAMPLE_SOFTMAX || temperature > 0.f);
   ABCD_REQUIRE(!kl_out || N > 0);
@@ -1052,6 +1125,7 @@ extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_
   a.p = w.p; a.alpha = w.alpha; a.elog = w.elog; a.tri = w.tri; a.kl_small = w.kl_small;
   a.klpart = w.klpart; a.kl_out = kl_out;
   a.CT = w.CT; a.W2T = w.W2T[0];
+  a.ppl = ppl_out; a.entpart = w.entpart; a.qcolpart = w.qcolpart;
   const int grid = cdiv(B, HEAD_ROWS);
   ABCD_TRY((hipError_t)head_dispatch<HeadFwdLaunch>(K, a, grid, lds, s));
   note_dispatch(TK_SAMP_FWD, "gemm_slabs[%d] + samp_head_fwd grid %d", Z, grid);
@@ -1425,6 +1499,32 @@ __global__ __launch_bounds__(1024) void perplex_kernel(const float* logits, int 
     out[1] = (float)exp(tb);
     out[2] = (float)exp(tp);
   }
+}
+
+// exp(entropy of softmax(posterior_shape_logits)) (learning.py:176-178), one block
+__global__ void shape_ppl_kernel(const float* psl, int K, float* out) {
+  __shared__ double sh[16];
+  const int tid = threadIdx.x;
+  double m = -1e300;
+  for (int k = tid; k < K; k += blockDim.x) m = fmax(m, (double)psl[k]);
+  m = block_max_dd(m, sh);
+  double se = 0.0;
+  for (int k = tid; k < K; k += blockDim.x) se += exp((double)psl[k] - m);
+  se = block_sum_dd(se, sh);
+  double pe = 0.0;
+  for (int k = tid; k < K; k += blockDim.x) {
+    const double pp = exp((double)psl[k] - m) / se;
+    if (pp > 0) pe += -pp * log(pp);
+  }
+  pe = block_sum_dd(pe, sh);
+  if (tid == 0) *out = (float)exp(pe);
+}
+
+extern "C" int abcd_shape_perplexity(const float* psl, int K, float* out, void* stream) {
+  if (!psl || !out || K <= 0) return ABCD_EINVAL;
+  shape_ppl_kernel<<<1, 256, 0, (hipStream_t)stream>>>(psl, K, out);
+  ABCD_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int abcd_perplexities(const float* logits, int B, int K, const float* psl, float* out, void* stream) {

@@ -99,7 +99,7 @@ _SIGS = {
                                 c_size_t, c_void_p]),
     "abcd_sampler_forward_fused": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float,
                                            c_void_p, c_uint64, c_uint64, c_double, c_void_p, c_void_p, c_void_p,
-                                           c_void_p, c_size_t, c_void_p]),
+                                           c_void_p, c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float, c_double,
                                       c_void_p, c_void_p, c_void_p, _P(SamplerGrads), c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_backward_split": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float,
@@ -112,6 +112,7 @@ _SIGS = {
     "abcd_sampler_forward_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_void_p,
                                               c_void_p, _P(SamplerGrads), c_int, c_void_p, c_size_t, c_void_p]),
     "abcd_perplexities": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "abcd_shape_perplexity": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     "abcd_decoder_workspace_bytes": (c_size_t, [_P(DecoderCfg), c_int, c_int, c_int]),
     "abcd_decoder_forward": (c_int, [_P(DecoderCfg), _P(DecoderParams), _P(Packed), c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

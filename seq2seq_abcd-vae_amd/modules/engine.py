@@ -165,7 +165,9 @@ class FusedStep:
         # sampler-head kernel (logits, Gumbel-softmax, y C^T, KL) per step
         N.check(L_.abcd_sampler_forward_fused(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, N.ptr(nt), seed,
                                               off, float(entire_data_size), N.ptr(logits), N.ptr(feats),
-                                              N.ptr(sc[KL:KL + 1]), N.ptr(ws_s), ws_s.numel(), st), "sampler")
+                                              N.ptr(sc[KL:KL + 1]),
+                                              None if self.plain else N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 2]),
+                                              N.ptr(ws_s), ws_s.numel(), st), "sampler")
         F = self.decoder.rnn_cell.cell.input_size
         pdrop = self.decoder._input_dropout_p() if train else 0.0
         eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
@@ -240,10 +242,10 @@ class FusedStep:
         sc, logits = self.forward_backward(data, batch_sizes, is_offset, speakers, entire_data_size,
                                            is_pretraining, loss_batch=loss_batch)
         self.optimizer_step(lr, momentum, clip)
-        if not self.plain:  # learning.py:171-178 reads posterior_shape_logits AFTER the SGD step
-            N.check(N.lib().abcd_perplexities(N.ptr(logits), logits.shape[0], logits.shape[1],
-                                              N.ptr(self.sampler.posterior_shape_logits),
-                                              N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 3]), N.stream()), "perplexities")
+        if not self.plain:  # learning.py:171-178: cluster / batch perplexities came with the sampler head;
+            # the shape perplexity reads posterior_shape_logits AFTER the SGD step
+            N.check(N.lib().abcd_shape_perplexity(N.ptr(self.sampler.posterior_shape_logits), logits.shape[1],
+                                                  N.ptr(sc[PPL_SHAPE:PPL_SHAPE + 1]), N.stream()), "perplexities")
         N.check(N.lib().abcd_step_status(N.ptr(sc[STATUS:STATUS + 1]), N.stream()), "step status")
         return sc
 

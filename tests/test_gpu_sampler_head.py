@@ -80,8 +80,9 @@ def test_fused_head_matches_per_method_path(K, B, mode):
     wb = N.workspace(nbytes, dev)
     L.abcd_dispatch_reset()
     lb, fb, kb = torch.empty(B, K, device=dev), torch.empty(B, D, device=dev), torch.empty(1, device=dev)
+    pb = torch.zeros(3, device=dev)
     _ck(L.abcd_sampler_forward_fused(cfg, par, N.ptr(h), B, gmode, tau, N.ptr(noise), seed, off, NDATA,
-                                         N.ptr(lb), N.ptr(fb), N.ptr(kb), N.ptr(wb), wb.numel(), st))
+                                         N.ptr(lb), N.ptr(fb), N.ptr(kb), N.ptr(pb), N.ptr(wb), wb.numel(), st))
     gb, gsb = _grads(samp, dev)
     dhb = torch.empty(B, E, device=dev)
     _ck(L.abcd_sampler_backward_split(cfg, par, N.ptr(h), B, gmode, tau, NDATA, N.ptr(d_feats), N.ptr(d_kl),
@@ -95,6 +96,10 @@ def test_fused_head_matches_per_method_path(K, B, mode):
     assert _rel(fb, fa) < 1e-5
     assert abs(float(kb) - float(ka)) <= 1e-5 * abs(float(ka)) + 1e-6, (float(kb), float(ka))
     assert torch.equal(lb.argmax(-1), la.argmax(-1))
+    pa = torch.zeros(3, device=dev)  # the per-method perplexity kernel on the same logits
+    _ck(L.abcd_perplexities(N.ptr(la), B, K, N.ptr(samp.posterior_shape_logits), N.ptr(pa), st))
+    _ck(L.abcd_shape_perplexity(N.ptr(samp.posterior_shape_logits), K, N.ptr(pb[2:]), st))
+    assert _rel(pb, pa) < 1e-5, (pb, pa)
     assert _rel(dhb, dha) < 1e-4
     for k in ga:
         assert _rel(gb[k], ga[k]) < 1e-4, (k, _rel(gb[k], ga[k]))
@@ -117,13 +122,15 @@ def test_fused_head_repeatable():
     outs = []
     for _ in range(2):
         lg, ft, kl = torch.empty(B, K, device=dev), torch.empty(B, D, device=dev), torch.empty(1, device=dev)
+        pp = torch.empty(2, device=dev)
         _ck(L.abcd_sampler_forward_fused(cfg, par, N.ptr(h), B, N.SAMPLE_GUMBEL, 0.5, None, 5, 0, 1e4,
-                                             N.ptr(lg), N.ptr(ft), N.ptr(kl), N.ptr(ws), ws.numel(), N.stream()))
+                                             N.ptr(lg), N.ptr(ft), N.ptr(kl), N.ptr(pp), N.ptr(ws), ws.numel(),
+                                             N.stream()))
         g, gs = _grads(samp, dev)
         dh = torch.empty(B, E, device=dev)
         _ck(L.abcd_sampler_backward_split(cfg, par, N.ptr(h), B, N.SAMPLE_GUMBEL, 0.5, 1e4, N.ptr(d_feats),
                                               N.ptr(d_kl), N.ptr(dh), gs, N.ptr(ws), ws.numel(), N.stream(), None))
         torch.cuda.synchronize()
-        outs.append([lg, ft, kl, dh] + [g[k] for k in sorted(g)])
+        outs.append([lg, ft, kl, pp, dh] + [g[k] for k in sorted(g)])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
