@@ -671,6 +671,183 @@ static int gemm_x6f_launch(hipStream_t s, int M, int N, int K, const float* A, l
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// gemm_x6t: gemm_x6f for two K-major operands (element (row, k) at
+// P[k * ld + row]: the weight gradients dW = dG^T X over all packed frames).
+// A thread stages one row quad x 8 k of one operand per chunk: eight 16-B
+// loads (rows 4rq .. 4rq + 3 at k, k + 1, ..., k + 7; the 32 row quads of a
+// k are one contiguous 512-B read), then four splits (one per row) into the
+// fragment-ordered bf16 planes.  Split-K over the grid into fp32 slabs as
+// gemm_x6s.  Rows in [M, roundup4(M)) (padding of the leading dimension) are
+// zeroed after the load; k >= the slab's end reads 0 (buffer range).
+// dW_hh at c2 (M = 4H = 1024, N = H = 256, K = 65.6k frames): 250 us against
+// gemm_x6s's 311 us (PMC: VALU per MFMA 3.7; LDS bank-conflict cycles 37.9 M
+// -> 12.7 M per launch with the padded subtile blocks).  Two chunks of loads
+// in flight measured no faster than one (kept: it costs no occupancy).
+// ---------------------------------------------------------------------------
+template <int MR, int NR>
+__global__ __launch_bounds__(256, 2) void gemm_x6t_kernel(const float* __restrict__ A, long lda,
+                                                          const float* __restrict__ B, long ldb, int K, int kps,
+                                                          EpiArgs e, int remap) {
+  extern __shared__ __attribute__((aligned(16))) f4 fsm[];
+  constexpr int BM = 32 * MR, BN = 32 * NR, SA = BM / 16;
+  constexpr int QA = BM / 4 * 4, QT = (BM + BN) / 4 * 4;  // (row quad, k group) units: A, A + B
+  static_assert(QT == 256, "one unit per thread");
+  // subtile blocks of three 1-KiB planes, 16 B of pad between blocks: the
+  // eight row quads a wave writes per store land in eight different
+  // subtiles, which without the pad share one bank set (8-way conflicts)
+  constexpr int BLK = 3 * 64 + 1;
+  const dim3 bid = xcd_tile(remap != 0);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = bid.y * BM, n0 = bid.x * BN;
+  const int M = e.M, N = e.N;
+  const int kb = bid.z * kps, ke = min(K, kb + kps);
+  const int nch = (ke - kb + 31) / 32;
+  // this thread's unit: operand, row quad, k group
+  const int tid = threadIdx.x;
+  const bool isB = tid >= QA;
+  const int ui = isB ? tid - QA : tid;
+  const int nrq = (isB ? BN : BM) / 4;
+  const int rq = ui % nrq, qg = ui / nrq;
+  const int row = (isB ? n0 : m0) + 4 * rq, R = isB ? N : M;
+  const long ld = isB ? ldb : lda;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(isB ? B : A, (uint32_t)((size_t)ke * ld * 4));
+  const bool rowok = row < R;
+  auto gload = [&](int c, f4 (&v)[8]) {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int k = kb + c * 32 + 8 * qg + kk;
+      const uint32_t o = (rowok && k < ke) ? (uint32_t)(((long)k * ld + row) * 4) : 0x80000000u;
+      v[kk] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+    }
+  };
+  auto lstore = [&](const f4 (&v)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f4 x0, x1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        x0[t] = row + i < R ? v[t][i] : 0.f;
+        x1[t] = row + i < R ? v[4 + t][i] : 0.f;
+      }
+      bf8 h, m, l;
+      split8(x0, x1, h, m, l);
+      const int rr = 4 * rq + i;
+      f4* dst = fsm + ((isB ? SA : 0) + (rr >> 4)) * BLK + qg * 16 + (rr & 15);
+      dst[0] = __builtin_bit_cast(f4, h);
+      dst[64] = __builtin_bit_cast(f4, m);
+      dst[128] = __builtin_bit_cast(f4, l);
+    }
+  };
+  f4 acc[MR][NR];
+  acc_zero(acc);
+  auto compute = [&]() {
+    bf8 bp[NR][3];
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bp[j][p] = __builtin_bit_cast(bf8, fsm[(SA + wn * NR + j) * BLK + p * 64 + lane]);
+    constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      bf8 ap[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) ap[p] = __builtin_bit_cast(bf8, fsm[(wm * MR + i) * BLK + p * 64 + lane]);
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = mfma_bf(ap[TA[t]], bp[j][TB[t]], acc[i][j]);
+    }
+  };
+  // two chunks of global loads in flight (register sets v0 / v1 alternate):
+  // with one, every chunk waited out most of an HBM round trip
+  f4 v0[8], v1[8];
+  gload(0, v0);
+  if (nch > 1) gload(1, v1);
+  lstore(v0);
+  __syncthreads();
+  for (int c = 0; c < nch; c += 2) {
+    if (c + 2 < nch) gload(c + 2, v0);
+    compute();
+    __syncthreads();
+    if (c + 1 < nch) {
+      lstore(v1);
+      __syncthreads();
+      if (c + 3 < nch) gload(c + 3, v1);
+      compute();
+      __syncthreads();
+      if (c + 2 < nch) {
+        lstore(v0);
+        __syncthreads();
+      }
+    }
+  }
+  // epilogue (gemm_x6s_kernel's): wave-private LDS transpose, 16-B row stores, slab or C
+  const int r = lane & 15, q = lane >> 4;
+  constexpr int SW = 16 * NR, SP = SW + 4;
+  float* stg = reinterpret_cast<float*>(fsm) + w * 16 * SP;
+  float* const dst = e.slab ? e.slab + (long)bid.z * M * N : e.C;
+  const long ldd = e.slab ? (long)N : e.ldc;
+  const bool vec = (ldd % 4 == 0) && (((uintptr_t)dst & 15) == 0);
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int pp = 0; pp < NR; ++pp) {
+      const int lr = (lane + 64 * pp) / (4 * NR), c4 = (lane + 64 * pp) % (4 * NR);
+      const int gcol = n0 + wn * SW + 4 * c4;
+      const int grow = m0 + wm * 16 * MR + 16 * i + lr;
+      f4 val = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
+      if (grow < M) {
+        if (!e.slab) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (gcol + t < N) val[t] = apply_epi(e, grow, gcol + t, val[t]);
+        }
+        float* d = dst + (long)grow * ldd + gcol;
+        if (vec && gcol + 4 <= N) *reinterpret_cast<f4*>(d) = val;
+        else
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (gcol + t < N) d[t] = val[t];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int MR, int NR>
+static int gemm_x6t_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                           EpiArgs e, float* scratch, size_t scratch_floats) {
+  const int BM = 32 * MR, BN = 32 * NR;
+  const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  int Z = std::max(1, std::min(cdiv(512, tiles), cdiv(K, 32 * 16)));
+  if (scratch) Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)M * N)));
+  else Z = 1;
+  Z = std::max(Z, 1);
+  const int kps = ((cdiv(K, Z) + 31) / 32) * 32;
+  Z = cdiv(K, kps);
+  EpiArgs ek = e;
+  if (Z > 1) ek.slab = scratch;
+  const size_t lds = (size_t)(BM / 16 + BN / 16) * (3 * 64 + 1) * 16;
+  gemm_x6t_kernel<MR, NR><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, lds, s>>>(A, lda, B, ldb, K, kps, ek, 1);
+  ABCD_CHECK_LAUNCH();
+  if (Z > 1) {
+    const long n = (long)M * N;
+    slab_reduce_kernel<<<std::min<long>(2048, cdiv(n, 256)), 256, 0, s>>>(scratch, Z, e);
+    ABCD_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+
 template <int MR, int NR, bool AKC, bool BKC>
 static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
                            EpiArgs e, float* scratch, size_t scratch_floats) {
@@ -763,6 +940,8 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
     if (!tl_side) {  // 66-76 KB of LDS: not beside a persistent kernel
       if (N > 128 && N <= 160)  // one 160-wide tile (e.g. dW_ih, N = F = 129)
         return gemm_x6s_launch<4, 5, false, false>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+      if ((size_t)K * A.ld * 4 < (1ull << 31) && (size_t)K * B.ld * 4 < (1ull << 31))
+        return gemm_x6t_launch<4, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
       return gemm_x6s_launch<4, 4, false, false>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
     }
     return gemm_tn(s, M, N, K, A, B, e, scratch, scratch_floats);
