@@ -693,6 +693,8 @@ __global__ __launch_bounds__(256, 2) void gemm_x6t_kernel(const float* __restric
   constexpr int BM = 32 * MR, BN = 32 * NR, SA = BM / 16;
   constexpr int QA = BM / 4 * 4, QT = (BM + BN) / 4 * 4;  // (row quad, k group) units: A, A + B
   static_assert(QT == 256, "one unit per thread");
+  // the operand's buffer resource lives in SGPRs: each wave must stage one operand only
+  static_assert(QA % 64 == 0, "A / B split on a wave boundary");
   // subtile blocks of three 1-KiB planes, 16 B of pad between blocks: the
   // eight row quads a wave writes per store land in eight different
   // subtiles, which without the pad share one bank set (8-way conflicts)
