@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
       const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u),
                     (uint32_t)H * 4u};
       if (X6) {
-        wave_mma_x6<G, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q);
+        wave_mma_x6<G, (X6 > 0 ? X6 : 1), 4>(acc[0], A, row0 + r, smem, X6, lane, q);
       } else {
         wave_mma_lds<G, PD>(acc, A, row0 + r, smem, nch, lane, q);
       }
@@ -1052,9 +1052,9 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         acc[0] = acch[0];
         acc[1] = acch[1];
         if constexpr (NXC > 0)
-          wave_mma_x6<2, (NXC > 0 ? NXC : 1), 8>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC);
+          wave_mma_x6<2, (NXC > 0 ? NXC : 1), 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC);
       } else {
-        wave_mma_x6<2, NCC, 8>(acc, A, row0 + r, BC, NCC, lane, q, mem % NCC);
+        wave_mma_x6<2, NCC, 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NCC);
       }
     }
     PSTAMP(7);
@@ -1121,12 +1121,12 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
-          wave_mma_x6p<3, NH32, 8>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
+          wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
           a1[0] = a3[0];
           acch[0] = a3[1];
           acch[1] = a3[2];
         } else {
-          wave_mma_x6<1, NH32, 8>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32);
+          wave_mma_x6<1, NH32, 4>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32);
         }
       }
       PSTAMP(6);
@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       if (erow0 < bs) {
         const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
                        (uint32_t)2 * Hm * 4u};
-        wave_mma_x6<1, NM32, 8>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
+        wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
                                 mem % NM32);
       }
 #pragma unroll
@@ -1580,7 +1580,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     f4 acc[1] = {f4zero()};
     if (row0 < bs) {
       const BufKC Az{make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u), (uint32_t)2 * Hm * 4u};
-      wave_mma_x6<1, NZ, 8>(acc, Az, row0 + r, B2, NZ, lane, q, mem % NZ);
+      wave_mma_x6<1, NZ, 4>(acc, Az, row0 + r, B2, NZ, lane, q, mem % NZ);
     }
     PSTAMP(7);
     float dgh[4][4];

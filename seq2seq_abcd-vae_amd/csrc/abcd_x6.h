@@ -126,7 +126,10 @@ DEV void stage_x6(f4* dst, const float* W, long ldw, int kvalid, int nsub, int n
 // trip count made the compiler rotate the ring with moves that waited for
 // every load).  A supplies frag8(row, c, q, lo, hi) (k = 32c + 8q + 0..7 as
 // two float4).  PD chunks of raw fp32 stay in flight; each is split in
-// registers right before its chunk's 6 x NR MFMAs.  Bl: the chunk-major x6
+// registers right before its chunk's 6 x NR MFMAs (the persistent kernels
+// use PD = 4: same-box A/B at c2 against PD = 8, enc_fwd 1.35 -> 1.23 ms,
+// dec_fwd 2.51 -> 2.36 ms, dec_bwd 4.22 -> 4.17 ms; PD = 2 no better).
+// Bl: the chunk-major x6
 // image with `nch` chunks per subtile (nch >= NCH; a segment of a wider image
 // starts at Bl + c0 * 3 * 64).
 template <int NR, int NCH, int PD, class OA>
