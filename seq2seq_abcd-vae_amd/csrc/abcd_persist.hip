@@ -1401,6 +1401,20 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
 constexpr int DSK_PITCH = 36;  // floats per row of the wave-private dG transpose
 constexpr int DSK_WAVE_FLOATS = 2 * TP_FLOATS;  // per-wave LDS region: the dG transpose or two tp_quad tiles
 static_assert(16 * DSK_PITCH <= DSK_WAVE_FLOATS, "dG transpose fits the wave's region");
+// Operands a phase needs only after its hand-off wait are loaded before it,
+// branch-free (buffer loads: rows past the resource's extent read 0), and
+// pinned after it: the poll's `s_waitcnt vmcnt(0)` then covers them in ONE
+// round trip.  Conditional loads let the compiler hoist their consumers
+// (tanh of the cell state) into the load branches, each with its own
+// vmcnt(0) -- four serialized round trips in front of the P2 poll.
+DEV float bld(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+}
+template <int N>
+DEV void pin(float (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
+}
 // acc += sum of NP partial f4s at base + p * 1 KiB, NB loads in flight
 template <int NP, int NB = NP>
 DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc, int rot = 0) {
@@ -1487,18 +1501,31 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     // emission operands of the tile: independent of the hand-off, loaded before the wait
     const int col0 = 16 * mem + r;
     float emu[4], elv[4], eox[4], ey[4], emk[4];
+    if (mem < nFt) {
+      const uint32_t ef = (uint32_t)bs * Fp * 4u;
+      const __amdgpu_buffer_rsrc_t rmu = make_rsrc(a.MU + (size_t)o * Fp, ef), rlv = make_rsrc(a.LV + (size_t)o * Fp, ef),
+                                   rox = make_rsrc(a.OUT + (size_t)o * Fp, ef),
+                                   ryy = make_rsrc(a.Y + (size_t)o * F, (uint32_t)bs * F * 4u);
+      // rows >= succ_valid have no dx (zero partials), so their mask value is irrelevant
+      const __amdgpu_buffer_rsrc_t rmk =
+          make_rsrc(a.xmask ? a.xmask + (size_t)(o + bs) * F : a.Y, a.xmask ? (uint32_t)succ_valid * F * 4u : 0u);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-      const bool live = mem < nFt && b < bs && col0 < F;
-      const long rr = o + (live ? b : 0);
-      emu[g] = live ? a.MU[rr * Fp + col0] : 0.f;
-      elv[g] = live ? a.LV[rr * Fp + col0] : 0.f;
-      eox[g] = live ? a.OUT[rr * Fp + col0] : 0.f;
-      ey[g] = live ? a.Y[rr * F + col0] : 0.f;
-      emk[g] = (a.xmask && live && b < succ_valid) ? a.xmask[(long)(o + bs + b) * F + col0] : 1.f;
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
+        const uint32_t of = col0 < F ? (b * Fp + col0) * 4u : 0x80000000u;
+        const uint32_t oy = col0 < F ? (b * F + col0) * 4u : 0x80000000u;
+        emu[g] = bld(rmu, of);
+        elv[g] = bld(rlv, of);
+        eox[g] = bld(rox, of);
+        ey[g] = bld(ryy, oy);
+        emk[g] = a.xmask ? bld(rmk, oy) : 1.f;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) emu[g] = elv[g] = eox[g] = ey[g] = 0.f, emk[g] = 1.f;
     }
     if (i > 0) gs.wait(3u * i);
+    pin(emu), pin(elv), pin(eox), pin(ey), pin(emk);
     PSTAMP(0);
     if (mem < nFt) {
       f4 dx = f4zero();
@@ -1526,12 +1553,13 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     PSTAMP(6);
     // ---------------- P1: dZ tile ----------------
     float zpre[4];
+    {
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-      zpre[g] = b < bs ? a.Aact[(long)(o + b) * 2 * Hm + 16 * mem + r] : 0.f;
+      for (int g = 0; g < 4; ++g) zpre[g] = bld(rz, ((uint32_t)(row0 + 4 * q + g) * 2 * Hm + 16 * mem + r) * 4u);
     }
     gs.wait(3u * i + 1);
+    pin(zpre);
     PSTAMP(2);
     {
       f4 acc[2][1];
@@ -1556,26 +1584,33 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
     // loaded across the P1 -> P2 hand-off.  The producers stored them after
     // their P2 publish of step t+1; their P0 publish of this step drained them
     // (vmcnt(0)), and the P1 wait above saw every member's P0 publish.
+    // ---------------- P2: dh -> cell backward -> dG_t -> partials ----------------
+    // cell operands first, then the dh_rec partials: summing those waits for
+    // both in one round trip, before the poll
+    float pg[4][4], pc[4], pcp[4], pdho[4];
+    {
+      const uint32_t eh = (uint32_t)bs * H * 4u;
+      const __amdgpu_buffer_rsrc_t rgs = make_rsrc(a.Gst + (size_t)o * 4 * H, eh * 4u),
+                                   rcs = make_rsrc(a.Cst + (size_t)o * H, GRU ? 0u : eh),
+                                   rcp = make_rsrc((GRU ? a.Hprev : a.Cprev) + (size_t)o * H, eh),
+                                   rdo = make_rsrc(a.DHO + (size_t)o * H, eh);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pg[g][j] = bld(rgs, (b * 4 * H + j * H + unit) * 4u);
+        pc[g] = GRU ? 0.f : bld(rcs, (b * H + unit) * 4u);
+        pcp[g] = bld(rcp, (b * H + unit) * 4u);
+        pdho[g] = bld(rdo, (b * H + unit) * 4u);
+      }
+    }
     f4 dhr = f4zero();
     if (has_part) {
       const int pl = q * 16 + (mem & 1) * 8 + (r & 7);
       sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr, mem % M);
     }
-    // ---------------- P2: dh -> cell backward -> dG_t -> partials ----------------
-    float pg[4][4], pc[4], pcp[4], pdho[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-      const bool live = b < bs;
-      const long rr = o + (live ? b : 0);
-      const float* Gr = a.Gst + rr * 4 * H;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pg[g][j] = live ? Gr[j * H + unit] : 0.f;
-      pc[g] = (live && !GRU) ? a.Cst[rr * H + unit] : 0.f;
-      pcp[g] = live ? (GRU ? a.Hprev : a.Cprev)[rr * H + unit] : 0.f;
-      pdho[g] = live ? a.DHO[rr * H + unit] : 0.f;
-    }
     gs.wait(3u * i + 2);
+    pin(pg[0]), pin(pg[1]), pin(pg[2]), pin(pg[3]), pin(pc), pin(pcp), pin(pdho);
     PSTAMP(4);
     f4 acc[1] = {f4zero()};
     if (row0 < bs) {
