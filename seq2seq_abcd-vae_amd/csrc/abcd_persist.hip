@@ -117,6 +117,20 @@ DEV void st4(__amdgpu_buffer_rsrc_t rs, uint32_t off, f4 v, bool wt) {
   else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, off, 0, 0);
 }
 
+// Operands a phase needs only after its hand-off wait are loaded before it,
+// branch-free (buffer loads: rows past the resource's extent read 0), and
+// pinned after it: the poll's `s_waitcnt vmcnt(0)` then covers them in ONE
+// round trip.  Conditional loads let the compiler hoist their consumers
+// (tanh of the cell state) into the load branches, each with its own
+// vmcnt(0) -- four serialized round trips in front of the P2 poll.
+DEV float bld(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+}
+template <int N>
+DEV void pin(float (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
+}
 // lane 0 of the workgroup polls until *cnt >= target (bounded), then the
 // barrier releases every wave
 DEV void group_wait(unsigned* cnt, unsigned target) {
@@ -273,15 +287,16 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
     // input projection of this step (independent of the recurrence: loaded
     // before the wait so its latency hides behind it)
     float gxp[4][G];
+    {
+      const __amdgpu_buffer_rsrc_t rgx = make_rsrc(D.GX + (size_t)o * D.ldgx, (uint32_t)bs * D.ldgx * 4u);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-      const bool live = b < bs;
-      const long rr = o + (live ? b : 0);
+      for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int j = 0; j < G; ++j) gxp[g][j] = live ? D.GX[rr * D.ldgx + j * H + unit] : 0.f;
+        for (int j = 0; j < G; ++j) gxp[g][j] = bld(rgx, ((uint32_t)(row0 + 4 * q + g) * D.ldgx + j * H + unit) * 4u);
     }
     if (i > 0) group_wait(cnt, (unsigned)(nut * i));
+#pragma unroll
+    for (int g = 0; g < 4; ++g) pin(gxp[g]);
     PSTAMP(1);
     f4 acc[2][G];
     acc2_zero(acc);
@@ -548,34 +563,37 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
       prev_valid = t == T - 1 ? 0 : off[t + 2] - off[t + 1];
     }
     PSTAMP(0);
-    float pg[4][4], pc[4], pcp[4], pdh[4], pdc[4];
+    // cell operands: branch-free loads before the wait, pinned after it (bld)
+    float pg[4][4], pc[4], pcp[4], pdh[4], pdl[4], pdc[4];
+    {
+      const uint32_t eh = (uint32_t)bs * H * 4u;
+      const __amdgpu_buffer_rsrc_t rgs = make_rsrc(D.Gst + (size_t)o * 4 * H, eh * 4u),
+                                   rcs = make_rsrc(D.Cst + (size_t)o * H, G == 4 ? eh : 0u),
+                                   rcp = make_rsrc((G == 4 ? D.Cprev : D.Hprev) + (size_t)o * H,
+                                                   (uint32_t)prev_valid * H * 4u),
+                                   rdx = make_rsrc(D.DHX ? D.DHX + (size_t)o * D.lddhx : D.Gst,
+                                                   D.DHX ? (uint32_t)bs * D.lddhx * 4u : 0u),
+                                   rdl = make_rsrc(D.dlast ? D.dlast : D.Gst, D.dlast ? (uint32_t)bs * D.ldl * 4u : 0u);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-      const bool live = b < bs;
-      const long rr = o + (live ? b : 0);
-      const bool fin = b >= succ_valid;
-      const bool haspred = live && b < prev_valid;
-      const float* Gr = D.Gst + rr * 4 * H;
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
+        const bool fin = (int)b >= succ_valid;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pg[g][j] = live ? Gr[j * H + unit] : 0.f;
-      pc[g] = (live && G == 4) ? D.Cst[rr * H + unit] : 0.f;
-      pcp[g] = 0.f;
-      if (haspred) pcp[g] = G == 4 ? D.Cprev[rr * H + unit] : D.Hprev[rr * H + unit];
-      float dh = 0.f, dc = 0.f;
-      if (live) {
-        if (D.DHX) dh += D.DHX[rr * D.lddhx + unit];
-        if (fin && D.dlast) {
-          dh += D.dlast[(long)b * D.ldl + D.hcol + unit];
-          if (G == 4 && D.ccol >= 0) dc = D.dlast[(long)b * D.ldl + D.ccol + unit];
-        }
+        for (int j = 0; j < 4; ++j) pg[g][j] = bld(rgs, (b * 4 * H + j * H + unit) * 4u);
+        pc[g] = G == 4 ? bld(rcs, (b * H + unit) * 4u) : 0.f;
+        pcp[g] = bld(rcp, (b * H + unit) * 4u);
+        pdh[g] = bld(rdx, (b * D.lddhx + unit) * 4u);
+        // the last step's gradient enters rows that have no successor (rows >= bs read 0)
+        pdl[g] = bld(rdl, fin ? (b * D.ldl + D.hcol + unit) * 4u : 0x80000000u);
+        pdc[g] = (G == 4 && D.ccol >= 0) ? bld(rdl, fin ? (b * D.ldl + D.ccol + unit) * 4u : 0x80000000u) : 0.f;
       }
-      pdh[g] = dh;
-      pdc[g] = dc;
     }
     f4 dhr = f4zero();
+    if (i > 0) group_wait(cnt, (unsigned)(nut * i));
+    pin(pg[0]), pin(pg[1]), pin(pg[2]), pin(pg[3]), pin(pc), pin(pcp), pin(pdh), pin(pdl), pin(pdc);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) pdh[g] += pdl[g];
     if (i > 0) {
-      group_wait(cnt, (unsigned)(nut * i));
       if (row0 < succ_valid) {
         const __amdgpu_buffer_rsrc_t pr = make_rsrc(a.part + (size_t)(i & 1) * slot_f, (uint32_t)(slot_f * 4));
         const uint32_t base = (uint32_t)((((size_t)grp * nut + mem) * 4 + w) * nut * 256 + lane * 4) * 4u;
@@ -1401,20 +1419,6 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
 constexpr int DSK_PITCH = 36;  // floats per row of the wave-private dG transpose
 constexpr int DSK_WAVE_FLOATS = 2 * TP_FLOATS;  // per-wave LDS region: the dG transpose or two tp_quad tiles
 static_assert(16 * DSK_PITCH <= DSK_WAVE_FLOATS, "dG transpose fits the wave's region");
-// Operands a phase needs only after its hand-off wait are loaded before it,
-// branch-free (buffer loads: rows past the resource's extent read 0), and
-// pinned after it: the poll's `s_waitcnt vmcnt(0)` then covers them in ONE
-// round trip.  Conditional loads let the compiler hoist their consumers
-// (tanh of the cell state) into the load branches, each with its own
-// vmcnt(0) -- four serialized round trips in front of the P2 poll.
-DEV float bld(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-}
-template <int N>
-DEV void pin(float (&v)[N]) {
-#pragma unroll
-  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
-}
 // acc += sum of NP partial f4s at base + p * 1 KiB, NB loads in flight
 template <int NP, int NB = NP>
 DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc, int rot = 0) {
