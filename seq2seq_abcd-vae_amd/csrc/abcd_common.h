@@ -18,6 +18,7 @@
 // k assignment is used for A and B, so every k is summed exactly once.
 // Accumulator subtile (16x16): lane holds rows 4*q + {0..3}, column r.
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -250,13 +251,25 @@ DEV void stage_b_frag(f4* dst, const float* W, long ldw, int nsub, int nch, RowF
 // guards the MFMAs of a final partial block (uniform branches, which cost a
 // full drain there), so A must be readable up to chunk roundup(nch, PD)
 // (BufKC: range-checked).
-template <int NR, int PD, bool TAIL = false, class OA>
-DEV void wave_mma_lds(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q) {
+// `pre` (optional) runs between the A ring's first loads and the first
+// MFMA: work whose memory operations must not delay those loads (its stores
+// are issued after them, so the ring's vmcnt waits do not cover them).
+struct NoPre {
+  DEV void operator()() const {}
+};
+template <int NR, int PD, bool TAIL = false, class OA, class Pre = NoPre>
+DEV void wave_mma_lds(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q,
+                      Pre pre = Pre()) {
   f4 a[PD], b[NR];
 #pragma unroll
   for (int p = 0; p < PD; ++p) a[p] = A.frag(arow, p, q);
 #pragma unroll
   for (int j = 0; j < NR; ++j) b[j] = Bl[j * nch * 64 + lane];
+  if constexpr (!std::is_same_v<Pre, NoPre>) {
+    __builtin_amdgcn_sched_barrier(0);
+    pre();
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // one chunk: LDS reads of the NEXT chunk's B fragments are issued before
   // this chunk's MFMAs (their latency hides behind them); the A slot is
   // refilled PD chunks ahead when `refill`

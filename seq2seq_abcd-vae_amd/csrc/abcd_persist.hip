@@ -737,10 +737,10 @@ DEV void stage_rows_seg(f4* dst, const float* W, long ldw, int nsub, int nseg, i
 }
 
 // ring of 16 chunks; exact (drain-free) when nch is a multiple of 16
-template <int NR, class OA>
-DEV void mma16(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q) {
-  if (nch % 16 == 0) wave_mma_lds<NR, 16, false>(acc, A, arow, Bl, nch, lane, q);
-  else wave_mma_lds<NR, 16, true>(acc, A, arow, Bl, nch, lane, q);
+template <int NR, class OA, class Pre = NoPre>
+DEV void mma16(f4 (&acc)[2][NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q, Pre pre = Pre()) {
+  if (nch % 16 == 0) wave_mma_lds<NR, 16, false>(acc, A, arow, Bl, nch, lane, q, pre);
+  else wave_mma_lds<NR, 16, true>(acc, A, arow, Bl, nch, lane, q, pre);
 }
 
 // ---------------------------------------------------------------------------
@@ -1493,7 +1493,26 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
   const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
   // this wave's block of subtile s: (((grp*NS + s)*4 + w)*M + producer)*256 floats
   auto blk = [&](int s) { return (uint32_t)((((size_t)grp * NS + s) * 4 + w) * M) * 1024u; };
+  // this member's partial of output subtile s from the split dG tile (a0, a1, a2)
+  auto partial_st = [&](int s, const bf8& a0, const bf8& a1, const bf8& a2, __amdgpu_buffer_rsrc_t pw) {
+    const f4* bp = SK + (s * 3) * 64 + lane;
+    const f4 v = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                        __builtin_bit_cast(bf8, bp[128]));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
+                                           blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+  };
   float carry[4] = {0.f, 0.f, 0.f, 0.f};
+  // members < ND (the P0 members) defer their dh_rec partial stores from the
+  // end of P2 to the next step's P1 (issued behind the dMU / dLV loads and
+  // drained by the P1 publish): otherwise their next P0 poll -- on the
+  // critical path -- waits for 16 KiB per wave of write-through stores to
+  // drain (in-order vmcnt).  Consumers read those ND producers' partials
+  // after the P2 wait, the others' before it.
+  constexpr int ND = NXS;
+  const bool defer = mem < ND;
+  bool dmk = false;
+  bf8 da0{}, da1{}, da2{};
+  __amdgpu_buffer_rsrc_t dpw = pr0;
   const int* off = a.off;
   for (int i = 0; i < T; ++i) {
     const int t = T - 1 - i;
@@ -1570,7 +1589,14 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       acc2_zero(acc);
       if (row0 < bs) {
         const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
-        mma16<1>(acc, A, row0 + r, B1, nchx, lane, q);
+        if (ND > 0 && defer && dmk) {
+          mma16<1>(acc, A, row0 + r, B1, nchx, lane, q, [&] {
+#pragma unroll
+            for (int s = NXS; s < NS; ++s) partial_st(s, da0, da1, da2, dpw);
+          });
+        } else {
+          mma16<1>(acc, A, row0 + r, B1, nchx, lane, q);
+        }
       }
       acc2_fold(acc);
       float dz[4];
@@ -1609,17 +1635,24 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       }
     }
     f4 dhr = f4zero();
-    if (has_part) {
-      const int pl = q * 16 + (mem & 1) * 8 + (r & 7);
-      sum_partials<M>(prd, blk(NXS + (mem >> 1)) + (uint32_t)pl * 16u, dhr, mem % M);
-    }
+    const uint32_t dhb = blk(NXS + (mem >> 1)) + (uint32_t)(q * 16 + (mem & 1) * 8 + (r & 7)) * 16u;
+    if (has_part) sum_partials<M - ND>(prd, dhb + (uint32_t)ND * 1024u, dhr, mem % (M - ND));
     gs.wait(3u * i + 2);
     pin(pg[0]), pin(pg[1]), pin(pg[2]), pin(pg[3]), pin(pc), pin(pcp), pin(pdho);
     PSTAMP(4);
+    f4 dhd[ND > 0 ? ND : 1];
+#pragma unroll
+    for (int p = 0; p < ND; ++p)
+      dhd[p] = has_part ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(prd, dhb + (uint32_t)p * 1024u, 0, 16))
+                        : f4zero();
     f4 acc[1] = {f4zero()};
     if (row0 < bs) {
       const BufKC Az{make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u), (uint32_t)2 * Hm * 4u};
       wave_mma_x6<1, NZ, 4>(acc, Az, row0 + r, B2, NZ, lane, q, mem % NZ);
+    }
+    if (ND > 0) {  // the deferred producers' partials (issued with the dZ ring's first loads)
+#pragma unroll
+      for (int p = 0; p < ND; ++p) dhr += dhd[p];
     }
     PSTAMP(7);
     float dgh[4][4];
@@ -1676,22 +1709,21 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
       split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
     }
     const __amdgpu_buffer_rsrc_t pw = (i & 1) ? pr1 : pr0;
-    auto partial = [&](int s) {
-      const f4* bp = SK + (s * 3) * 64 + lane;
-      const f4 v = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
-                          __builtin_bit_cast(bf8, bp[128]));
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
-                                             blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
-    };
+    auto partial = [&](int s) { partial_st(s, a0, a1, a2, pw); };
     if (mk) {
 #pragma unroll
       for (int s = 0; s < NXS; ++s) partial(s);
     }
     gs.publish();
     PSTAMP(5);
-    if (mk) {
+    if (mk && !defer) {
 #pragma unroll
       for (int s = NXS; s < NS; ++s) partial(s);
+    }
+    if (defer) {
+      dmk = mk;
+      da0 = a0, da1 = a1, da2 = a2;
+      dpw = pw;
     }
     // stash for the weight-gradient GEMMs (plain 16-B stores, after the
     // publish), straight from the dG tile in LDS: 16 rows x 4 gates x 2 quads
