@@ -672,6 +672,194 @@ static int gemm_x6f_launch(hipStream_t s, int M, int N, int K, const float* A, l
 }
 
 // ---------------------------------------------------------------------------
+// gemm_x6r: frame-streaming split-fp32 GEMM for short K (K <= 32 NC) and
+// K-contiguous operands: C[M x N] = A B^T with M = packed frames (~65k) and
+// N = a few hundred to 2048 weight rows.  gemm_x6f re-stages and re-splits
+// the B tile for every 128 x 128 output tile and pays a load -> split ->
+// barrier round per 32-deep chunk -- at K = 144 a workgroup does 5 such
+// rounds and its epilogue, so the launch ran at ~80 TF/s.  Here a workgroup
+// owns one BN-column slice of B for the whole launch (split ONCE into the
+// three bf16 planes in fragment order, resident in LDS) and streams a
+// contiguous range of frames: each wave takes 16 MR rows at a time, loads
+// the A fragments straight into registers (the next block's loads in
+// flight during this block's MFMAs), splits each chunk once and issues
+// 6 MR NR MFMAs per chunk.  Epilogue: wave-private LDS transpose, whole
+// 16-B row stores.  Workgroups of one XCD (blockIdx % 8) take the slices of
+// the same frame ranges, so A rows are fetched from HBM once per XCD L2.
+// Measured (scripts/gemm_bench.py, MI355X): input projection 64044 x 2048 x
+// 144 302 us against gemm_x6f's 450 us (273 vs 458 us inside the c2 step),
+// offset head 64044 x 256 x 256 71 vs 82 us.  Where the rest goes (same
+// script, stores or MFMAs removed): 320 us -> 237 without the stores, 198
+// without the MFMAs, 136 without either -- one wave per SIMD serialises the
+// B-plane LDS reads, the splits, the epilogue transposes and the MFMAs.
+// Tried and slower: a three-slot register ring (blocks two ahead, 391 us),
+// MR = 4 (scratch), BN = 64 at two workgroups per CU (294-311 us, more A
+// re-reads), MR = 1 (306-339 us).
+// ---------------------------------------------------------------------------
+template <int NC, int BN, int MR, int OCC>
+__global__ __launch_bounds__(256, OCC) void gemm_x6r_kernel(const float* __restrict__ A, long lda,
+                                                       const float* __restrict__ B, long ldb, int K, EpiArgs e,
+                                                       int nslices, int rows_per) {
+  extern __shared__ __attribute__((aligned(16))) f4 rsm[];
+  constexpr int NR = BN / 16, SP = BN + 4;
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3;  // grid = 8 * per
+  const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int slice = lin % nslices, part = lin / nslices;
+  const int n0 = slice * BN, M = e.M, N = e.N;
+  // B slice -> LDS planes [j][c][plane][lane]; rows >= N and k >= K read 0 (K % 8 == 0)
+  {
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (size_t)n0 * ldb, (uint32_t)(std::max(0, std::min(BN, N - n0)) * ldb * 4));
+    for (int x = threadIdx.x; x < NR * NC * 64; x += 256) {
+      const int j = x / (NC * 64), c = (x / 64) % NC, ln = x & 63;
+      const int row = 16 * j + (ln & 15), kk = 32 * c + 8 * (ln >> 4);
+      const uint32_t o = kk < K ? (uint32_t)(row * ldb + kk) * 4u : 0x80000000u;
+      const f4 lo = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, o, 0, 0));
+      const f4 hi = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, kk < K ? o + 16u : o, 0, 0));
+      bf8 h, m, l;
+      split8(lo, hi, h, m, l);
+      f4* d = rsm + ((j * NC + c) * 3) * 64 + ln;
+      d[0] = __builtin_bit_cast(f4, h);
+      d[64] = __builtin_bit_cast(f4, m);
+      d[128] = __builtin_bit_cast(f4, l);
+    }
+  }
+  float* stg = reinterpret_cast<float*>(rsm + NR * NC * 3 * 64) + w * 16 * SP;
+  __syncthreads();
+  const int r0 = part * rows_per, r1 = std::min(M, r0 + rows_per);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A, (uint32_t)((size_t)M * lda * 4));
+  // the lane's A fragments of the block at row b: rows b + 16 i + r, k = 32 c + 8 q + 0..7
+  auto aload = [&](int b, f4 (&v)[MR][NC][2]) {
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int kk = 32 * c + 8 * q;
+        const uint32_t o = kk < K ? (uint32_t)((b + 16 * i + r) * lda + kk) * 4u : 0x80000000u;
+        v[i][c][0] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, o, 0, 0));
+        v[i][c][1] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, kk < K ? o + 16u : o, 0, 0));
+      }
+  };
+  constexpr int RB = 16 * MR;
+  // epilogue columns of this lane: the same 4 for every row it stores (bias preloaded)
+  const int ec = n0 + 4 * (lane % (BN / 4));
+  f4 bq = f4zero();
+  if (e.bias) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bq[t] = ec + t < N ? e.bias[ec + t] : 0.f;
+  }
+  f4 va[MR][NC][2];
+  int b = r0 + w * RB;
+  if (b < r1) aload(b, va);
+  for (; b < r1; b += 4 * RB) {
+    // next block's fragments: issued here, unconditionally (rows past M read
+    // 0; a last block's look-ahead into the next range is a wasted read), and
+    // pinned -- the compiler otherwise sinks them to the copy at the end of
+    // the block, exposing the whole load latency once per block
+    f4 vn[MR][NC][2];
+    const bool more = b + 4 * RB < r1;
+    aload(b + 4 * RB, vn);
+    __builtin_amdgcn_sched_barrier(0);
+    f4 acc[MR][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) acc[i][j] = f4zero();
+    // B planes of step (c, j) read one step ahead (their LDS latency hides
+    // behind the previous step's 6 MR MFMAs)
+    auto bread = [&](int c, int j, f4 (&bb)[3]) {
+      const f4* bp = rsm + ((j * NC + c) * 3) * 64 + lane;
+      bb[0] = bp[0], bb[1] = bp[64], bb[2] = bp[128];
+    };
+    f4 bcur[3];
+    bread(0, 0, bcur);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      bf8 as[MR][3];
+#pragma unroll
+      for (int i = 0; i < MR; ++i) split8(va[i][c][0], va[i][c][1], as[i][0], as[i][1], as[i][2]);
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        f4 bnxt[3];
+        const bool nx = j + 1 < NR || c + 1 < NC;
+        if (nx) bread(j + 1 < NR ? c : c + 1, j + 1 < NR ? j + 1 : 0, bnxt);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+          acc[i][j] = mma_x6(acc[i][j], as[i][0], as[i][1], as[i][2], __builtin_bit_cast(bf8, bcur[0]),
+                             __builtin_bit_cast(bf8, bcur[1]), __builtin_bit_cast(bf8, bcur[2]));
+        __builtin_amdgcn_sched_barrier(0);
+        if (nx) bcur[0] = bnxt[0], bcur[1] = bnxt[1], bcur[2] = bnxt[2];
+      }
+    }
+    // epilogue: 16 rows x BN per subtile row i through the wave's LDS tile
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int pp = 0; pp < NR; ++pp) {  // 16 rows x BN / 4 quads = 64 NR quads per wave
+        const int lr = (lane + 64 * pp) / (BN / 4), col = ec;
+        const int row = b + 16 * i + lr;
+        f4 val = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * (lane % (BN / 4)));
+        if (row < r1 && col < N) {
+          float* d = e.C + (long)row * e.ldc + col;
+          val = val * e.alpha + bq;
+          if (e.beta != 0.f) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              if (col + t < N) val[t] += e.beta * d[t];
+          }
+          if (e.act == ACT_TANH) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) val[t] = tanhf(val[t]);
+          }
+          if (col + 4 <= N) *reinterpret_cast<f4*>(d) = val;
+          else
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              if (col + t < N) d[t] = val[t];
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) va[i][c][0] = vn[i][c][0], va[i][c][1] = vn[i][c][1];
+    }
+  }
+}
+
+template <int NC, int BN, int MR, int OCC = 1>
+static int gemm_x6r_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                           EpiArgs e) {
+  const int nslices = cdiv(N, BN);
+  // OCC workgroups per CU: 256 OCC / nslices frame ranges (grid a multiple of 8)
+  const int nparts = std::max(1, 256 * OCC / nslices);
+  int grid = nslices * nparts;
+  grid = (grid + 7) / 8 * 8;
+  const int nparts_eff = cdiv(grid, nslices);
+  const int rows_per = ((cdiv(M, nparts_eff) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
+  const size_t lds = (size_t)(BN / 16) * NC * 3 * 64 * 16 + (size_t)4 * 16 * (BN + 4) * 4;
+  static bool attr = false;  // per process (the attribute is per function, not per device)
+  if (!attr) {
+    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_x6r_kernel<NC, BN, MR, OCC>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  gemm_x6r_kernel<NC, BN, MR, OCC><<<grid, 256, lds, s>>>(A, lda, B, ldb, K, e, nslices, rows_per);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // gemm_x6t: gemm_x6f for two K-major operands (element (row, k) at
 // P[k * ld + row]: the weight gradients dW = dG^T X over all packed frames).
 // A thread stages one row quad x 8 k of one operand per chunk: eight 16-B
@@ -918,8 +1106,12 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
         ((uintptr_t)A.p % 16) == 0 && ((uintptr_t)B.p % 16) == 0) {
       if (!tl_side) {
         // fragment-staged form (one split per workgroup) when both operands fit a buffer resource
-        if (K % 8 == 0 && (size_t)M * A.ld * 4 < (1ull << 31) && (size_t)N * B.ld * 4 < (1ull << 31))
+        if (K % 8 == 0 && (size_t)M * A.ld * 4 < (1ull << 31) && (size_t)N * B.ld * 4 < (1ull << 31)) {
+          // short K: B slice resident, frames streamed (gemm_x6r)
+          if (K <= 160) return gemm_x6r_launch<5, 128, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
+          if (K <= 256) return gemm_x6r_launch<8, 64, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
           return gemm_x6f_launch<4, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
+        }
         return gemm_x6s_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
       }
       if (N >= 256) return gemm_tn_launch<4, 8, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);

@@ -7,11 +7,13 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("M,N,K", [(16, 16, 16), (33, 70, 48), (512, 1024, 256), (65, 2048, 144), (7, 5, 3),
-                                   (1000, 129, 385), (300, 512, 1024), (8001, 520, 144), (7000, 256, 256)])
+                                   (1000, 129, 385), (300, 512, 1024), (8001, 520, 144), (7000, 256, 256),
+                                   (9000, 300, 136), (64044, 2048, 144)])
 def test_gemm_nt_vs_torch(M, N, K):
-    """C = A B^T + bias; the last two shapes take the frame-parallel LDS route
-    (>= 240 128-wide tiles: split-fp32 gemm_x6s with K-contiguous operands,
-    ragged M / N / K)."""
+    """C = A B^T + bias; the shapes from (8001, 520, 144) on take the
+    frame-parallel route (>= 240 128-wide tiles): K <= 256 the frame-streaming
+    split-fp32 gemm_x6r (ragged M / N, a partial last K chunk, the c2 input
+    projection), else the fragment-staged gemm_x6f."""
     from modules import _native as Nn
     g = torch.Generator(device="cuda").manual_seed(M * 1000 + N + K)
     A = torch.randn(M, K, device="cuda", generator=g)
