@@ -133,8 +133,8 @@ DEV void pin(float (&v)[N]) {
 }
 // lane 0 of the workgroup polls until *cnt >= target (bounded), then the
 // barrier releases every wave
-DEV void group_wait(unsigned* cnt, unsigned target) {
-  if (threadIdx.x == 0) {
+DEV void group_wait(unsigned* cnt, unsigned target, int pw = 0) {
+  if (threadIdx.x == 64 * pw) {
     unsigned spins = 0;
     const unsigned lim = g_spin_limit;
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -168,9 +168,10 @@ DEV void flags_publish(unsigned* fl, int mem, unsigned epoch) {
   if (threadIdx.x == 0)
     __hip_atomic_store(fl + mem * PERSIST_SYNC_STRIDE, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-DEV void flags_wait(const unsigned* fl, int M, unsigned epoch) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
+// pw: the polling wave (one whose pre-wait work is done soonest)
+DEV void flags_wait(const unsigned* fl, int M, unsigned epoch, int pw = 0) {
+  if ((threadIdx.x >> 6) == pw) {
+    const int lane = threadIdx.x & 63;
     unsigned spins = 0;
     const unsigned lim = g_spin_limit;
     for (;;) {
@@ -193,9 +194,9 @@ struct GSync {
   unsigned *cnt, *fl;
   int M, mem, use_flags;
   unsigned ep;  // publishes so far by this member
-  DEV void wait(unsigned publishes) {
-    if (use_flags) flags_wait(fl, M, publishes);
-    else group_wait(cnt, (unsigned)M * publishes);
+  DEV void wait(unsigned publishes, int pw = 0) {
+    if (use_flags) flags_wait(fl, M, publishes, pw);
+    else group_wait(cnt, (unsigned)M * publishes, pw);
   }
   DEV void publish() {
     ++ep;
@@ -1170,7 +1171,9 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         }
       }
     }
-    gs.wait(3u * i + 2);
+    // polled by wave 3 (an lv wave): the mu waves' noise draw above is ~1 us
+    // of VALU that would otherwise delay the poll
+    gs.wait(3u * i + 2, 3);
     PSTAMP(4);
     float ev[4] = {0.f, 0.f, 0.f, 0.f};  // mu (part 0) / lv (part 1); sample x kept in epre
     if (has2) {
