@@ -75,12 +75,12 @@ int abcd_encoder_backward(const abcd_encoder_cfg* cfg, const abcd_encoder_params
                           void* stream);
 
 /* The same backward with part of the weight-gradient reductions on
- * `wgrad_stream`: for a single bidirectional layer on the persistent split-K
- * path, the gradients of the rows the BPTT finishes in its first half are
- * reduced on wgrad_stream BESIDE the second half (a gate kernel waits on the
- * BPTT's progress counters); the rest follow on `stream`, which waits for
- * them, so on return every gradient is complete in `stream` order.
- * wgrad_stream == NULL or == stream: identical to abcd_encoder_backward. */
+ * `wgrad_stream`: for a bidirectional encoder, the first layer's
+ * backward-direction weight gradients are reduced on wgrad_stream (forked
+ * after the BPTT) beside the forward direction's on `stream`, which then
+ * waits for wgrad_stream, so on return every gradient is complete in
+ * `stream` order.  wgrad_stream == NULL or == stream: identical to
+ * abcd_encoder_backward. */
 int abcd_encoder_backward_overlap(const abcd_encoder_cfg* cfg, const abcd_encoder_params* p, const abcd_packed* x,
                                   const float* d_last_hidden, const abcd_encoder_grads* g, void* ws, size_t ws_bytes,
                                   void* stream, void* wgrad_stream);

@@ -358,7 +358,7 @@ static EncWS carve_encoder(Arena& A, const abcd_encoder_cfg* c, int T, int L, in
     maxMN = std::max(maxMN, (size_t)G * H * std::max(In, H));
   }
   w.GX = A.f((size_t)L * D * G * H);
-  w.dWb = A.f((size_t)G * H * (F + 1));
+  w.dWb = A.f((size_t)D * G * H * (F + 1));  // one per direction (their reductions may run concurrently)
   w.off = (int*)A.f((size_t)T + 1);
   w.sync = (unsigned*)A.f(persist_sync_uints(D, B));
   w.part = A.f(persist_part_floats(D, B, H));
@@ -521,7 +521,9 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
   const std::vector<int> off = step_offsets(x->batch_sizes, T);
   const int64_t* bs = x->batch_sizes;
   const int TN = bwd_tn(H);
-  (void)wgrad_stream;  // the encoder's weight gradients follow the BPTT on s (a side-stream gate measured no gain)
+  // wgrad_stream: the last layer's backward-direction weight gradients run
+  // there after the BPTT, beside the forward direction's on s (a side-stream
+  // gate that started them DURING the BPTT measured no gain)
   for (int l = c->layers - 1; l >= 0; --l) {
     const int In = l == 0 ? F : D * H;
     for (int d = 0; d < D; ++d)
@@ -596,11 +598,12 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       const float* dGH = w.dGH[l][d] + (size_t)r0 * GH;
       if (ones_col && r0 == 0 && r1 == L && beta == 0.f && gr.w_ih && gr.b_ih) {
         // [dW_ih | db] in one GEMM
-        ABCD_TRY((hipError_t)gemm(st, GH, In + 1, K, opKM(dGX, GH, GH), opKM(X, ldxx, In + 1), w.dWb, In + 1, 1.f,
+        float* dWb = w.dWb + (size_t)d * GH * (In + 1);
+        ABCD_TRY((hipError_t)gemm(st, GH, In + 1, K, opKM(dGX, GH, GH), opKM(X, ldxx, In + 1), dWb, In + 1, 1.f,
                                   0.f, nullptr, ACT_NONE, scratch, scf));
         const bool same = dGX == dGH;  // LSTM: b_hh receives the same sum
         split_wb_kernel<<<(int)std::min<long>(1024, cdiv((long)GH * (In + 1), 256)), 256, 0, st>>>(
-            w.dWb, GH, In, gr.w_ih, gr.b_ih, same ? gr.b_hh : nullptr);
+            dWb, GH, In, gr.w_ih, gr.b_ih, same ? gr.b_hh : nullptr);
         ABCD_CHECK_LAUNCH();
         if (gr.w_hh)
           ABCD_TRY((hipError_t)gemm(st, GH, H, K, opKM(dGH, GH, GH), opKM(w.Hprev[l][d], H, H), gr.w_hh, H, 1.f,
@@ -627,7 +630,20 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       set_col_kernel<<<std::max(1, std::min(1024, cdiv(L, 256))), 256, 0, s>>>(w.Xp, Fp, L, F, 1.f);
       ABCD_CHECK_LAUNCH();
     }
-    for (int d = 0; d < D; ++d) ABCD_TRY((hipError_t)wgrad(s, d, 0, L, 0.f, w.scratch, w.scratch_floats));
+    if (D == 2 && l == 0 && wgrad_stream && wgrad_stream != stream) {
+      // the last layer's two directions reduce concurrently: the backward
+      // direction on wgrad_stream (forked after the BPTT), the forward one on
+      // s, each with half of the split-K scratch; s then waits for
+      // wgrad_stream, so every gradient is complete in `stream` order
+      hipStream_t sw = (hipStream_t)wgrad_stream;
+      const size_t half = w.scratch_floats / 2;
+      ABCD_TRY((hipError_t)stream_fork(s, sw, 6));
+      ABCD_TRY((hipError_t)wgrad(sw, 1, 0, L, 0.f, w.scratch + half, half));
+      ABCD_TRY((hipError_t)wgrad(s, 0, 0, L, 0.f, w.scratch, half));
+      ABCD_TRY((hipError_t)stream_fork(sw, s, 7));
+    } else {
+      for (int d = 0; d < D; ++d) ABCD_TRY((hipError_t)wgrad(s, d, 0, L, 0.f, w.scratch, w.scratch_floats));
+    }
     if (l > 0) {  // dX of this layer = dh of the layer below (both directions)
       for (int d = 0; d < D; ++d) {
         ABCD_TRY((hipError_t)pack2d(s, p->w[l][d].w_ih, In, In, GH, true, w.WihT[l][d], GH, In, GH));
