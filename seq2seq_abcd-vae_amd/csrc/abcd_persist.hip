@@ -1853,12 +1853,33 @@ template <class K>
 static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
   *ok = false;
   if (lds > 160 * 1024) return 0;
-  ABCD_TRY(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  int dev = 0, cus = 0, per = 0;
+  // (kernel, LDS bytes, device) -> resident workgroups on the chip; the
+  // attribute and occupancy queries run once per key, not once per launch
+  struct Key {
+    const void* k;
+    size_t lds;
+    int dev;
+  };
+  static std::mutex mu;
+  static std::vector<std::pair<Key, long>> cache;
+  int dev = 0;
   ABCD_TRY(hipGetDevice(&dev));
-  ABCD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  ABCD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kernel, 256, lds));
-  *ok = per > 0 && (long)grid <= (long)cus * per;
+  long cap = -1;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto& e : cache)
+      if (e.first.k == (const void*)kernel && e.first.lds == lds && e.first.dev == dev) cap = e.second;
+  }
+  if (cap < 0) {
+    int cus = 0, per = 0;
+    ABCD_TRY(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    ABCD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    ABCD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kernel, 256, lds));
+    cap = (long)cus * per;
+    std::lock_guard<std::mutex> lk(mu);
+    cache.push_back({Key{(const void*)kernel, lds, dev}, cap});
+  }
+  *ok = cap > 0 && (long)grid <= cap;
   return 0;
 }
 
