@@ -358,8 +358,9 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
         st4(rg, go + (uint32_t)(j * H) * 4u, tp_quad(tb, v, lane), false);
       }
       if (G == 4) st4(make_rsrc(D.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qh, tp_quad(tb, cv, lane), false);
-      st4(make_rsrc(D.Y + (size_t)o * D.ldy, (uint32_t)bs * D.ldy * 4u),
-          (uint32_t)((row0 + trow) * D.ldy + u0 + tcol) * 4u, tp_quad(tb, hv, lane), false);
+      if (D.Y)  // (null: the top layer's output sequence, which nothing reads)
+        st4(make_rsrc(D.Y + (size_t)o * D.ldy, (uint32_t)bs * D.ldy * 4u),
+            (uint32_t)((row0 + trow) * D.ldy + u0 + tcol) * 4u, tp_quad(tb, hv, lane), false);
       if (G == 4 && row0 < next_bs)
         st4(make_rsrc(D.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qh, tp_quad(tb, cv, lane), false);
     }

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void rnn_fwd_step(FwdArgs a) {
     Gr[unit] = r_; Gr[H + unit] = z_; Gr[2 * H + unit] = n_; Gr[3 * H + unit] = gh[G - 1];
     if (!haspred) D.Hprev[rr * H + unit] = 0.f;
   }
-  D.Y[rr * D.ldy + unit] = h;
+  if (D.Y) D.Y[rr * D.ldy + unit] = h;  // (null: the top encoder layer, whose output sequence nothing reads)
   if (b < D.next_bs) {
     D.Hprev[(long)(D.next_off + b) * H + unit] = h;
     if (G == 4) D.Cprev[(long)(D.next_off + b) * H + unit] = c;
@@ -352,7 +352,7 @@ static EncWS carve_encoder(Arena& A, const abcd_encoder_cfg* c, int T, int L, in
       w.dGH[l][d] = c->rnn_type == ABCD_LSTM ? w.dGX[l][d] : A.f((size_t)L * G * H);
       w.DC[l][d] = A.f((size_t)L * H);
     }
-    w.Y[l] = A.f((size_t)L * D * H);
+    w.Y[l] = l + 1 < c->layers ? A.f((size_t)L * D * H) : nullptr;  // the top layer's sequence is never read
     w.DHX[l] = l + 1 < c->layers ? A.f((size_t)L * D * H) : nullptr;
     w.Ydrop[l] = l + 1 < c->layers ? A.f((size_t)L * D * H) : nullptr;
     maxMN = std::max(maxMN, (size_t)G * H * std::max(In, H));
@@ -433,7 +433,7 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
         f.GX = w.GX + (size_t)d * G * H; f.ldgx = (long)D * G * H;
         f.bhh = G == 3 ? W.b_hh : nullptr;
         f.Gst = w.Gst[l][d]; f.Cst = w.Cst[l][d];
-        f.Y = w.Y[l] + (size_t)d * H; f.ldy = (long)D * H;
+        f.Y = l + 1 < c->layers ? w.Y[l] + (size_t)d * H : nullptr; f.ldy = (long)D * H;
         f.Hprev = w.Hprev[l][d]; f.Cprev = w.Cprev[l][d];
         f.out = last_hidden; f.ldo = E;
         const int base = (l * D + d) * (G == 4 ? 2 * H : H);
@@ -468,7 +468,7 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
         f.bih = nullptr;
         f.bhh = G == 3 ? W.b_hh : nullptr;
         f.Gst = w.Gst[l][d]; f.Cst = w.Cst[l][d];
-        f.Y = w.Y[l] + (size_t)d * H; f.ldy = (long)D * H;
+        f.Y = l + 1 < c->layers ? w.Y[l] + (size_t)d * H : nullptr; f.ldy = (long)D * H;
         f.Hprev = w.Hprev[l][d]; f.Cprev = w.Cprev[l][d];
         f.out = last_hidden; f.ldo = E;
         const int base = (l * D + d) * (G == 4 ? 2 * H : H);
