@@ -192,7 +192,14 @@ def cpu_baseline(cfg, cfg_name, device, target_s=10.0, budget_s=25.0):
               "seed-1111 weights, replayed noise; oracle = torch-CPU restatement pinned to the reference's "
               "fixtures (tests/golden)"}
     if not cfg["plain"]:
-        parity["argmax_equal"] = bool(torch.equal(logits.argmax(-1).cpu(), ref["logits"].argmax(-1)))
+        lh, lr = logits.float().cpu(), ref["logits"].float()
+        ah, ar = lh.argmax(-1), lr.argmax(-1)
+        parity["argmax_equal"] = bool(torch.equal(ah, ar))
+        parity["logits_max_abs_diff"] = float((lh - lr).abs().max())
+        bad = (ah != ar).nonzero().flatten()
+        parity["argmax_mismatch_rows"] = int(bad.numel())
+        if bad.numel():  # the oracle's own gap between its top category and the HIP's pick: a near-tie?
+            parity["argmax_tie_gap"] = float((lr[bad, ar[bad]] - lr[bad, ah[bad]]).max())
     del step
     return base, parity
 

@@ -9,6 +9,7 @@
 //              whose reduction runs over the packed frames (K = L ~ 65k), where
 //              the grid is also split along K into fp32 slabs that a second
 //              pass reduces deterministically.
+#include <numeric>
 #include <cstdlib>
 
 #include "abcd_common.h"
@@ -841,12 +842,13 @@ template <int NC, int BN, int MR, int OCC = 1>
 static int gemm_x6r_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
                            EpiArgs e) {
   const int nslices = cdiv(N, BN);
-  // OCC workgroups per CU: 256 OCC / nslices frame ranges (grid a multiple of 8)
-  const int nparts = std::max(1, 256 * OCC / nslices);
-  int grid = nslices * nparts;
-  grid = (grid + 7) / 8 * 8;
-  const int nparts_eff = cdiv(grid, nslices);
-  const int rows_per = ((cdiv(M, nparts_eff) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
+  // OCC workgroups per CU: about 256 OCC / nslices frame ranges, their count
+  // a multiple of 8 / gcd(nslices, 8) so that the grid (every (slice, range)
+  // pair exactly once) is a multiple of 8 for the kernel's XCD grouping
+  const int step = 8 / std::gcd(nslices, 8);
+  const int nparts = std::max(step, (256 * OCC / nslices) / step * step);
+  const int grid = nslices * nparts;
+  const int rows_per = ((cdiv(M, nparts) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
   const size_t lds = (size_t)(BN / 16) * NC * 3 * 64 * 16 + (size_t)4 * 16 * (BN + 4) * 4;
   static bool attr = false;  // per process (the attribute is per function, not per device)
   if (!attr) {

@@ -8,12 +8,14 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("M,N,K", [(16, 16, 16), (33, 70, 48), (512, 1024, 256), (65, 2048, 144), (7, 5, 3),
                                    (1000, 129, 385), (300, 512, 1024), (8001, 520, 144), (7000, 256, 256),
-                                   (9000, 300, 136), (64044, 2048, 144)])
+                                   (9000, 300, 136), (64044, 2048, 144), (22854, 1536, 144), (30001, 384, 256)])
 def test_gemm_nt_vs_torch(M, N, K):
     """C = A B^T + bias; the shapes from (8001, 520, 144) on take the
     frame-parallel route (>= 240 128-wide tiles): K <= 256 the frame-streaming
     split-fp32 gemm_x6r (ragged M / N, a partial last K chunk, the c2 input
-    projection), else the fragment-staged gemm_x6f."""
+    projection, the GRU encoder's 3 x 2 x 256 = 1536 gate columns: slice
+    counts that do not divide the grid evenly), else the fragment-staged
+    gemm_x6f."""
     from modules import _native as Nn
     g = torch.Generator(device="cuda").manual_seed(M * 1000 + N + K)
     A = torch.randn(M, K, device="cuda", generator=g)
