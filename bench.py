@@ -133,7 +133,7 @@ REFERENCE_CPU = {
 }
 
 
-def cpu_baseline(cfg, cfg_name, device, target_s=10.0, budget_s=25.0):
+def cpu_baseline(cfg, cfg_name, device, target_s=10.0, budget_s=25.0, min_steps=3):
     """Time the CPU oracle on a bounded sample of the same workload: one
     untimed warm-up step, then b = 64 steps until ~target_s of CPU work
     (at least 3, stopping past budget_s).
@@ -163,7 +163,7 @@ def cpu_baseline(cfg, cfg_name, device, target_s=10.0, budget_s=25.0):
     obatch = dict(data=batch["data"], batch_sizes=bsz, is_offset=batch["is_offset"], speakers=batch["speakers"])
     ref, _, _, _, _ = O.train_step(P, obatch, ocfg, noise, cfg["N"])
     steps, t_total = 0, 0.0
-    while steps < 3 or t_total < target_s:
+    while steps < min_steps or (min_steps and t_total < target_s):
         t0 = time.perf_counter()
         O.train_step(P, obatch, ocfg, noise, cfg["N"])
         t_total += time.perf_counter() - t0
@@ -171,7 +171,7 @@ def cpu_baseline(cfg, cfg_name, device, target_s=10.0, budget_s=25.0):
         if t_total > budget_s:
             break
     rc = REFERENCE_CPU.get(cfg_name)
-    base = {"value": round(steps * b / t_total, 3), "unit": "segments/s", "cores": threads, "kind": "port",
+    base = {"value": round(steps * b / t_total, 3) if steps else None, "unit": "segments/s", "cores": threads, "kind": "port",
             "sample": f"{steps} oracle train steps of b={b} segments (T_max={cfg['tmax']}, L={batch['L']} frames) "
                       f"of the {cfg['workload']} workload, torch-CPU fp32, {threads} threads",
             "reference_cpu_seg_s": None if rc is None else rc["value"],
