@@ -18,7 +18,10 @@ Besides the one JSON line the driver reads, it reports
   cpu_baseline -- the CPU oracle (oracle/abcd_oracle.py, a torch-CPU
                   restatement of the reference step) timed on a bounded sample
                   on this host (rank 0, N = 1 only).
-For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
+For N > 1 the driver launches it under torch.distributed.run (one rank per
+GPU, RCCL, WORLD_SIZE set).  Run by hand as ``bench.py --gpus N`` without a
+WORLD_SIZE, the process starts that same launcher as a CHILD (N fresh worker
+processes; this parent never touches the GPU) and exits with its code.
 """
 import argparse
 import json
@@ -204,6 +207,43 @@ def cpu_baseline(cfg, cfg_name, device, target_s=10.0, budget_s=25.0, min_steps=
     return base, parity
 
 
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` with no WORLD_SIZE: run N ranks through
+    torch.distributed.run as a child process (rendezvous on 127.0.0.1, one
+    rank per GPU) and return its exit code.  Nothing here initialises the GPU
+    (torch.cuda.device_count does not on this image), so the parent is never
+    a GPU process that would have to be replaced."""
+    import socket
+    import subprocess
+    if not os.environ.get("ABCD_BENCH_DRYRUN"):
+        have = torch.cuda.device_count()
+        if have < n:
+            raise SystemExit(f"bench.py --gpus {n}: only {have} GPU(s) visible")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def dryrun_rank():
+    """ABCD_BENCH_DRYRUN=1: a CPU stand-in for one bench rank (gloo, no GPU):
+    checks the launcher's per-rank environment and prints what rank 0 sees.
+    Used by the CPU test of the --gpus N launch path."""
+    world = int(os.environ["WORLD_SIZE"])
+    rank, local = int(os.environ["RANK"]), int(os.environ["LOCAL_RANK"])
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(rank), float(local)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"dryrun": True, "world_size": dist.get_world_size(), "env_world": world,
+                          "rank_sum": float(t[0]), "local_rank_sum": float(t[1]),
+                          "master_addr": os.environ.get("MASTER_ADDR")}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,10 +255,16 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if os.environ.get("ABCD_BENCH_DRYRUN"):
+        return dryrun_rank()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"bench.py --gpus {args.gpus} under WORLD_SIZE={world}")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -280,6 +326,9 @@ def main():
                    "parallelism": f"dp{world}", "noise": "philox in-kernel", "final_loss": round(loss, 4)},
         "step_tflops": round(fl / (elapsed / args.steps) / 1e12, 3),
     }
+    if world > 1:
+        out["config"]["rccl_world_size"] = dist.get_world_size()
+        out["allreduce_us_per_step"] = allreduce_time(step)
     if not args.no_kernel_timing:
         out["roofline"] = kernel_roofline(step, batches, cfg, run, args.config)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -290,6 +339,26 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def allreduce_time(step, reps=10):
+    """Mean time of the step's one collective (the SUM all-reduce of the flat
+    fp32 gradient buffer, parallel.make_allreduce) on this rank, in us, max
+    over ranks; bracketed by events on the current stream (the process
+    group's collective is stream-ordered after it and waited for by it)."""
+    g = step.flat.grad
+    step.allreduce(g)
+    torch.cuda.synchronize()
+    dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        step.allreduce(g)
+    e1.record()
+    torch.cuda.synchronize()
+    t = torch.tensor([e0.elapsed_time(e1) * 1e3 / reps], device=g.device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return round(float(t), 2)
 
 
 def load_traffic(kernel, cfg_name):

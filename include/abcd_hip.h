@@ -22,9 +22,18 @@
  *   - return value: 0 on success, a hipError_t code, or ABCD_EINVAL for
  *     unsupported shapes/arguments.  Nothing throws across this ABI.
  *
- * Shape support: hidden sizes, MLP width, codebook dim, #categories, speaker
- * embedding dim and the plain feature size must be multiples of 16; the
- * frequency-bin count F is arbitrary (padded internally); encoder layers <= 4.
+ * Shape support: the kernels take hidden sizes, MLP width, codebook dim,
+ * #categories, speaker embedding dim and the plain feature size in multiples
+ * of 16; the frequency-bin count F is arbitrary (padded internally); encoder
+ * layers <= 4.  Any other size (the reference accepts every -K, -f and
+ * --*_hidden_size, learning.py:371-376) runs as the ZERO-PADDED model: each
+ * size rounded up to 16, the real weights embedded at their unit / gate /
+ * block positions and every padding weight 0.  Padding units then stay exactly
+ * 0 through every recurrence, tanh and product, so values and gradients at the
+ * real positions are the real model's; only the categorical softmax needs to
+ * know the real sizes (abcd_sampler_cfg.valid_categories / valid_feature_dim).
+ * The Python host (modules/padding.py) embeds the parameters and extracts the
+ * gradients; INTEGRATION.md shows the index maps.
  */
 #ifndef ABCD_HIP_H
 #define ABCD_HIP_H
@@ -105,6 +114,13 @@ int abcd_encoder_backward_dropout(const abcd_encoder_cfg* cfg, const abcd_encode
 typedef struct abcd_sampler_cfg {
   int input_size, mlp_hidden, num_categories, feature_dim;
   int plain; /* 1: plain Gaussian feature sampler (feature_dim = output_size) */
+  /* A zero-padded model (every size rounded up to 16, padding weights 0; see
+   * "Shape support" above): the model's own category count (the first
+   * valid_categories of the num_categories logit columns are categories, the
+   * rest are masked out of every softmax, KL and perplexity) and feature dim
+   * (the logits scale 1 / sqrt(valid_feature_dim), model.py:589).  0: the
+   * padded size itself. */
+  int valid_categories, valid_feature_dim;
 } abcd_sampler_cfg;
 typedef struct abcd_sampler_params {
   abcd_mlp_w mlp[2];                 /* ABCD: mlp[0] = to_code_like; plain: mlps.0 (mean), mlps.1 (log-var) */
@@ -319,6 +335,14 @@ int abcd_gemm_tn(int M, int N, int K, const float* A, long lda, const float* B, 
  * ws >= (M + N) * roundup(K,16) * 4 bytes when K is not a multiple of 16. */
 int abcd_linear(int M, int N, int K, const float* x, long ldx, const float* W, long ldw, const float* b, int act,
                 float* y, long ldy, void* ws, size_t ws_bytes, void* stream);
+/* backward of abcd_linear (the standalone MLP's training path, model.py:316-334):
+ * dy' = dy (act 0) or dy (1 - y^2) (act 1, y = the forward's output);
+ * dx = dy' W (M x K, may be NULL), dW = dy'^T x (N x K, row stride K, may be
+ * NULL), db = column sums of dy' (N, may be NULL).  Any M, N, K. */
+size_t abcd_linear_backward_workspace_bytes(int M, int N, int K);
+int abcd_linear_backward(int M, int N, int K, const float* x, long ldx, const float* W, long ldw, const float* y,
+                         long ldy, int act, const float* dy, long lddy, float* dx, long lddx, float* dW, float* db,
+                         void* ws, size_t ws_bytes, void* stream);
 /* n standard normals from Philox-4x32-10(seed, offset + i) */
 int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offset, void* stream);
 /* dropout noise bernoulli(1 - p) / (1 - p) from the same Philox stream */

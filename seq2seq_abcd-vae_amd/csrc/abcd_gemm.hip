@@ -1427,6 +1427,68 @@ extern "C" int abcd_linear(int M, int N, int K, const float* x, long ldx, const 
               ws_bytes / 4 - need);
 }
 
+namespace abcd {
+// dy' = dy (act none) or dy (1 - y^2) (tanh) into an M x Np buffer, zero in the padding columns
+__global__ void linear_dact(const float* dy, long lddy, const float* y, long ldy, int act, int M, int N, int Np,
+                            float* out) {
+  const long n = (long)M * Np;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int m = (int)(i / Np), j = (int)(i - (long)m * Np);
+    float v = 0.f;
+    if (j < N) {
+      v = dy[(long)m * lddy + j];
+      if (act == ACT_TANH) {
+        const float t = y[(long)m * ldy + j];
+        v *= 1.f - t * t;
+      }
+    }
+    out[i] = v;
+  }
+}
+static size_t linear_bwd_floats(int M, int N, int K) {
+  const size_t Np = rup16(N), K4 = (K + 3) & ~3;
+  return (size_t)M * Np + Np * K4 + (size_t)M * K4 + ((size_t)1 << 20) + 3 * 64;
+}
+}  // namespace abcd
+
+extern "C" size_t abcd_linear_backward_workspace_bytes(int M, int N, int K) {
+  return M > 0 && N > 0 && K > 0 ? abcd::linear_bwd_floats(M, N, K) * 4 : 0;
+}
+
+// C ABI: backward of abcd_linear (y = act(x W^T + b)): dx = dy' W, dW = dy'^T x,
+// db = sum_m dy' with dy' = dy (1 - y^2) for tanh; each output may be NULL
+extern "C" int abcd_linear_backward(int M, int N, int K, const float* x, long ldx, const float* W, long ldw,
+                                    const float* y, long ldy, int act, const float* dy, long lddy, float* dx,
+                                    long lddx, float* dW, float* db, void* ws, size_t ws_bytes, void* stream) {
+  using namespace abcd;
+  if (M <= 0 || N <= 0 || K <= 0 || !dy || !ws || (act != ACT_NONE && act != ACT_TANH)) return ABCD_EINVAL;
+  if ((act == ACT_TANH && !y) || (dx && !W) || (dW && !x)) return ABCD_EINVAL;
+  if (ws_bytes / 4 < linear_bwd_floats(M, N, K)) return ABCD_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int Np = rup16(N), K4 = (K + 3) & ~3;
+  Arena A(ws, ws_bytes);
+  float* dyp = A.f((size_t)M * Np);
+  float* Wp = A.f((size_t)Np * K4);
+  float* xp = A.f((size_t)M * K4);
+  float* sc = A.f((size_t)1 << 20);
+  ABCD_REQUIRE(A.ok);
+  linear_dact<<<(int)std::min<long>(4096, cdiv((long)M * Np, 256)), 256, 0, s>>>(dy, lddy, y, ldy, act, M, N, Np,
+                                                                                  dyp);
+  ABCD_CHECK_LAUNCH();
+  if (dx) {  // dx(m, k) = sum_n dy'(m, n) W(n, k)
+    ABCD_TRY((hipError_t)pack2d(s, W, ldw, N, K, false, Wp, K4, Np, K4));
+    ABCD_TRY((hipError_t)gemm(s, M, K, Np, opKC(dyp, Np, M), opKM(Wp, K4, K), dx, lddx, 1.f, 0.f, nullptr, ACT_NONE,
+                              nullptr, 0));
+  }
+  if (dW) {  // dW(n, k) = sum_m dy'(m, n) x(m, k)
+    ABCD_TRY((hipError_t)pack2d(s, x, ldx, M, K, false, xp, K4, M, K4));
+    ABCD_TRY((hipError_t)gemm(s, N, K, M, opKM(dyp, Np, N), opKM(xp, K4, K), dW, K, 1.f, 0.f, nullptr, ACT_NONE, sc,
+                              (size_t)1 << 20));
+  }
+  if (db) ABCD_TRY((hipError_t)colsum(s, dyp, Np, M, N, nullptr, db, 0.f, sc, (size_t)1 << 20));
+  return 0;
+}
+
 extern "C" int abcd_fill_dropout(float* out, long n, float p, uint64_t seed, uint64_t offset, void* stream) {
   if (!out || n < 0 || !(p >= 0.f && p < 1.f)) return ABCD_EINVAL;
   if (n == 0) return 0;

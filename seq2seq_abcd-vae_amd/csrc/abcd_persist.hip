@@ -131,6 +131,17 @@ DEV void pin(float (&v)[N]) {
 #pragma unroll
   for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
 }
+// Once any wait has timed out (this launch: g_persist_status; an earlier
+// step not yet read back by abcd_device_status: g_persist_sticky) the results
+// are invalid anyway, so a wait that is still unsatisfied after
+// SPIN_PROBE_MASK + 1 polls gives up at once instead of spinning to its own
+// limit: a failed step drains in ~one wait instead of one limit per wait.
+// Probed every 1024 polls only, off the fast path of a healthy hand-off.
+constexpr unsigned SPIN_PROBE_MASK = 1023;
+DEV bool spin_abandoned() {
+  return (__hip_atomic_load(&g_persist_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+          __hip_atomic_load(&g_persist_sticky, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+}
 // lane 0 of the workgroup polls until *cnt >= target (bounded), then the
 // barrier releases every wave
 DEV void group_wait(unsigned* cnt, unsigned target, int pw = 0) {
@@ -143,6 +154,7 @@ DEV void group_wait(unsigned* cnt, unsigned target, int pw = 0) {
         __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
+      if ((spins & SPIN_PROBE_MASK) == 0 && spin_abandoned()) break;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -184,6 +196,7 @@ DEV void flags_wait(const unsigned* fl, int M, unsigned epoch, int pw = 0) {
         if (lane == 0) __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
+      if ((spins & SPIN_PROBE_MASK) == 0 && spin_abandoned()) break;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

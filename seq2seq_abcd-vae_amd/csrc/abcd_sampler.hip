@@ -13,6 +13,9 @@
 
 namespace abcd {
 
+// learning.py:171-178 perplexities of rows of `ld` floats (first K = categories)
+int perplexities_ld(const float* logits, int B, int ld, int K, const float* psl, float* out, void* stream);
+
 // ---- special functions (fp64, x > 0) --------------------------------------
 DEV double digamma_d(double x) {
   double r = 0.0;
@@ -42,17 +45,20 @@ DEV double wave_sum_d(double v) {
   return v;
 }
 
-// y = softmax((logits + g) / tau) per row (g = 0 for the plain softmax)
-__global__ void sample_softmax_rows(const float* logits, int B, int K, int gumbel, float tau, const float* noise,
-                                    uint64_t seed, uint64_t offset, float* Y) {
+// y = softmax((logits + g) / tau) per row (g = 0 for the plain softmax).
+// Rows have K columns of which the first Kv are categories; the padding
+// columns (a zero-padded model, modules/padding.py) get y = 0.
+__global__ void sample_softmax_rows(const float* logits, int B, int K, int Kv, int gumbel, float tau,
+                                    const float* noise, uint64_t seed, uint64_t offset, float* Y) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   const float* l = logits + (long)b * K;
   float* y = Y + (long)b * K;
   const float it = 1.f / tau;
+  for (int k = Kv + lane; k < K; k += 64) y[k] = 0.f;
   float m = -INFINITY;
-  for (int k = lane; k < K; k += 64) {
+  for (int k = lane; k < Kv; k += 64) {
     float v = l[k];
     if (gumbel) v = (v + (noise ? noise[(long)b * K + k] : philox_gumbel(seed, offset + (uint64_t)b * K + k))) * it;
     y[k] = v;
@@ -60,14 +66,14 @@ __global__ void sample_softmax_rows(const float* logits, int B, int K, int gumbe
   }
   m = wave_max(m);
   float s = 0.f;
-  for (int k = lane; k < K; k += 64) {
+  for (int k = lane; k < Kv; k += 64) {
     const float e = __expf(y[k] - m);
     y[k] = e;
     s += e;
   }
   s = wave_sum(s);
   const float is = 1.f / s;
-  for (int k = lane; k < K; k += 64) y[k] *= is;
+  for (int k = lane; k < Kv; k += 64) y[k] *= is;
 }
 
 // Block reductions (blockDim = 64 x nw, nw <= 16); `sh` holds 16 doubles.
@@ -97,11 +103,19 @@ DEV double block_max_dd(double v, double* sh) {
 // alpha = p N + a0, elog = psi(alpha) - psi(S).  alphaL / elogL: K floats of
 // block-shared scratch receiving alpha and elog (as fp32, the values the row
 // terms use).  stash: also p / alpha / elog / tri to global and
-// kl_small = [Eq log q(pi) - Eq log p(pi), psi'(S), S].
-DEV void prior_block(const float* psl, int K, double N, float a0, float* alphaL, float* elogL, double* sh,
+// kl_small = [Eq log q(pi) - Eq log p(pi), psi'(S), S].  Only the first Kv of
+// the K entries are categories; the padding entries are written as 0 (so the
+// row terms that read them multiply a zero probability by a finite value).
+DEV void prior_block(const float* psl, int K, int Kv, double N, float a0, float* alphaL, float* elogL, double* sh,
                      bool stash, float* p_out, float* alpha_out, float* elog_out, float* tri_out,
                      double* kl_small) {
   const int tid = threadIdx.x, nt = blockDim.x;
+  for (int k = Kv + tid; k < K; k += nt) {
+    alphaL[k] = 0.f;
+    elogL[k] = 0.f;
+    if (stash) { p_out[k] = 0.f; alpha_out[k] = 0.f; elog_out[k] = 0.f; tri_out[k] = 0.f; }
+  }
+  K = Kv;
   double m = -1e300;
   for (int k = tid; k < K; k += nt) m = fmax(m, (double)psl[k]);
   m = block_max_dd(m, sh);
@@ -142,27 +156,28 @@ DEV void prior_block(const float* psl, int K, double N, float a0, float* alphaL,
 }
 
 // standalone form (abcd_sampler_kl): alpha / elog land in the global stash
-__global__ void kl_prior(const float* psl, int K, double N, float a0, float* p_out, float* alpha_out,
+__global__ void kl_prior(const float* psl, int K, int Kv, double N, float a0, float* p_out, float* alpha_out,
                          float* elog_out, float* tri_out, double* kl_small) {
   __shared__ double sh[16];
-  prior_block(psl, K, N, a0, alpha_out, elog_out, sh, true, p_out, alpha_out, elog_out, tri_out, kl_small);
+  prior_block(psl, K, Kv, N, a0, alpha_out, elog_out, sh, true, p_out, alpha_out, elog_out, tri_out, kl_small);
 }
 
-// per row: Q = softmax(l); v_b = sum_k Q (log Q - elog)
-__global__ void kl_rows(const float* logits, int B, int K, const float* elog, float* Q, float* v) {
+// per row: Q = softmax(l); v_b = sum_k Q (log Q - elog)  (padding columns: Q = 0)
+__global__ void kl_rows(const float* logits, int B, int K, int Kv, const float* elog, float* Q, float* v) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   const float* l = logits + (long)b * K;
+  for (int k = Kv + lane; k < K; k += 64) Q[(long)b * K + k] = 0.f;
   float m = -INFINITY;
-  for (int k = lane; k < K; k += 64) m = fmaxf(m, l[k]);
+  for (int k = lane; k < Kv; k += 64) m = fmaxf(m, l[k]);
   m = wave_max(m);
   float s = 0.f;
-  for (int k = lane; k < K; k += 64) s += __expf(l[k] - m);
+  for (int k = lane; k < Kv; k += 64) s += __expf(l[k] - m);
   s = wave_sum(s);
   const float ls = __logf(s);
   float acc = 0.f;
-  for (int k = lane; k < K; k += 64) {
+  for (int k = lane; k < Kv; k += 64) {
     const float lq = l[k] - m - ls;
     const float q = __expf(lq);
     Q[(long)b * K + k] = q;
@@ -430,6 +445,7 @@ constexpr int HEAD_MAX_SLABS = 8;  // split-K slabs the forward head sums (gemm_
 
 struct HeadFwdArgs {
   int B, Hm, D, K, nslab;
+  int Kv; float rsD;  // categories (the first Kv of K columns), 1 / sqrt(model feature dim)
   const float *slab, *b1, *W2, *b2, *C, *psl;  // slab: nslab x B x Hm raw partials of h W1^T
   double N; float a0;
   int gumbel; float tau; const float* noise; uint64_t seed, offset;
@@ -536,8 +552,9 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     }
   });
   __syncthreads();
-  // logits = U C / sqrt(D)   (C: D x K, the K-major operand)
-  const float rs = 1.f / sqrtf((float)D);
+  // logits = U C / sqrt(D)   (C: D x K, the K-major operand; D the model's feature dim)
+  const float rs = a.rsD;
+  const int Kv = a.Kv;
   tile_mma_any(R2, ld2, D, bkm(a.C, K, D), K, w, lane, [&](int c0, f4 acc) {
     const int col = c0 + r;
 #pragma unroll
@@ -549,7 +566,8 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     }
   });
   // Dirichlet posterior: elog for the row terms (every tile), the stash once
-  prior_block(a.psl, K, a.N, a.a0, alphaL, elogL, sh, blockIdx.x == 0, a.p, a.alpha, a.elog, a.tri, a.kl_small);
+  prior_block(a.psl, K, Kv, a.N, a.a0, alphaL, elogL, sh, blockIdx.x == 0, a.p, a.alpha, a.elog, a.tri,
+              a.kl_small);
   // rows: KL row term v_b = sum_k Q (log Q - elog) (kl_rows) and the sample
   // Y = softmax((logits + g) / tau) (sample_softmax_rows), one wave per row,
   // the row's KPL logits per lane in registers
@@ -571,8 +589,8 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
 #pragma unroll
     for (int u = 0; u < KPL; ++u) {
       const int k = lane + 64 * u;
-      lv[u] = k < K ? l[k] : -INFINITY;
-      gv[u] = (a.gumbel && a.noise && k < K) ? a.noise[g0 + k] : 0.f;
+      lv[u] = k < Kv ? l[k] : -INFINITY;
+      gv[u] = (a.gumbel && a.noise && k < Kv) ? a.noise[g0 + k] : 0.f;
     }
     float m = -INFINITY;
 #pragma unroll
@@ -580,20 +598,22 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     m = wave_max(m);
     float se = 0.f;
 #pragma unroll
-    for (int u = 0; u < KPL; ++u) se += lane + 64 * u < K ? __expf(lv[u] - m) : 0.f;
+    for (int u = 0; u < KPL; ++u) se += lane + 64 * u < Kv ? __expf(lv[u] - m) : 0.f;
     se = wave_sum(se);
     const float ls = __logf(se);
     float acc = 0.f, ent = 0.f;
 #pragma unroll
     for (int u = 0; u < KPL; ++u) {
       const int k = lane + 64 * u;
-      if (k < K) {
+      if (k < Kv) {
         const float lq = lv[u] - m - ls;
         const float qv = __expf(lq);
         a.Q[g0 + k] = qv;
         acc += qv * (lq - elogL[k]);
         ent += -qv * lq;
         qcol[u] += qv;
+      } else if (k < K) {
+        a.Q[g0 + k] = 0.f;  // padding column of a zero-padded model
       }
     }
     acc = wave_sum(acc);
@@ -605,7 +625,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
 #pragma unroll
     for (int u = 0; u < KPL; ++u) {
       const int k = lane + 64 * u;
-      if (k < K && a.gumbel) {
+      if (k < Kv && a.gumbel) {
         const float g = a.noise ? gv[u] : philox_gumbel(a.seed, a.offset + (uint64_t)g0 + k);
         lv[u] = (lv[u] + g) * it;
       }
@@ -615,7 +635,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     float s2 = 0.f;
 #pragma unroll
     for (int u = 0; u < KPL; ++u) {
-      lv[u] = lane + 64 * u < K ? __expf(lv[u] - m2) : 0.f;
+      lv[u] = lane + 64 * u < Kv ? __expf(lv[u] - m2) : 0.f;
       s2 += lv[u];
     }
     s2 = wave_sum(s2);
@@ -702,6 +722,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
 
 struct HeadBwdArgs {
   int B, Hm, D, K; float it;                // it: 1 / tau (Gumbel mode), else 1
+  int Kv; float rsD;                        // as HeadFwdArgs
   const float *dfeat, *dkl, *Y, *Q, *v, *elog, *Z1, *C, *W2;
   const float *p, *alpha, *tri; const double* kl_small; double N; float a0;
   float* dfeat_copy;                       // the stacked [d_feats; U] operand of dC (top half), or null
@@ -801,7 +822,7 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
   // dL = Y (dY - sum Y dY) / tau  +  s Q ((log Q - elog) - v_b)
   // (sample_softmax_bwd + kl_rows_bwd), one wave per row; the next row's
   // Y / Q / v_b loads are in flight while this row is reduced
-  const float s = *a.dkl, rs = 1.f / sqrtf((float)D);
+  const float s = *a.dkl, rs = a.rsD;
   {
     const int rbase = w * (HEAD_ROWS / 4);
     float* qc = QcL + w * K;
@@ -889,7 +910,7 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
     else QcL[c - D - Hm] = t;
   }
   __syncthreads();
-  if (a.dpsl) prior_bwd_block(a.p, a.alpha, a.tri, a.kl_small, QcL, K, a.B, a.N, a.a0, s, a.dpsl, sh);
+  if (a.dpsl) prior_bwd_block(a.p, a.alpha, a.tri, a.kl_small, QcL, a.Kv, a.B, a.N, a.a0, s, a.dpsl, sh);
 }
 
 // KPL dispatch: K <= 64 * KPL
@@ -953,7 +974,16 @@ static int samp_check(const abcd_sampler_cfg* c) {
       c->feature_dim <= 0 || c->feature_dim % 16)
     return ABCD_EINVAL;
   if (!c->plain && (c->num_categories <= 0 || c->num_categories % 16)) return ABCD_EINVAL;
+  if (c->valid_categories < 0 || c->valid_categories > c->num_categories || c->valid_feature_dim < 0 ||
+      c->valid_feature_dim > c->feature_dim)
+    return ABCD_EINVAL;
   return 0;
+}
+// categories of a zero-padded model (modules/padding.py): the first Kv of the K columns
+static int kvalid(const abcd_sampler_cfg* c) { return c->valid_categories ? c->valid_categories : c->num_categories; }
+// the logits scale 1 / sqrt(D) of model.py:589 with the MODEL's feature dim
+static float rs_dim(const abcd_sampler_cfg* c) {
+  return 1.f / sqrtf((float)(c->valid_feature_dim ? c->valid_feature_dim : c->feature_dim));
 }
 
 static SampWS carve_sampler(Arena& A, const abcd_sampler_cfg* c, int B) {
@@ -1023,7 +1053,7 @@ extern "C" int abcd_sampler_forward(const abcd_sampler_cfg* c, const abcd_sample
                             nullptr, 0));
   // logits = U @ codebook / sqrt(D)   (codebook D x K used as a K-major operand)
   ABCD_TRY((hipError_t)gemm(s, B, K, D, opKC(w.U, D, B), opKM(p->codebook, K, K), logits, K,
-                            1.f / sqrtf((float)D), 0.f, nullptr, ACT_NONE, nullptr, 0));
+                            rs_dim(c), 0.f, nullptr, ACT_NONE, nullptr, 0));
   // the transposed codebook / W2 the fused backward reads (the fused forward writes them in-kernel)
   ABCD_TRY((hipError_t)pack2d(s, p->codebook, K, K, D, true, w.CT, D, K, D));
   return pack2d(s, m.w2, Hm, Hm, D, true, w.W2T[0], D, Hm, D);
@@ -1046,8 +1076,9 @@ extern "C" int abcd_sampler_sample(const abcd_sampler_cfg* c, const abcd_sampler
     return 0;
   }
   ABCD_REQUIRE(mode == ABCD_SAMPLE_SOFTMAX || temperature > 0.f);
-  sample_softmax_rows<<<cdiv(B, 4), 256, 0, s>>>(logits, B, K, mode == ABCD_SAMPLE_GUMBEL, mode == ABCD_SAMPLE_GUMBEL ? temperature : 1.f,
-                                                 noise, seed, offset, w.Y);
+  sample_softmax_rows<<<cdiv(B, 4), 256, 0, s>>>(logits, B, K, kvalid(c), mode == ABCD_SAMPLE_GUMBEL,
+                                                 mode == ABCD_SAMPLE_GUMBEL ? temperature : 1.f, noise, seed, offset,
+                                                 w.Y);
   ABCD_CHECK_LAUNCH();
   // feats = Y @ codebook^T
   return gemm(s, B, D, K, opKC(w.Y, K, B), opKC(p->codebook, K, D), feats, D, 1.f, 0.f, nullptr, ACT_NONE, nullptr,
@@ -1071,10 +1102,10 @@ extern "C" int abcd_sampler_kl(const abcd_sampler_cfg* c, const abcd_sampler_par
   }
   ABCD_REQUIRE(logits && N > 0);
   const int K = c->num_categories;
-  kl_prior<<<1, 256, 0, s>>>(p->posterior_shape_logits, K, N, p->prior_concentration, w.p, w.alpha, w.elog, w.tri,
-                             w.kl_small);
+  kl_prior<<<1, 256, 0, s>>>(p->posterior_shape_logits, K, kvalid(c), N, p->prior_concentration, w.p, w.alpha,
+                             w.elog, w.tri, w.kl_small);
   ABCD_CHECK_LAUNCH();
-  kl_rows<<<cdiv(B, 4), 256, 0, s>>>(logits, B, K, w.elog, w.Q, w.v);
+  kl_rows<<<cdiv(B, 4), 256, 0, s>>>(logits, B, K, kvalid(c), w.elog, w.Q, w.v);
   ABCD_CHECK_LAUNCH();
   kl_final<<<1, 256, 0, s>>>(w.kl_small, w.v, B, N, kl_out);
   ABCD_CHECK_LAUNCH();
@@ -1100,7 +1131,7 @@ extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_
       Arena A(ws, ws_bytes);
       SampWS w = carve_sampler(A, c, B);
       ABCD_REQUIRE(A.ok);
-      ABCD_TRY((hipError_t)abcd_perplexities(logits, B, K, p->posterior_shape_logits, w.ppl3, stream));
+      ABCD_TRY((hipError_t)perplexities_ld(logits, B, K, kvalid(c), p->posterior_shape_logits, w.ppl3, stream));
       ABCD_TRY(hipMemcpyAsync(ppl_out, w.ppl3, 2 * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
     }
     return 0;
@@ -1116,7 +1147,7 @@ extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_
   ABCD_TRY((hipError_t)gemm_slabs(s, B, Hm, E, opKC(h, E, B), opKC(m.w1, E, Hm), w.scratch,
                                         std::min(w.scratch_floats, (size_t)HEAD_MAX_SLABS * B * Hm), &Z));
   HeadFwdArgs a{};
-  a.B = B; a.Hm = Hm; a.D = D; a.K = K; a.nslab = Z;
+  a.B = B; a.Hm = Hm; a.D = D; a.K = K; a.nslab = Z; a.Kv = kvalid(c); a.rsD = rs_dim(c);
   a.slab = w.scratch; a.b1 = m.b1; a.W2 = m.w2; a.b2 = m.b2; a.C = p->codebook; a.psl = p->posterior_shape_logits;
   a.N = N > 0 ? N : 1.0; a.a0 = p->prior_concentration;
   a.gumbel = mode == ABCD_SAMPLE_GUMBEL; a.tau = a.gumbel ? temperature : 1.f;
@@ -1192,8 +1223,8 @@ static int samp_kl_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p, 
   if (d_psl) {  // forward products only: no wait on s beyond the caller's fork
     SideWork side(s, sw);
     ABCD_TRY((hipError_t)colsum(sw, w.Q, K, B, K, nullptr, w.Qsum, 0.f, w.scratch, w.scratch_floats));
-    kl_prior_bwd<<<1, 256, 0, sw>>>(w.p, w.alpha, w.tri, w.kl_small, w.Qsum, K, B, N, p->prior_concentration, d_kl,
-                                    d_psl);
+    kl_prior_bwd<<<1, 256, 0, sw>>>(w.p, w.alpha, w.tri, w.kl_small, w.Qsum, kvalid(c), B, N,
+                                    p->prior_concentration, d_kl, d_psl);
     ABCD_CHECK_LAUNCH();
   }
   return 0;
@@ -1214,7 +1245,7 @@ static int samp_fwd_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p,
   if (c->plain) {
     dOut[0] = d_logits; dOut[1] = d_logits + D; ldOut = 2 * D;
   } else {
-    const float rs = 1.f / sqrtf((float)D);
+    const float rs = rs_dim(c);
     if (g->codebook) {
       SideWork side(s, sw);
       ABCD_TRY((hipError_t)gemm(sw, D, K, B, opKM(w.U, D, D), opKM(d_logits, K, K), g->codebook, K, rs,
@@ -1267,7 +1298,7 @@ static int samp_fused_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* 
   const abcd_mlp_w& m = p->mlp[0];
   const abcd_mlp_g& mg = g->mlp[0];
   HeadBwdArgs a{};
-  a.B = B; a.Hm = Hm; a.D = D; a.K = K;
+  a.B = B; a.Hm = Hm; a.D = D; a.K = K; a.Kv = kvalid(c); a.rsD = rs_dim(c);
   a.it = 1.f / (mode == ABCD_SAMPLE_GUMBEL ? temperature : 1.f);
   a.dfeat = d_feats; a.dkl = d_kl; a.Y = w.Y; a.Q = w.Q; a.v = w.v; a.elog = w.elog; a.Z1 = w.Z1[0];
   a.C = p->codebook; a.W2 = m.w2;
@@ -1394,8 +1425,9 @@ extern "C" int abcd_sampler_backward(const abcd_sampler_cfg* c, const abcd_sampl
 // One wave per row (rows dealt round-robin over the waves); each wave keeps
 // its own column-sum row in LDS (no atomics, deterministic), summed over the
 // waves at the end.
+// rows of `ld` floats whose first K columns are the categories
 template <int KPL>
-__global__ __launch_bounds__(1024) void perplex_kernel(const float* logits, int B, int K, const float* psl,
+__global__ __launch_bounds__(1024) void perplex_kernel(const float* logits, int B, int ld, int K, const float* psl,
                                                        float* out) {
   extern __shared__ __attribute__((aligned(16))) float colsum_sh[];  // nw x K floats
   __shared__ double sh[32];
@@ -1414,7 +1446,7 @@ __global__ __launch_bounds__(1024) void perplex_kernel(const float* logits, int 
 #pragma unroll
       for (int u = 0; u < KPL; ++u) {
         const int k = lane + 64 * u;
-        v[rr][u] = (b0 + rr < B && k < K) ? logits[(long)(b0 + rr) * K + k] : -INFINITY;
+        v[rr][u] = (b0 + rr < B && k < K) ? logits[(long)(b0 + rr) * ld + k] : -INFINITY;
       }
 #pragma unroll
     for (int rr = 0; rr < PR; ++rr) {
@@ -1527,19 +1559,25 @@ extern "C" int abcd_shape_perplexity(const float* psl, int K, float* out, void* 
   return 0;
 }
 
-extern "C" int abcd_perplexities(const float* logits, int B, int K, const float* psl, float* out, void* stream) {
-  if (!logits || !psl || !out || B <= 0 || K <= 0) return ABCD_EINVAL;
+namespace abcd {
+int perplexities_ld(const float* logits, int B, int ld, int K, const float* psl, float* out, void* stream) {
+  if (!logits || !psl || !out || B <= 0 || K <= 0 || ld < K) return ABCD_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   // as many waves (<= 16) as per-wave column-sum rows fit in 64 KiB of LDS
   int nw = 16;
   while (nw > 1 && (size_t)nw * K * sizeof(float) > 65536) nw >>= 1;
   if ((size_t)nw * K * sizeof(float) > 160 * 1024) return ABCD_EINVAL;
   const size_t lds = (size_t)nw * K * sizeof(float);
-  if (K <= 64) perplex_kernel<1><<<1, 64 * nw, lds, s>>>(logits, B, K, psl, out);
-  else if (K <= 128) perplex_kernel<2><<<1, 64 * nw, lds, s>>>(logits, B, K, psl, out);
-  else if (K <= 256) perplex_kernel<4><<<1, 64 * nw, lds, s>>>(logits, B, K, psl, out);
-  else if (K <= 1024) perplex_kernel<16><<<1, 64 * nw, lds, s>>>(logits, B, K, psl, out);
+  if (K <= 64) perplex_kernel<1><<<1, 64 * nw, lds, s>>>(logits, B, ld, K, psl, out);
+  else if (K <= 128) perplex_kernel<2><<<1, 64 * nw, lds, s>>>(logits, B, ld, K, psl, out);
+  else if (K <= 256) perplex_kernel<4><<<1, 64 * nw, lds, s>>>(logits, B, ld, K, psl, out);
+  else if (K <= 1024) perplex_kernel<16><<<1, 64 * nw, lds, s>>>(logits, B, ld, K, psl, out);
   else return ABCD_EINVAL;
   ABCD_CHECK_LAUNCH();
   return 0;
+}
+}  // namespace abcd
+
+extern "C" int abcd_perplexities(const float* logits, int B, int K, const float* psl, float* out, void* stream) {
+  return abcd::perplexities_ld(logits, B, K, K, psl, out, stream);
 }

@@ -10,9 +10,9 @@ annotation columns, rows ordered category-major within each batch.
 
 How it runs here: every batch goes through the encoder and sampler forward
 kernels once (model.py:60-66, 581-590) and stays on the device; the softmax
-(or nothing, or the to_code_like MLP) is applied there, and the whole table
-is built at the end with numpy index arithmetic -- no per-batch DataFrame
-melt / merge / append cycle."""
+(or nothing, or the to_code_like MLP) is applied there, and the table is
+written batch by batch with numpy index arithmetic (no DataFrame melt /
+merge / append cycle), the previous batch's rows while the current one runs."""
 import argparse
 import os
 
@@ -60,27 +60,43 @@ class Encoder(learning.Learner):
         return out
 
     def encode_dataset(self, dataset, save_path, to_numpy=True, batch_size=1, output=None):
+        """Streams the table: each batch's device output is copied to pinned
+        host memory without blocking, and the PREVIOUS batch's rows are written
+        while the current one computes, so host and device memory stay bounded
+        by two batches whatever the dataset size (the reference also writes
+        per batch, encode.py:38-55)."""
         output = output or OUTPUT
         var_name, value_name = COLUMNS[output]
         rename_existing_file(save_path)
-        blocks, ixs = [], []
-        for packed, _, _, ix in data_utils.DataLoader(dataset, batch_size=batch_size):
-            blocks.append(self._device_output(packed, output))
-            ixs.append(np.asarray(ix, dtype=np.int64))
         ann = None
         if "label" in dataset.df_annotation.columns:
             ann = dataset.df_annotation.drop(columns=["onset_ix", "offset_ix", "length"])
-        header = True
-        for vals, ix in zip(blocks, ixs):
-            v = vals.cpu().numpy()
+        state = {"header": True}
+
+        def write(host, event, ix):
+            event.synchronize()
+            v = host.numpy()
             n, k = v.shape
             table = pd.DataFrame({"data_ix": np.tile(ix, k), var_name: np.repeat(np.arange(k), n),
                                   value_name: v.T.reshape(-1)})
             if ann is not None:
                 extra = ann.reindex(table["data_ix"].to_numpy()).reset_index(drop=True)
                 table = pd.concat([table, extra], axis=1)
-            table.to_csv(save_path, index=False, mode="w" if header else "a", header=header)
-            header = False
+            table.to_csv(save_path, index=False, mode="w" if state["header"] else "a", header=state["header"])
+            state["header"] = False
+
+        pending = None
+        for packed, _, _, ix in data_utils.DataLoader(dataset, batch_size=batch_size):
+            vals = self._device_output(packed, output)
+            host = torch.empty(vals.shape, dtype=vals.dtype, pin_memory=True)
+            host.copy_(vals, non_blocking=True)
+            event = torch.cuda.Event()
+            event.record()
+            if pending is not None:
+                write(*pending)
+            pending = (host, event, np.asarray(ix, dtype=np.int64))
+        if pending is not None:
+            write(*pending)
 
 
 def rename_existing_file(filepath):

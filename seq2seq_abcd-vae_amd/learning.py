@@ -61,6 +61,8 @@ def _check_device(device):
 
 
 class Learner(object):
+    status_every = 16  # steps between the non-blocking STATUS reads (engine.StatusWatch)
+
     def __init__(self, input_size, encoder_rnn_hidden_size, decoder_rnn_hidden_size, mlp_hidden_size,
                  num_feature_categories, feature_dim, save_dir, encoder_rnn_type="LSTM", decoder_rnn_type="LSTM",
                  encoder_rnn_layers=1, bidirectional_encoder=True, bidirectional_decoder=False,
@@ -75,6 +77,12 @@ class Learner(object):
         self.device = torch.device(device)
         logger.info("Device: {device}".format(device=device))
         logger.info("HIP library: {v}".format(v=model.N.lib().abcd_version().decode()))
+        if noise_mode == "reference" and self.world > 1:
+            # the reference draws from ONE global CPU generator for the whole
+            # batch; seeded alike, every rank would draw the same noise for its
+            # own shard, which no single-device run draws
+            raise ValueError("--noise reference reproduces a single-device reference run; "
+                             "use --noise philox (per-rank keys) with data parallelism")
         noise.set_mode(noise_mode)
         logger.info("Noise source: {m}".format(m=noise_mode))
         self.step = None
@@ -178,6 +186,7 @@ class Learner(object):
         num_strings = len(dataloader.dataset)
         records = []
         group = self.optimizer.param_groups[0]
+        watch = engine.StatusWatch(self.device, every=self.status_every)
         for batch_ix, (packed_input, is_offset, speaker, _) in enumerate(dataloader, 1):
             # loss / batch_sizes[0] of the GLOBAL batch (learning.py:156) on every rank
             b_global = int(packed_input.batch_sizes[0])
@@ -190,8 +199,10 @@ class Learner(object):
                                     momentum=group["momentum"], clip=self.gradient_clip, loss_batch=b_global)
             self._momentum_views()
             records.append(sc.clone())
+            watch.update(records)
             if not is_pretraining and hasattr(self.feature_sampler, "increment_iter_counts"):
                 self.feature_sampler.increment_iter_counts()
+        watch.finish()
         recs = torch.stack(records)
         if self.world > 1:
             dist.all_reduce(recs, op=dist.ReduceOp.SUM)
@@ -268,12 +279,17 @@ class Learner(object):
         datasets return raw samples (--gpu_featurize)."""
         # single device: RandomSampler draws from the global CPU generator as in
         # the reference (bit-exact batch order).  Data parallel: a generator of
-        # its own, seeded alike on every rank, so the host-side noise draws of
-        # --noise reference (shard-sized, so rank-dependent) cannot make the
-        # ranks shuffle -- and shard -- different global batches
+        # its own, seeded alike on every rank, so every rank shuffles -- and
+        # shards -- the same global batches whatever else uses the CPU RNG
+        # The generator's seed and state travel in the checkpoint, so a resumed
+        # run continues the shuffle sequence instead of replaying epoch 1's.
         gen = None
         if self.world > 1:
-            gen = torch.Generator().manual_seed(getattr(self, "seed", 1111))
+            gen = torch.Generator().manual_seed(self.seed)
+            state = self.checkpoint.get("dp_shuffle_state") if self.retrieval else None
+            if state is not None:
+                gen.set_state(state)
+        self._shuffle_gen = gen
         train_dataloader = data_utils.DataLoader(train_dataset, batch_size=batch_size_train, shuffle=True,
                                                  featurizer=featurizer, generator=gen)
         valid_dataloader = data_utils.DataLoader(valid_dataset, batch_size=batch_size_valid, featurizer=featurizer)
@@ -350,7 +366,10 @@ class Learner(object):
             "gradient_clip": self.gradient_clip,
             "random_state": torch.get_rng_state(),
             "abcd_noise_state": nstate,
+            "seed": self.seed,
         }
+        if getattr(self, "_shuffle_gen", None) is not None:
+            checkpoint["dp_shuffle_state"] = self._shuffle_gen.get_state()
         if torch.cuda.is_available():
             checkpoint["random_state_cuda"] = torch.cuda.get_rng_state_all()
         torch.save(checkpoint, os.path.join(self.save_dir, "checkpoint.pt"))
@@ -373,6 +392,8 @@ class Learner(object):
             self.rank, self.world = parallel.world()
         self._finish_modules()
         self.gradient_clip = self.checkpoint["gradient_clip"]
+        # the run's seed (reference checkpoints carry none: the CLI default)
+        self.seed = int(self.checkpoint.get("seed", 1111))
         try:
             torch.set_rng_state(self.checkpoint["random_state"])
         except RuntimeError:

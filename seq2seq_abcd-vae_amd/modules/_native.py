@@ -50,7 +50,7 @@ class EncoderParams(ctypes.Structure):
 
 class SamplerCfg(ctypes.Structure):
     _fields_ = [("input_size", c_int), ("mlp_hidden", c_int), ("num_categories", c_int),
-                ("feature_dim", c_int), ("plain", c_int)]
+                ("feature_dim", c_int), ("plain", c_int), ("valid_categories", c_int), ("valid_feature_dim", c_int)]
 
 
 class SamplerParams(ctypes.Structure):
@@ -147,6 +147,10 @@ _SIGS = {
                              c_size_t, c_void_p]),
     "abcd_linear": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_void_p,
                             c_long, c_void_p, c_size_t, c_void_p]),
+    "abcd_linear_backward_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "abcd_linear_backward": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long,
+                                     c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
+                                     c_size_t, c_void_p]),
     "abcd_timing_enable": (None, [c_int]),
     "abcd_timing_reset": (None, []),
     "abcd_timing_read": (c_int, [ctypes.POINTER(c_double)]),

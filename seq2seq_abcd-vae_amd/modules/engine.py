@@ -18,6 +18,7 @@ import torch
 
 from . import _native as N
 from . import noise as _noise
+from . import padding as _pad
 from .model import ABCDSampler
 
 # layout of the device scalar vector returned by FusedStep.step; STATUS is the
@@ -68,6 +69,19 @@ class FusedStep:
         self.device = device
         params = itertools.chain(encoder.parameters(), sampler.parameters(), decoder.parameters())
         self.flat = FlatParams(params, device)
+        # a size that is not a multiple of 16: the kernels run the zero-padded
+        # twin model (padding.py); its parameters are embedded from self.flat
+        # before every pass and its gradients gathered into self.flat.grad
+        self.pad = None
+        self.kmods = (encoder, sampler, decoder)  # the modules whose shapes the kernels run
+        self.kflat = self.flat
+        if _pad.PadPlan.needed(encoder, sampler, decoder):
+            self.pad = _pad.PadPlan(encoder, sampler, decoder)
+            self.kmods = self.pad.twins
+            self.kflat = FlatParams(itertools.chain(*(m.parameters() for m in self.kmods)), device)
+            self.kflat.flat.zero_()
+            self.pad_index = self.pad.index.to(device)
+            self.enc_cols = self.pad.dims[0].out_cols.to(device)
         self.momentum_buf = None
         self.momentum_init = True
         self._ws = {}
@@ -79,7 +93,7 @@ class FusedStep:
 
     # ------------------------------------------------------------------ setup
     def _build_structs(self):
-        enc, samp, dec, fp = self.encoder, self.sampler, self.decoder, self.flat
+        (enc, samp, dec), fp = self.kmods, self.kflat
         self.enc_cfg = enc._cfg()
         self.enc_p = enc._params()
         dirs = 2 if enc.rnn.bidirectional else 1
@@ -104,6 +118,8 @@ class FusedStep:
     def refresh(self):
         """Call after load_state_dict / .to(): re-bind views and pointer tables."""
         self.flat.rebind()
+        if self.pad is not None:
+            self.kflat.rebind()
         self._build_structs()
 
     def _workspace(self, name, nbytes):
@@ -130,6 +146,10 @@ class FusedStep:
         GLOBAL batch size, so its loss is (em_r + off_r + kl_r) / B_global and
         the SUM of the ranks' gradients (and losses) is exactly the reference's
         global-batch value (parallel.py)."""
+        if self.allreduce is not None and loss_batch is None:
+            # a data-parallel rank normalising by its own B would scale the
+            # summed gradient (and loss) by the world size
+            raise ValueError("FusedStep with an all-reduce attached needs loss_batch = the GLOBAL batch size")
         L_ = N.lib()
         st = N.stream()
         data = data.contiguous()
@@ -139,27 +159,35 @@ class FusedStep:
         Bn = int(loss_batch) if loss_batch is not None else B
         dev = self.device
         sc = self.scalars
+        kenc, ksamp, kdec = self.kmods
+        if self.pad is not None:  # this pass's weights into the padded twin (padding positions stay 0)
+            self.kflat.flat.index_copy_(0, self.pad_index, self.flat.flat)
+            for real, twin in zip((self.encoder, self.sampler, self.decoder), self.kmods):
+                twin.train(real.training)
         ws_e = self._workspace("enc", L_.abcd_encoder_workspace_bytes(self.enc_cfg, T, L, B))
         ws_s = self._workspace("samp", L_.abcd_sampler_workspace_bytes(self.samp_cfg, B))
-        dcfg = self.decoder._dcfg(None if train else 1)
+        dcfg = kdec._dcfg(None if train else 1)
         ws_d = self._workspace("dec", L_.abcd_decoder_workspace_bytes(dcfg, T, L, B))
         h = torch.empty(B, self.E, device=dev)
         # inter-layer dropout noise: the step's first RNG draw, as in the reference
         enc_noise = self.encoder.draw_dropout_noise(L, dev) if train else None
+        if enc_noise is not None and self.pad is not None:
+            de = self.pad.dims[0]
+            enc_noise = [_pad.pad_col_blocks(n, de.dirs, de.H, de.Hp) for n in enc_noise]
         N.check(L_.abcd_encoder_forward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(h),
                                                 N.ptr(ws_e), ws_e.numel(), st), "encoder forward")
-        W = self.sampler._logit_width()
+        W = ksamp._logit_width()
         logits = torch.empty(B, W, device=dev)
         feats = torch.empty(B, self.Dfeat, device=dev)
-        self.last_hidden, self.feats = h, feats  # kept for inspection (encode paths, parity tests)
+        self._inspect(h, feats)  # kept for inspection (encode paths, parity tests)
         if self.plain:
             mode, tau = 0, 1.0
-            nt, seed, off = _noise.normal(B, self.Dfeat, dev)
+            nt, seed, off = _noise.normal(B, self.sampler._feat_dim(), dev, width=self.Dfeat)
         elif is_pretraining:
             mode, tau, nt, seed, off = N.SAMPLE_SOFTMAX, 1.0, None, 0, 0
         else:
             mode, tau = N.SAMPLE_GUMBEL, float(self.sampler.temperature)
-            nt, seed, off = _noise.gumbel(B, W, dev)
+            nt, seed, off = _noise.gumbel(B, self.sampler._logit_width(), dev, width=W)
         # feature_sampler(h) -> .sample(logits) -> .kl_divergence(logits, N)
         # (learning.py:149-153): ABCD = the split-K MLP GEMM + one row-tiled
         # sampler-head kernel (logits, Gumbel-softmax, y C^T, KL) per step
@@ -168,11 +196,11 @@ class FusedStep:
                                               N.ptr(sc[KL:KL + 1]),
                                               None if self.plain else N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 2]),
                                               N.ptr(ws_s), ws_s.numel(), st), "sampler")
-        F = self.decoder.rnn_cell.cell.input_size
+        F = kdec.rnn_cell.cell.input_size
         pdrop = self.decoder._input_dropout_p() if train else 0.0
         eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
         spk = None
-        if self.decoder.embed_speaker is not None:
+        if kdec.embed_speaker is not None:
             spk = speakers.to(dev, torch.int64).contiguous()
         gt_off = is_offset.contiguous()
         N.check(L_.abcd_decoder_forward_split(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
@@ -183,7 +211,7 @@ class FusedStep:
                 "total loss")
         if not train:
             N.check(L_.abcd_step_status(N.ptr(sc[STATUS:STATUS + 1]), st), "step status")
-            return sc, logits
+            return sc, self._real_logits(logits)
         inv = self._inv_b(Bn)
         d_feats = torch.empty(B, self.Dfeat, device=dev)
         # the decoder's weight-gradient reductions run on a side stream beside
@@ -203,7 +231,35 @@ class FusedStep:
                                                  self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
                                                  N.c_void_p(side.cuda_stream)), "encoder backward")
         torch.cuda.current_stream(dev).wait_stream(side)
-        return sc, logits
+        if self.pad is not None:  # the real positions of the twin's gradients
+            torch.index_select(self.kflat.grad, 0, self.pad_index, out=self.flat.grad)
+        return sc, self._real_logits(logits)
+
+    def _real_logits(self, logits):
+        """The real model's logits (ABCD: B x K; plain: [mean | log_var], B x 2f)
+        from the kernels' (padded) ones."""
+        if self.pad is None:
+            return logits
+        d = self.pad.dims[1]
+        if not self.plain:
+            return logits[:, :d.K]
+        return torch.cat([logits[:, :d.D], logits[:, d.Dp:d.Dp + d.D]], 1)
+
+    def _inspect(self, h, feats):
+        """last_hidden / feats of the real model (views or gathers of the padded ones)."""
+        if self.pad is None:
+            self.last_hidden, self.feats = h, feats
+            return
+        self._padded_hidden, self._padded_feats = h, feats
+        self.__dict__.pop("last_hidden", None)
+        self.__dict__.pop("feats", None)
+
+    def __getattr__(self, name):  # lazily gathered real views of the padded inspection tensors
+        if name == "last_hidden" and "_padded_hidden" in self.__dict__:
+            return self._padded_hidden.index_select(1, self.enc_cols)
+        if name == "feats" and "_padded_feats" in self.__dict__:
+            return self._padded_feats[:, :self.pad.dims[1].D]
+        raise AttributeError(name)
 
     def _side_stream(self):
         s = getattr(self, "_side", None)
@@ -244,7 +300,7 @@ class FusedStep:
         self.optimizer_step(lr, momentum, clip)
         if not self.plain:  # learning.py:171-178: cluster / batch perplexities came with the sampler head;
             # the shape perplexity reads posterior_shape_logits AFTER the SGD step
-            N.check(N.lib().abcd_shape_perplexity(N.ptr(self.sampler.posterior_shape_logits), logits.shape[1],
+            N.check(N.lib().abcd_shape_perplexity(N.ptr(self.sampler.posterior_shape_logits), self.sampler.num_categories,
                                                   N.ptr(sc[PPL_SHAPE:PPL_SHAPE + 1]), N.stream()), "perplexities")
         N.check(N.lib().abcd_step_status(N.ptr(sc[STATUS:STATUS + 1]), N.stream()), "step status")
         return sc
@@ -257,6 +313,51 @@ def check_status(records, where="training step"):
     bad = r.nonzero()
     if bad.numel():
         N.raise_on_status(float(r[bad[0, 0]]), f"{where} {int(bad[0, 0]) + 1}")
+
+
+class StatusWatch:
+    """Bounded-latency check of the steps' STATUS slots inside an epoch.
+
+    Every ``every`` steps the maximum STATUS of the records since the last
+    check is reduced on the device and copied without blocking into pinned
+    host memory; the copy of the PREVIOUS window is read (its event has long
+    completed, so the host does not stall the stream) and a non-zero value
+    raises ``PersistTimeout``.  A timed-out persistent kernel therefore stops
+    training within two windows instead of at the end of the epoch, while
+    the epoch loop still never synchronises with the device on the fast path.
+    (The persistent kernels' own waits give up at once after a timeout, see
+    ``spin_abandoned`` in abcd_persist.hip, so the steps in between are cheap.)
+    """
+
+    def __init__(self, device, every=16, where="training batch"):
+        self.every, self.where = int(every), where
+        self.host = torch.zeros(1, pin_memory=torch.cuda.is_available())
+        self.event = None
+        self.first = 0   # first record of the window in flight
+        self.done = 0    # records covered by the window in flight
+
+    def _read(self):
+        if self.event is not None:
+            self.event.synchronize()
+            if float(self.host[0]) != 0.0:
+                N.raise_on_status(float(self.host[0]),
+                                  f"{self.where}s {self.first + 1}-{self.done}")
+            self.event = None
+
+    def update(self, records):
+        """records: the list of per-step scalar vectors of this epoch so far."""
+        n = len(records)
+        if n - self.done < self.every:
+            return
+        self._read()
+        window = torch.stack(records[self.done:n])[:, STATUS].amax().reshape(1)
+        self.host.copy_(window, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record()
+        self.first, self.done = self.done, n
+
+    def finish(self):
+        self._read()
 
 
 def _packed(data, batch_sizes, F):

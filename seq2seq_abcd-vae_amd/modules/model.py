@@ -20,6 +20,18 @@ import torch
 from . import _native as N
 from . import noise as _noise
 from . import ops
+from . import padding as _pad
+
+
+def _module_pad(module, kind):
+    """The module's padded twin (padding.ModulePad) when one of its sizes is
+    not a multiple of 16, else None; built once per module."""
+    mp = module.__dict__.get("_abcd_mpad", False)
+    if mp is False:
+        dims = {"encoder": _pad.encoder_dims, "sampler": _pad.sampler_dims, "decoder": _pad.decoder_dims}[kind]
+        mp = _pad.ModulePad(kind, module) if dims(module).active else None
+        module.__dict__["_abcd_mpad"] = mp
+    return mp
 
 
 # ----------------------------------------------------------------------------
@@ -128,26 +140,16 @@ class MLP(torch.nn.Module):
                 self.whole_network[2].bias)
 
     def forward(self, batched_input):
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("standalone MLP forward is inference-only on the HIP path; its training "
-                                      "backward is fused into the sampler/decoder kernels")
+        """Linear -> Tanh -> Linear on the HIP GEMMs (``abcd::linear``), with
+        autograd (``abcd::linear_bwd``): the standalone MLP trains like the
+        reference's (model.py:332-334).  Inside the training step the MLPs run
+        fused into the sampler / decoder kernels instead."""
         x = _f32c(batched_input)
         N.require_gpu(x)
         shp = x.shape
-        x2 = x.reshape(-1, shp[-1])
-        M = x2.shape[0]
-        w1, b1, w2, b2 = [t.detach() for t in self.weights()]
-        hid = torch.empty(M, self.hidden_size, device=x.device)
-        out = torch.empty(M, self.output_size, device=x.device)
-        Kp = (max(self.input_size, self.hidden_size) + 15) // 16 * 16
-        ws = N.workspace((M + max(self.hidden_size, self.output_size)) * Kp * 4 + (1 << 22), x.device)
-        L = N.lib()
-        N.check(L.abcd_linear(M, self.hidden_size, self.input_size, N.ptr(x2), x2.shape[1], N.ptr(w1), w1.shape[1],
-                              N.ptr(b1), 1, N.ptr(hid), self.hidden_size, N.ptr(ws), ws.numel(), N.stream()),
-                "MLP layer 1")
-        N.check(L.abcd_linear(M, self.output_size, self.hidden_size, N.ptr(hid), self.hidden_size, N.ptr(w2),
-                              w2.shape[1], N.ptr(b2), 0, N.ptr(out), self.output_size, N.ptr(ws), ws.numel(),
-                              N.stream()), "MLP layer 2")
+        w1, b1, w2, b2 = self.weights()
+        hid = ops.linear(x.reshape(-1, shp[-1]), w1, b1, 1)
+        out = ops.linear(hid, w2, b2, 0)
         return out.reshape(*shp[:-1], self.output_size)
 
 
@@ -178,8 +180,33 @@ class RNN_Cell(torch.nn.Module):
         self.cell = getattr(torch.nn, model_type + "Cell")(input_size, hidden_size)
 
     def forward(self, batched_input, init_hidden=None):
-        raise NotImplementedError("RNN_Cell is stepped inside the fused decoder kernels "
-                                  "(RNN_Variational_Decoder.forward)")
+        """One standalone cell step, model.py:297-300: ``cell(drop(x), init_hidden)``.
+
+        The decoder steps its cell inside the fused persistent kernels; this
+        is the reference module's own API for other callers.  The two
+        projections x W_ih^T + b_ih and h W_hh^T + b_hh run on the HIP GEMMs
+        (``abcd::linear``, differentiable); the gate nonlinearities of
+        nn.LSTMCell / nn.GRUCell (PyTorch's gate order i, f, g, o / r, z, n)
+        are elementwise torch ops on the device."""
+        x = _f32c(self.drop(batched_input))
+        N.require_gpu(x)
+        cell = self.cell
+        B, H = x.shape[0], cell.hidden_size
+        if init_hidden is None:
+            z = x.new_zeros(B, H)
+            init_hidden = (z, z) if self.mode == "LSTM" else z
+        h = init_hidden[0] if self.mode == "LSTM" else init_hidden
+        gi = ops.linear(x, cell.weight_ih, cell.bias_ih, 0)
+        gh = ops.linear(_f32c(h), cell.weight_hh, cell.bias_hh, 0)
+        if self.mode == "LSTM":
+            i, f, g, o = (gi + gh).chunk(4, 1)
+            c = torch.sigmoid(f) * init_hidden[1] + torch.sigmoid(i) * torch.tanh(g)
+            return torch.sigmoid(o) * torch.tanh(c), c
+        ir, iz, inn = gi.chunk(3, 1)
+        hr, hz, hn = gh.chunk(3, 1)
+        r, zg = torch.sigmoid(ir + hr), torch.sigmoid(iz + hz)
+        n = torch.tanh(inn + r * hn)
+        return (1 - zg) * n + zg * h
 
 
 # ----------------------------------------------------------------------------
@@ -240,8 +267,15 @@ class RNN_Variational_Encoder(torch.nn.Module):
         data = _f32c(packed_input.data)
         N.require_gpu(data)
         noise = self.draw_dropout_noise(int(data.shape[0]), data.device)
-        out, _ws = ops.encoder(data, packed_input.batch_sizes, self._weights(), noise or [], self._cfg_list())
-        return out
+        mp = _module_pad(self, "encoder")
+        if mp is None:
+            out, _ws = ops.encoder(data, packed_input.batch_sizes, self._weights(), noise or [], self._cfg_list())
+            return out
+        # hidden size not a multiple of 16: the zero-padded twin (padding.py), real columns out
+        d = mp.dims
+        noise = [_pad.pad_col_blocks(n, d.dirs, d.H, d.Hp) for n in (noise or [])]
+        out, _ws = ops.encoder(data, packed_input.batch_sizes, mp.weights(self._weights()), noise, mp.cfg)
+        return out.index_select(1, d.out_cols.to(out.device))
 
     def pack_init_parameters(self):
         return {"input_size": self.rnn.input_size, "rnn_hidden_size": self.rnn.hidden_size,
@@ -295,7 +329,15 @@ class _SamplerBase(torch.nn.Module):
 
     def _cfg_list(self):
         c = self._scfg()
-        return [c.input_size, c.mlp_hidden, c.num_categories, c.feature_dim, c.plain]
+        return [c.input_size, c.mlp_hidden, c.num_categories, c.feature_dim, c.plain, c.valid_categories,
+                c.valid_feature_dim]
+
+    def _valid(self, c):
+        """A padded twin (padding.sampler_twin) carries its model's real (K, D)."""
+        vs = self.__dict__.get("valid_sizes")
+        if vs is not None:
+            c.valid_categories, c.valid_feature_dim = (int(vs[0]), int(vs[1])) if not c.plain else (0, 0)
+        return c
 
     def _mlp_weights(self):
         return [t for m in self._mlps() for t in m.weights()]
@@ -337,7 +379,7 @@ class ABCDSampler(_SamplerBase):
         c = N.SamplerCfg()
         c.input_size, c.mlp_hidden = self.to_code_like.input_size, self.to_code_like.hidden_size
         c.num_categories, c.feature_dim, c.plain = self.num_categories, self.to_code_like.output_size, 0
-        return c
+        return self._valid(c)
 
     def _logit_width(self):
         return self.num_categories
@@ -347,25 +389,41 @@ class ABCDSampler(_SamplerBase):
 
     # -- reference API --
     def forward(self, x):
-        return ops.sampler(_f32c(x), self._mlp_weights(), self.codebook, self._cfg_list())[0]
+        mp = _module_pad(self, "sampler")
+        if mp is None:
+            return ops.sampler(_f32c(x), self._mlp_weights(), self.codebook, self._cfg_list())[0]
+        d = mp.dims  # a size not a multiple of 16: the zero-padded twin (padding.py)
+        lp = ops.sampler(_pad.pad_cols(_f32c(x), d.Ep), mp.weights(self._mlp_weights()), mp.weight(self.codebook),
+                         mp.cfg)[0]
+        return lp[:, :d.K]
 
     def sample(self, logits, no_sample=False):
         logits = _f32c(logits)
         N.require_gpu(logits)
         B, K = logits.shape
+        mp = _module_pad(self, "sampler")
+        width = K if mp is None else mp.dims.Kp
         if no_sample:
             mode, tau, nt, seed, off = N.SAMPLE_SOFTMAX, 1.0, None, 0, 0
         else:
             mode, tau = N.SAMPLE_GUMBEL, float(self.temperature)
-            nt, seed, off = _noise.gumbel(B, K, logits.device)
-        return ops.sampler_sample(logits, self.codebook, self._cfg_list(), mode, tau, nt, ops._i64(seed),
-                                  ops._i64(off))[0]
+            nt, seed, off = _noise.gumbel(B, K, logits.device, width=width)
+        if mp is None:
+            return ops.sampler_sample(logits, self.codebook, self._cfg_list(), mode, tau, nt, ops._i64(seed),
+                                      ops._i64(off))[0]
+        feats = ops.sampler_sample(_pad.pad_cols(logits, width), mp.weight(self.codebook), mp.cfg, mode, tau, nt,
+                                   ops._i64(seed), ops._i64(off))[0]
+        return feats[:, :mp.dims.D]
 
     def kl_divergence(self, logits, entire_data_size):
         logits = _f32c(logits)
         N.require_gpu(logits)
-        return ops.sampler_kl(logits, self.posterior_shape_logits, self._cfg_list(), self._prior_value(),
-                              float(entire_data_size))[0]
+        mp = _module_pad(self, "sampler")
+        if mp is None:
+            return ops.sampler_kl(logits, self.posterior_shape_logits, self._cfg_list(), self._prior_value(),
+                                  float(entire_data_size))[0]
+        return ops.sampler_kl(_pad.pad_cols(logits, mp.dims.Kp), mp.weight(self.posterior_shape_logits), mp.cfg,
+                              self._prior_value(), float(entire_data_size))[0]
 
     def log_pmf(self, targets, logits):
         return torch.nn.functional.cross_entropy(logits, targets, reduction="sum")
@@ -411,7 +469,7 @@ class Sampler(_SamplerBase):
         c = N.SamplerCfg()
         c.input_size, c.mlp_hidden = self.to_parameters.input_size, self.to_parameters.hidden_size
         c.num_categories, c.feature_dim, c.plain = 16, self.to_parameters.output_size, 1
-        return c
+        return self._valid(c)
 
     def _logit_width(self):
         return 2 * self.to_parameters.output_size
@@ -421,8 +479,15 @@ class Sampler(_SamplerBase):
 
     def forward(self, parameter_seed):
         f = self.to_parameters.output_size
-        mv = ops.sampler(_f32c(parameter_seed), self._mlp_weights(), None, self._cfg_list())[0]
-        mu, lv = mv[:, :f], mv[:, f:]
+        mp = _module_pad(self, "sampler")
+        if mp is None:
+            mv = ops.sampler(_f32c(parameter_seed), self._mlp_weights(), None, self._cfg_list())[0]
+            mu, lv = mv[:, :f], mv[:, f:]
+        else:  # the zero-padded twin: mv = [mu | 0 | log_var | 0], padding mu = log_var = 0
+            fp = mp.dims.Dp
+            mv = ops.sampler(_pad.pad_cols(_f32c(parameter_seed), mp.dims.Ep), mp.weights(self._mlp_weights()), None,
+                             mp.cfg)[0]
+            mu, lv = mv[:, :f], mv[:, fp:fp + f]
         mu._abcd_mv = mv
         return [mu, lv]
 
@@ -432,15 +497,19 @@ class Sampler(_SamplerBase):
         if mv is None:  # parameters not produced by this module's forward: reference torch formula
             return self._sampler(*parameters)
         B, f = mu.shape
-        nt, seed, off = _noise.normal(B, f, mu.device)
-        return ops.sampler_sample(mv, None, self._cfg_list(), 0, 1.0, nt, ops._i64(seed), ops._i64(off))[0]
+        mp = _module_pad(self, "sampler")
+        cfg = self._cfg_list() if mp is None else mp.cfg
+        # padding columns draw zero noise, so their samples are exactly 0 as well
+        nt, seed, off = _noise.normal(B, f, mu.device, width=mv.shape[1] // 2)
+        return ops.sampler_sample(mv, None, cfg, 0, 1.0, nt, ops._i64(seed), ops._i64(off))[0][:, :f]
 
     def kl_divergence(self, parameters):
         mu, lv = parameters
         mv = getattr(mu, "_abcd_mv", None)
         if mv is None:
             return self._kl_divergence(*parameters)
-        return ops.sampler_kl(mv, None, self._cfg_list(), 1.0, 1.0)[0]
+        mp = _module_pad(self, "sampler")
+        return ops.sampler_kl(mv, None, self._cfg_list() if mp is None else mp.cfg, 1.0, 1.0)[0]
 
     def log_pdf(self, samples, parameters):
         return self._log_pdf(samples, *parameters)
@@ -556,9 +625,14 @@ class RNN_Variational_Decoder(torch.nn.Module):
         gt = None if ground_truth_out is None else _f32c(ground_truth_out)
         gt_off = None if ground_truth_offset is None else _f32c(ground_truth_offset)
         spk = speaker if self.embed_speaker is not None else None
-        em, off, flat, mu, lv, offl, _ws = ops.decoder(_f32c(features), batch_sizes, spk, gt, gt_off, eps,
-                                                       ops._i64(seed), ops._i64(offset), xmask, self._param_list(),
-                                                       self._cfg_list())
+        mp = _module_pad(self, "decoder")
+        features = _f32c(features)
+        params, cfg = self._param_list(), self._cfg_list()
+        if mp is not None:  # a size not a multiple of 16: the zero-padded twin (padding.py)
+            mp.twin.train(self.training)
+            features, params, cfg = _pad.pad_cols(features, mp.dims.Ddp), mp.weights(params), mp.twin._cfg_list()
+        em, off, flat, mu, lv, offl, _ws = ops.decoder(features, batch_sizes, spk, gt, gt_off, eps,
+                                                       ops._i64(seed), ops._i64(offset), xmask, params, cfg)
         return (em if gt is not None else None), (off if gt_off is not None else None), flat, (mu, lv), offl
 
     def _length_to_batch_sizes(self, lengths):

@@ -88,25 +88,38 @@ def philox(n):
     return _state["seed"], off
 
 
-def gumbel(B, K, device):
-    """(noise tensor or None, seed, offset) for a B x K Gumbel draw."""
+def gumbel(B, K, device, width=None):
+    """(noise tensor or None, seed, offset) for a B x K Gumbel draw.  width:
+    the row stride the kernel reads Philox counters with (a zero-padded model,
+    modules/padding.py): host noise is returned zero-padded to it, the Philox
+    reservation covers B x width counters."""
+    width = K if width is None else int(width)
     if _replay:
-        return _pop((B, K), device)
+        t, s, o = _pop((B, K), device)
+        return _widen(t, width), s, o
     if _state["mode"] == "reference":
         g = -torch.empty(B, K).exponential_().log()
-        return g.to(device, non_blocking=True), 0, 0
-    s, o = philox(B * K)
+        return _widen(g.to(device, non_blocking=True), width), 0, 0
+    s, o = philox(B * width)
     return None, s, o
 
 
-def normal(B, f, device):
-    """(noise tensor or None, seed, offset) for a B x f standard normal draw."""
+def normal(B, f, device, width=None):
+    """(noise tensor or None, seed, offset) for a B x f standard normal draw (width: as gumbel)."""
+    width = f if width is None else int(width)
     if _replay:
-        return _pop((B, f), device)
+        t, s, o = _pop((B, f), device)
+        return _widen(t, width), s, o
     if _state["mode"] == "reference":
-        return torch.randn(B, f).to(device, non_blocking=True), 0, 0
-    s, o = philox(B * f)
+        return _widen(torch.randn(B, f).to(device, non_blocking=True), width), 0, 0
+    s, o = philox(B * width)
     return None, s, o
+
+
+def _widen(t, width):
+    if t.shape[-1] == width:
+        return t
+    return torch.nn.functional.pad(t, (0, width - t.shape[-1]))
 
 
 def decoder_eps(batch_sizes, F, device):

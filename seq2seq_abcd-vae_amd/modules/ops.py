@@ -19,6 +19,8 @@ operator                   replaces (reference)                            C ent
 ``abcd::sampler_kl_bwd``                                                   ``abcd_sampler_kl_backward``
 ``abcd::decoder``          ``RNN_Variational_Decoder.forward`` model.py:147 ``abcd_decoder_forward_dropout``
 ``abcd::decoder_bwd``      its backward (emission + offset losses)         ``abcd_decoder_backward_dropout``
+``abcd::linear``           ``MLP`` layers (Linear [+ Tanh]) model.py:316   ``abcd_linear``
+``abcd::linear_bwd``       their backward                                  ``abcd_linear_backward``
 =========================  ==============================================  =========================================
 
 Operators take tensors, ints and floats only (no module objects): the
@@ -157,8 +159,11 @@ encoder.register_autograd(_encoder_backward, setup_context=_encoder_setup)
 # samplers (ABCD: cfg[4] == 0; plain Gaussian: cfg[4] == 1)
 # ----------------------------------------------------------------------------
 def _samp_cfg(cfg):
+    """cfg: [input_size, mlp_hidden, num_categories, feature_dim, plain(, valid_categories, valid_feature_dim)]"""
     c = N.SamplerCfg()
-    c.input_size, c.mlp_hidden, c.num_categories, c.feature_dim, c.plain = (int(v) for v in cfg)
+    v = [int(x) for x in cfg] + [0] * (7 - len(cfg))
+    (c.input_size, c.mlp_hidden, c.num_categories, c.feature_dim, c.plain, c.valid_categories,
+     c.valid_feature_dim) = v
     return c
 
 
@@ -459,8 +464,74 @@ def _decoder_backward(ctx, grads):
 decoder.register_autograd(_decoder_backward, setup_context=_decoder_setup)
 
 
+# ----------------------------------------------------------------------------
+# nn.Linear (+ Tanh): the standalone MLP (model.py:316-334) outside the step
+# ----------------------------------------------------------------------------
+def _linear_ws(M, N, K, device, backward=False):
+    if backward:
+        return N.workspace(N.lib().abcd_linear_backward_workspace_bytes(M, N, K), device)
+    Kp = (max(K, N) + 15) // 16 * 16
+    return N.workspace((M + N) * Kp * 4 + (1 << 22), device)
+
+
+@torch.library.custom_op("abcd::linear", mutates_args=())
+def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor], act: int) -> Tensor:
+    """y = act(x W^T + b), act 0 = identity, 1 = tanh; x M x K, W N x K."""
+    N.require_gpu(x)
+    x = x.contiguous()
+    weight = weight.contiguous()
+    M, K = x.shape
+    Nn = weight.shape[0]
+    y = torch.empty(M, Nn, device=x.device)
+    ws = _linear_ws(M, Nn, K, x.device)
+    N.check(N.lib().abcd_linear(M, Nn, K, N.ptr(x), K, N.ptr(weight), K, N.ptr(None if bias is None else bias.contiguous()),
+                                int(act), N.ptr(y), Nn, N.ptr(ws), ws.numel(), N.stream()), "linear")
+    return y
+
+
+@linear.register_fake
+def _(x, weight, bias, act):
+    return x.new_empty(x.shape[0], weight.shape[0])
+
+
+@torch.library.custom_op("abcd::linear_bwd", mutates_args=())
+def linear_bwd(x: Tensor, weight: Tensor, y: Tensor, dy: Tensor, act: int, need_bias: bool) -> List[Tensor]:
+    """-> [dx, dW, db (empty when need_bias is false)]"""
+    x, weight, y, dy = x.contiguous(), weight.contiguous(), y.contiguous(), dy.contiguous()
+    M, K = x.shape
+    Nn = weight.shape[0]
+    dx = torch.empty_like(x)
+    dW = torch.empty_like(weight)
+    db = torch.empty(Nn if need_bias else 0, device=x.device)
+    ws = _linear_ws(M, Nn, K, x.device, backward=True)
+    N.check(N.lib().abcd_linear_backward(M, Nn, K, N.ptr(x), K, N.ptr(weight), K, N.ptr(y), Nn, int(act), N.ptr(dy),
+                                         Nn, N.ptr(dx), K, N.ptr(dW), N.ptr(db) if need_bias else None, N.ptr(ws),
+                                         ws.numel(), N.stream()), "linear backward")
+    return [dx, dW, db]
+
+
+@linear_bwd.register_fake
+def _(x, weight, y, dy, act, need_bias):
+    return [torch.empty_like(x), torch.empty_like(weight), x.new_empty(weight.shape[0] if need_bias else 0)]
+
+
+def _linear_setup(ctx, inputs, output):
+    x, weight, bias, act = inputs
+    ctx.save_for_backward(x, weight, output)
+    ctx.act, ctx.has_bias = act, bias is not None
+
+
+def _linear_backward(ctx, dy):
+    x, weight, y = ctx.saved_tensors
+    dx, dW, db = linear_bwd(x, weight, y, dy, ctx.act, ctx.has_bias)
+    return dx, dW, (db if ctx.has_bias else None), None
+
+
+linear.register_autograd(_linear_backward, setup_context=_linear_setup)
+
+
 OPS = ("encoder", "encoder_bwd", "sampler", "sampler_bwd", "sampler_sample", "sampler_sample_bwd", "sampler_kl",
-       "sampler_kl_bwd", "decoder", "decoder_bwd")
+       "sampler_kl_bwd", "decoder", "decoder_bwd", "linear", "linear_bwd")
 
 
 def registered() -> Sequence[str]:

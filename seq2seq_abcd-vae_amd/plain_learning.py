@@ -10,7 +10,7 @@ import torch
 
 import learning
 from learning import logger
-from modules import engine, model, noise
+from modules import engine, model, noise, parallel
 
 
 class Learner(learning.Learner):
@@ -57,11 +57,14 @@ class Learner(learning.Learner):
         self.encoder.load_state_dict(self.checkpoint["encoder"], strict=False)
         self.feature_sampler.load_state_dict(self.checkpoint["feature_sampler"])
         self.decoder.load_state_dict(self.checkpoint["decoder"])
+        if not hasattr(self, "rank"):
+            self.rank, self.world = parallel.world()
         self._finish_modules()
         self.gradient_clip = self.checkpoint["gradient_clip"]
+        self.seed = int(self.checkpoint.get("seed", 1111))
         torch.set_rng_state(self.checkpoint["random_state"])
         if "abcd_noise_state" in self.checkpoint:
-            noise.set_state(self.checkpoint["abcd_noise_state"])
+            noise.set_state(self.checkpoint["abcd_noise_state"], rank=self.rank)
         return self.checkpoint["epoch"]
 
     def train(self, dataloader, is_pretraining=False):

@@ -135,6 +135,12 @@ SMALL_VARIANTS = {
     "gru_speaker_pretrain": dict(rnn="GRU", speaker=True, pretrain=True),
     "plain_lstm": dict(rnn="LSTM", plain=True),
     "plain_gru": dict(rnn="GRU", plain=True),
+    # sizes that are not multiples of 16 (the HIP path runs the zero-padded
+    # model, seq2seq_abcd-vae_amd/modules/padding.py): K = 10, H = 24, Hm = 40,
+    # D = 20, speaker dim 12; a 2-layer GRU at H = 20; the plain VAE at f = 10
+    "lstm_odd": dict(rnn="LSTM", speaker=True, dims=dict(H=24, Hm=40, D=20, K=10, S=12)),
+    "gru_odd_2layer": dict(rnn="GRU", layers=2, dims=dict(H=20, Hm=24, D=12, K=10)),
+    "plain_odd": dict(rnn="LSTM", plain=True, dims=dict(H=24, Hm=40, FPLAIN=10)),
 }
 
 
@@ -145,7 +151,7 @@ def state_items(prefix, module):
 def run_small(name, cfg):
     plain = cfg.get("plain", False)
     torch, model, data_utils, clip_legacy = import_reference("plain" if plain else "ABCD-VAE")
-    d = SMALL_DIMS
+    d = dict(SMALL_DIMS, **cfg.get("dims", {}))
     F, H, Hm, D, K = d["F"], d["H"], d["Hm"], d["D"], d["K"]
     rnn = cfg["rnn"]
     layers = cfg.get("layers", 1)
@@ -469,6 +475,10 @@ CLI_RUNS = {
     "lstm2_drop_e2": ("ABCD-VAE", ["-e", "2", "-b", "4", "-R", "LSTM", "-K", "16", "--encoder_rnn_layers", "2",
                                    "--encoder_hidden_dropout", "0.1"]),
     "ddrop_e2": ("ABCD-VAE", ["-e", "2", "-b", "4", "-R", "LSTM", "-K", "16", "--decoder_input_dropout", "0.3"]),
+    # sizes off the 16-grid: one softmax epoch, then Gumbel
+    "odd_sizes_e2": ("ABCD-VAE", ["-e", "2", "-b", "4", "-R", "LSTM", "-K", "10", "-f", "20", "--mlp_hidden_size",
+                                  "100", "--encoder_rnn_hidden_size", "40", "--decoder_rnn_hidden_size", "24",
+                                  "--speaker_embed_dim", "12", "--pretrain_epochs", "1"]),
 }
 
 LINE_PATTERNS = {

@@ -61,7 +61,7 @@ def test_fused_step_vs_reference(name, modules_pkg):
 
 
 @pytest.mark.parametrize("name", ["lstm_gumbel", "gru_gumbel", "lstm_speaker", "plain_lstm", "lstm_2layer",
-                                  "lstm_ddrop"])
+                                  "lstm_ddrop", "lstm_odd", "gru_odd_2layer", "plain_odd"])
 def test_module_autograd_vs_reference(name, modules_pkg):
     """The nn.Module surface (encoder(packed) -> sampler -> sample -> kl ->
     decoder -> loss.backward()) on the HIP autograd Functions."""

@@ -33,7 +33,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("case,tol", [("lstm_softmax_e2", 1e-4), ("lstm_gumbel_e2", 1e-4), ("gru_softmax_e2", 1e-4),
-                                      ("greedy_e2", 1e-4), ("lstm2_drop_e2", 1e-4), ("ddrop_e2", 1e-4)])
+                                      ("greedy_e2", 1e-4), ("lstm2_drop_e2", 1e-4), ("ddrop_e2", 1e-4),
+                                      ("odd_sizes_e2", 1e-4)])
 def test_toy_trajectory_matches_reference(tmp_path, case, tol):
     ka = known_answers()[case]
     learner, save = _run(tmp_path, ka["flags"], case)
