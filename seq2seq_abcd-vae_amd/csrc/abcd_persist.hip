@@ -1765,6 +1765,295 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// dec_bwd_fold: dec_bwd_sk with the emission-MLP product dZ W1cat folded into
+// the split-K dh partials.
+//
+// In dec_bwd_sk every member gathers the whole 64 x 2Hm dZ tile of its group
+// (128 KiB per member per step) after the P1 -> P2 hand-off and multiplies it
+// by its 8 units' W1cat columns (a 512-deep x6 MMA) -- the largest load and
+// MMA on the step's critical path (P2 6.2 us of 17.9 at c2).
+// dh = dZ W1cat + dG_{t+1} W_hh is linear in both terms, so it splits over
+// the members the way dh_rec already did: in P1 each member, right after its
+// own 16 dZ columns, forms its partial of dh for ALL units,
+//     part_m = dG_{t+1}[:, own 32 gate columns] W_hh[own rows]      (x6, K = 32)
+//            + dZ_t[:, own 16 columns] W1cat[own rows]               (fp32 MFMA, K = 16)
+// and publishes it; P2 sums the M partials of its 8 units (64 KiB per member,
+// as the dh_rec gather did) and runs the cell backward.  The dZ gather and
+// the 512-deep MMA leave P2; dZ is only stashed (plain stores) for the
+// weight-gradient GEMMs.  dx_{t+1} partials are unchanged (P2 -> next P0).
+// LDS: split-K image [NS][3][64] | W1 slice [NHS][64] (fp32 fragments) | P1
+// image [nchx][64] | wave regions: 110 KiB at c2 (dec_bwd_sk: 142).
+// ---------------------------------------------------------------------------
+template <int NXS, int NHS, bool GRU = false>
+__global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  constexpr int H = NHS * 16, GH = (GRU ? 3 : 4) * H, M = H / 8, NS = NXS + NHS;
+  const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
+  const int nchx = Fp / 16, nFt = Fp / 16;
+  const Role role = assign_role(a.nrt, M);
+  const int grp = role.grp, mem = role.mem;
+  const int rt = grp;
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int row0 = rt * PERSIST_ROWS + w * 16;
+  GSync gs{a.sync + grp * PERSIST_SYNC_STRIDE,
+           a.sync + ((size_t)2 * a.nrt + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
+           M, mem, a.flags, 0u};
+  const int u0 = mem * 8, unit = u0 + (r & 7);
+  const bool lo = r < 8;
+  f4* SK = smem;
+  f4* W1I = SK + NS * 3 * 64;
+  f4* B1 = W1I + NHS * 64;
+  float* Ast = reinterpret_cast<float*>(B1 + nchx * 64) + w * DSK_WAVE_FLOATS;
+  float* tb = Ast;  // the same wave-private region, reused for the 16-B store transposes (tp_quad)
+  const int trow = lane >> 2, tcol = 4 * (lane & 3);
+  // split-K image (dec_bwd_sk's): subtile s, lane (rr, qq) holds rows
+  // k = 8qq + 0..7 (gate qq, own units 0..7) of output column 16s + rr
+  for (int e = threadIdx.x; e < NS * 64; e += 256) {
+    const int s = e >> 6, ln = e & 63, rr = ln & 15, qq = ln >> 4;
+    const bool xs = s < NXS;
+    int col = qq * H + u0;
+    if (GRU && qq >= 2) col = (qq == 2) == xs ? 2 * H + u0 : -1;
+    const float* src = (xs ? a.WihT + (long)(16 * s + rr) * GH : a.WhhT + (long)(16 * (s - NXS) + rr) * GH) +
+                       (col < 0 ? 0 : col);
+    bf8 h, m, l;
+    split8(col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src),
+           col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src + 4), h, m, l);
+    SK[(s * 3) * 64 + ln] = __builtin_bit_cast(f4, h);
+    SK[(s * 3 + 1) * 64 + ln] = __builtin_bit_cast(f4, m);
+    SK[(s * 3 + 2) * 64 + ln] = __builtin_bit_cast(f4, l);
+  }
+  // W1 slice: subtile s (units 16s .. 16s + 15), lane (rr, qq): the W1cat
+  // entries of unit 16s + rr at this member's dZ columns 16 mem + 4qq .. + 3
+  for (int e = threadIdx.x; e < NHS * 64; e += 256) {
+    const int s = e >> 6, ln = e & 63, rr = ln & 15, qq = ln >> 4;
+    W1I[e] = *reinterpret_cast<const f4*>(a.W1T + (long)(16 * s + rr) * 2 * Hm + 16 * mem + 4 * qq);
+  }
+  // P1: dZ tile j1 = mem (2Hm/16 == M: checked by the launcher)
+  const bool ismu = mem < Hm / 16;
+  if (ismu) stage_b_frag(B1, a.W2mT, Fp, 1, nchx, [&](int) { return 16 * mem; });
+  else stage_b_frag(B1, a.W2lT, Fp, 1, nchx, [&](int) { return 16 * (mem - Hm / 16); });
+  const float s_em = *a.s_em;
+  __syncthreads();
+  const size_t slot_f = (size_t)a.nrt * NS * 4 * M * 256;  // floats per parity slot
+  const __amdgpu_buffer_rsrc_t pr0 = make_rsrc(a.part, (uint32_t)(slot_f * 4));
+  const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
+  // this wave's block of subtile s: (((grp*NS + s)*4 + w)*M + producer)*256 floats
+  auto blk = [&](int s) { return (uint32_t)((((size_t)grp * NS + s) * 4 + w) * M) * 1024u; };
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+  bool dgv = false;  // a0..a2: the split dG tile of the previous step (rows < its batch)
+  bf8 a0{}, a1{}, a2{};
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = T - 1 - i;
+    const int o = off[t], bs = off[t + 1] - o;
+    const int succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+    const bool has_part = i > 0 && row0 < succ_valid;  // step t+1's producers covered this wave's rows
+    const __amdgpu_buffer_rsrc_t prd = (i & 1) ? pr0 : pr1;  // step t+1's slot
+    const __amdgpu_buffer_rsrc_t pw = (i & 1) ? pr1 : pr0;   // this step's slot
+    // ---------------- P0: dx_{t+1} tile -> dMU, dLV ----------------
+    const int col0 = 16 * mem + r;
+    float emu[4], elv[4], eox[4], ey[4], emk[4];
+    if (mem < nFt) {
+      const uint32_t ef = (uint32_t)bs * Fp * 4u;
+      const __amdgpu_buffer_rsrc_t rmu = make_rsrc(a.MU + (size_t)o * Fp, ef), rlv = make_rsrc(a.LV + (size_t)o * Fp, ef),
+                                   rox = make_rsrc(a.OUT + (size_t)o * Fp, ef),
+                                   ryy = make_rsrc(a.Y + (size_t)o * F, (uint32_t)bs * F * 4u);
+      const __amdgpu_buffer_rsrc_t rmk =
+          make_rsrc(a.xmask ? a.xmask + (size_t)(o + bs) * F : a.Y, a.xmask ? (uint32_t)succ_valid * F * 4u : 0u);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
+        const uint32_t of = col0 < F ? (b * Fp + col0) * 4u : 0x80000000u;
+        const uint32_t oy = col0 < F ? (b * F + col0) * 4u : 0x80000000u;
+        emu[g] = bld(rmu, of);
+        elv[g] = bld(rlv, of);
+        eox[g] = bld(rox, of);
+        ey[g] = bld(ryy, oy);
+        emk[g] = a.xmask ? bld(rmk, oy) : 1.f;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) emu[g] = elv[g] = eox[g] = ey[g] = 0.f, emk[g] = 1.f;
+    }
+    if (i > 0) gs.wait(3u * i);
+    pin(emu), pin(elv), pin(eox), pin(ey), pin(emk);
+    PSTAMP(0);
+    if (mem < nFt) {
+      f4 dx = f4zero();
+      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx, mem % M);
+      float dmu[4], dlv[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        dmu[g] = dlv[g] = 0.f;
+        if (col0 < F) {
+          const float dxv = dx[g] * emk[g], mu = emu[g], lv = elv[g];
+          const float iv = __expf(-lv), d = ey[g] - mu;
+          dmu[g] = dxv + s_em * (-d) * iv;
+          dlv[g] = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);
+        }
+      }
+      const f4 mq = tp_quad(tb, dmu, lane), lq = tp_quad(tb + TP_FLOATS, dlv, lane);
+      if (row0 < bs) {
+        const uint32_t qo = (uint32_t)((row0 + trow) * Fp + 16 * mem + tcol) * 4u;
+        st4(make_rsrc(a.dMU + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, mq, true);
+        st4(make_rsrc(a.dLV + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, lq, true);
+      }
+    }
+    gs.publish();
+    PSTAMP(1);
+    PSTAMP(6);
+    // ---------------- P1: dZ tile -> this member's dh partials ----------------
+    float zpre[4];
+    {
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) zpre[g] = bld(rz, ((uint32_t)(row0 + 4 * q + g) * 2 * Hm + 16 * mem + r) * 4u);
+    }
+    gs.wait(3u * i + 1);
+    pin(zpre);
+    PSTAMP(2);
+    if (row0 < bs) {
+      f4 acc[2][1];
+      acc2_zero(acc);
+      const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
+      mma16<1>(acc, A, row0 + r, B1, nchx, lane, q);
+      acc2_fold(acc);
+      float dz[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) dz[g] = acc[0][0][g] * (1.f - zpre[g] * zpre[g]);
+      const f4 zq = tp_quad(tb, dz, lane);
+      // the dZ tile as an A operand: lane (r, q) = row r, columns 4q .. 4q + 3
+      const f4 za = *reinterpret_cast<const f4*>(tb + r * TP_PITCH + 4 * q);
+#pragma unroll
+      for (int s = 0; s < NHS; ++s) {
+        f4 pa = f4zero();
+        if (dgv) {
+          const f4* bp = SK + ((NXS + s) * 3) * 64 + lane;
+          pa = mma_x6(pa, a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                      __builtin_bit_cast(bf8, bp[128]));
+        }
+        const f4 wv = W1I[s * 64 + lane];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pa = mfma4(za[k], wv[k], pa);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pa), pw,
+                                               blk(NXS + s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+      }
+      // the dZ stash: read only by the weight-gradient GEMMs after the launch
+      st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
+          (uint32_t)((row0 + trow) * 2 * Hm + 16 * mem + tcol) * 4u, zq, false);
+    }
+    gs.publish();
+    PSTAMP(3);
+    // ---------------- P2: dh -> cell backward -> dG_t -> dx partials ----------------
+    float pg[4][4], pc[4], pcp[4], pdho[4];
+    {
+      const uint32_t eh = (uint32_t)bs * H * 4u;
+      const __amdgpu_buffer_rsrc_t rgs = make_rsrc(a.Gst + (size_t)o * 4 * H, eh * 4u),
+                                   rcs = make_rsrc(a.Cst + (size_t)o * H, GRU ? 0u : eh),
+                                   rcp = make_rsrc((GRU ? a.Hprev : a.Cprev) + (size_t)o * H, eh),
+                                   rdo = make_rsrc(a.DHO + (size_t)o * H, eh);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pg[g][j] = bld(rgs, (b * 4 * H + j * H + unit) * 4u);
+        pc[g] = GRU ? 0.f : bld(rcs, (b * H + unit) * 4u);
+        pcp[g] = bld(rcp, (b * H + unit) * 4u);
+        pdho[g] = bld(rdo, (b * H + unit) * 4u);
+      }
+    }
+    gs.wait(3u * i + 2);
+    pin(pg[0]), pin(pg[1]), pin(pg[2]), pin(pg[3]), pin(pc), pin(pcp), pin(pdho);
+    PSTAMP(4);
+    // dh of the own units: the M members' partials (lane takes column
+    // (mem & 1) * 8 + (r & 7) of subtile NXS + mem / 2)
+    f4 dhr = f4zero();
+    if (row0 < bs)
+      sum_partials<M>(pw, blk(NXS + (mem >> 1)) + (uint32_t)(q * 16 + (mem & 1) * 8 + (r & 7)) * 16u, dhr, mem % M);
+    PSTAMP(7);
+    float dgh[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dgh[g][j] = 0.f;
+      if (b >= bs) continue;
+      const bool fin = b >= succ_valid;
+      if constexpr (GRU) {
+        // dh_t = dZ W1 + dh_rec + dh_offset + dh_{t+1} z_{t+1} (the carry)
+        const float dh = dhr[g] + (fin ? 0.f : carry[g]) + pdho[g];
+        const float r_ = pg[g][0], z_ = pg[g][1], n_ = pg[g][2], ghn = pg[g][3];
+        const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
+        dgh[g][0] = dnp * ghn * r_ * (1.f - r_);
+        dgh[g][1] = dh * (pcp[g] - n_) * z_ * (1.f - z_);
+        dgh[g][2] = dnp;
+        dgh[g][3] = dnp * r_;
+        carry[g] = dh * z_;
+        if (t == 0 && lo) a.DC0[(long)b * H + unit] = dh * z_;
+      } else {
+        const float dh = dhr[g] + pdho[g];
+        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
+        const float tc = ftanh(pc[g]);
+        const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
+        dgh[g][0] = dc * g_ * i_ * (1.f - i_);
+        dgh[g][1] = dc * pcp[g] * f_ * (1.f - f_);
+        dgh[g][2] = dc * i_ * (1.f - g_ * g_);
+        dgh[g][3] = dh * tc * o_ * (1.f - o_);
+        carry[g] = dc * f_;
+        if (t == 0 && lo) a.DC0[(long)b * H + unit] = dc * f_;
+      }
+    }
+    const bool mk = i + 1 < T && row0 < bs;
+    if (row0 < bs) {  // dG tile of the wave: rows x [gate j][own unit]
+      __builtin_amdgcn_wave_barrier();
+      if (lo) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Ast[(4 * q + g) * DSK_PITCH + 8 * j + r] = dgh[g][j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (mk) {  // split once: the dx partials below and the next step's P1 dh partials
+      const float* ar = Ast + r * DSK_PITCH + 8 * q;
+      split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
+    }
+    dgv = mk;
+    if (mk && NXS > 0) {
+#pragma unroll
+      for (int s = 0; s < NXS; ++s) {
+        const f4* bp = SK + (s * 3) * 64 + lane;
+        const f4 v = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                            __builtin_bit_cast(bf8, bp[128]));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
+                                               blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+      }
+    }
+    gs.publish();
+    PSTAMP(5);
+    // stash for the weight-gradient GEMMs (plain 16-B stores after the publish)
+    if (row0 < bs) {
+      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.dG + (size_t)o * GH, (uint32_t)bs * GH * 4u);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int k = lane + 64 * k2, row = k >> 3, gate = (k >> 1) & 3, hf = 4 * (k & 1);
+        const f4 v = *reinterpret_cast<const f4*>(Ast + row * DSK_PITCH + 8 * gate + hf);
+        const uint32_t so = (uint32_t)((row0 + row) * GH + u0 + hf) * 4u;
+        if constexpr (GRU) {  // dGX = (dr, dz, dn), dGH = (dr, dz, dn r)
+          const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.dGH + (size_t)o * GH, (uint32_t)bs * GH * 4u);
+          if (gate < 3) st4(rg, so + (uint32_t)(gate * H) * 4u, v, false);
+          if (gate != 2) st4(rh, so + (uint32_t)((gate == 3 ? 2 : gate) * H) * 4u, v, false);
+        } else {
+          st4(rg, so + (uint32_t)(gate * H) * 4u, v, false);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 bool persist_enabled() {
@@ -2171,6 +2460,33 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   return 0;
 }
 
+template <int NXS, int NHS, bool GRU = false>
+static int launch_dec_bwd_fold(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+  constexpr int NS = NXS + NHS, M = NHS * 2;
+  const size_t lds = (size_t)(NS * 3 + NHS) * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * DSK_WAVE_FLOATS * 4;
+  const int grid = a.nrt * M;
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_fold<NXS, NHS, GRU>, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(zero_sync(s, a.sync, a.nrt));
+  PDecBwdArgs b = a;
+  b.flags = 1;
+  b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
+  {
+    TimedScope ts(s, TK_DEC_BWD);
+    dec_bwd_fold<NXS, NHS, GRU><<<grid, 256, lds, s>>>(b);
+  }
+  note_dispatch(TK_DEC_BWD, "dec_bwd_fold<%d,%d,%s> grid %d", NXS, NHS, GRU ? "GRU" : "LSTM", grid);
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+// ABCD_DECBWD=fold: dec_bwd_fold (A/B timing against dec_bwd_sk)
+static bool dec_bwd_folded() {
+  const char* v = getenv("ABCD_DECBWD");
+  return v && v[0] == 'f';
+}
+
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled() || a.H % 8) return 0;
@@ -2179,6 +2495,12 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
           a.Fp / 16 <= a.H / 8))
       return 0;
     const int nxs = a.feedback ? a.Fp / 16 : 0;
+    if (dec_bwd_folded()) {
+      if (nxs == 9) return launch_dec_bwd_fold<9, 16, true>(s, a, launched);
+      if (nxs == 5) return launch_dec_bwd_fold<5, 16, true>(s, a, launched);
+      if (nxs == 0) return launch_dec_bwd_fold<0, 16, true>(s, a, launched);
+      return 0;
+    }
     if (nxs == 9) return launch_dec_bwd_sk<9, 16, 16, true>(s, a, launched);
     if (nxs == 5) return launch_dec_bwd_sk<5, 16, 16, true>(s, a, launched);
     if (nxs == 0) return launch_dec_bwd_sk<0, 16, 16, true>(s, a, launched);
@@ -2188,9 +2510,15 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   // split-K form: H = 256 (32 members), 2Hm/16 == members, Fp/16 <= members
   if (a.part && x6_enabled(a.H) && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8) {
     const int nxs = a.feedback ? a.Fp / 16 : 0;
-    if (nxs == 9) return launch_dec_bwd_sk<9, 16, 16>(s, a, launched);
-    if (nxs == 5) return launch_dec_bwd_sk<5, 16, 16>(s, a, launched);
-    if (nxs == 0) return launch_dec_bwd_sk<0, 16, 16>(s, a, launched);
+    if (dec_bwd_folded()) {
+      if (nxs == 9) return launch_dec_bwd_fold<9, 16>(s, a, launched);
+      if (nxs == 5) return launch_dec_bwd_fold<5, 16>(s, a, launched);
+      if (nxs == 0) return launch_dec_bwd_fold<0, 16>(s, a, launched);
+    } else {
+      if (nxs == 9) return launch_dec_bwd_sk<9, 16, 16>(s, a, launched);
+      if (nxs == 5) return launch_dec_bwd_sk<5, 16, 16>(s, a, launched);
+      if (nxs == 0) return launch_dec_bwd_sk<0, 16, 16>(s, a, launched);
+    }
   }
   const int M = a.H / 8, nchg = 4 * a.H / 16, nchx = a.Fp / 16, nchz = 2 * a.Hm / 16;
   const int n0 = cdiv(a.Fp / 16 + a.H / 16, M), n1 = cdiv(2 * a.Hm / 16, M);

@@ -467,11 +467,11 @@ decoder.register_autograd(_decoder_backward, setup_context=_decoder_setup)
 # ----------------------------------------------------------------------------
 # nn.Linear (+ Tanh): the standalone MLP (model.py:316-334) outside the step
 # ----------------------------------------------------------------------------
-def _linear_ws(M, N, K, device, backward=False):
+def _linear_ws(rows, cols, depth, device, backward=False):
     if backward:
-        return N.workspace(N.lib().abcd_linear_backward_workspace_bytes(M, N, K), device)
-    Kp = (max(K, N) + 15) // 16 * 16
-    return N.workspace((M + N) * Kp * 4 + (1 << 22), device)
+        return N.workspace(N.lib().abcd_linear_backward_workspace_bytes(rows, cols, depth), device)
+    Kp = (max(depth, cols) + 15) // 16 * 16
+    return N.workspace((rows + cols) * Kp * 4 + (1 << 22), device)
 
 
 @torch.library.custom_op("abcd::linear", mutates_args=())
