@@ -1784,6 +1784,8 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
 // LDS: split-K image [NS][3][64] | W1 slice [NHS][64] (fp32 fragments) | P1
 // image [nchx][64] | wave regions: 110 KiB at c2 (dec_bwd_sk: 142).
 // ---------------------------------------------------------------------------
+// (Forming the dG_{t+1} W_hh half at the end of the previous P2 and carrying
+// it in 16 accumulators into P1 measured 3.34 -> 4.24 ms: register pressure.)
 template <int NXS, int NHS, bool GRU = false>
 __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
@@ -2481,10 +2483,11 @@ static int launch_dec_bwd_fold(hipStream_t s, const PDecBwdArgs& a, bool* launch
   *launched = true;
   return 0;
 }
-// ABCD_DECBWD=fold: dec_bwd_fold (A/B timing against dec_bwd_sk)
+// dec_bwd_fold by default: same-box A/B at c2, 3.70 / 3.72 -> 3.34 / 3.33 ms
+// per launch, step 10.85 -> 10.50 ms; ABCD_DECBWD=sk: dec_bwd_sk (A/B timing)
 static bool dec_bwd_folded() {
   const char* v = getenv("ABCD_DECBWD");
-  return v && v[0] == 'f';
+  return !(v && v[0] == 's');
 }
 
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {

@@ -12,6 +12,8 @@ bench.py times at config 2 / 4 / 5 are the ones compared with the reference.
 Tolerances: loss terms 1e-4 relative (north star), logits / last hidden 1e-4
 of the tensor's max, gradients 1e-3 of the tensor's max (norms 1e-3
 relative), post-SGD parameter deltas 1e-3, argmax categories exact."""
+import os
+
 import pytest
 import torch
 
@@ -27,10 +29,13 @@ GRAD_TOL = 1e-3
 # the kernels bench.py's configs dispatch at H = Hm = 256, F = 129 (Fp = 144)
 EXPECT = {
     "LSTM": {"enc_fwd": "enc_fwd_persist<4,16,8>", "enc_bwd": "enc_bwd_sk<4,16>",
-             "dec_fwd": "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd": "dec_bwd_sk<9,16,16,LSTM>"},
+             "dec_fwd": "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd": "dec_bwd_fold<9,16,LSTM>"},
     "GRU": {"enc_fwd": "enc_fwd_persist<3,16,8>", "enc_bwd": "enc_bwd_sk<3,16>",
-            "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_sk<9,16,16,GRU>"},
+            "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_fold<9,16,GRU>"},
 }
+if os.environ.get("ABCD_DECBWD", "").startswith("s"):  # the unfolded decoder BPTT (A/B runs)
+    for _r in EXPECT:
+        EXPECT[_r]["dec_bwd"] = f"dec_bwd_sk<9,16,16,{_r}>"
 
 
 def _noise(inp):
