@@ -1786,7 +1786,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
 // ---------------------------------------------------------------------------
 // (Forming the dG_{t+1} W_hh half at the end of the previous P2 and carrying
 // it in 16 accumulators into P1 measured 3.34 -> 4.24 ms: register pressure.)
-template <int NXS, int NHS, bool GRU = false>
+template <int NXS, int NHS, bool GRU = false, bool P0S = true, bool HX = true>
 __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   constexpr int H = NHS * 16, GH = (GRU ? 3 : 4) * H, M = H / 8, NS = NXS + NHS;
@@ -1842,6 +1842,13 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
   const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
   // this wave's block of subtile s: (((grp*NS + s)*4 + w)*M + producer)*256 floats
   auto blk = [&](int s) { return (uint32_t)((((size_t)grp * NS + s) * 4 + w) * M) * 1024u; };
+  // P0 unit of this wave: dx tile jx (16 F columns) of its 16 rows.  P0S: the
+  // (Fp/16 tiles x 4 row blocks) units are dealt over every member's waves
+  // (wave w of member m takes tile (m - nFt w) mod M), so no member gathers
+  // more than two waves' partials; otherwise member m < Fp/16 takes tile m in
+  // all four waves (128 KiB of partials per step on one CU)
+  const int jx = P0S ? ((mem - nFt * w) % M + M) % M : mem;
+  const bool p0 = jx < nFt;
   float carry[4] = {0.f, 0.f, 0.f, 0.f};
   bool dgv = false;  // a0..a2: the split dG tile of the previous step (rows < its batch)
   bf8 a0{}, a1{}, a2{};
@@ -1854,9 +1861,9 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
     const __amdgpu_buffer_rsrc_t prd = (i & 1) ? pr0 : pr1;  // step t+1's slot
     const __amdgpu_buffer_rsrc_t pw = (i & 1) ? pr1 : pr0;   // this step's slot
     // ---------------- P0: dx_{t+1} tile -> dMU, dLV ----------------
-    const int col0 = 16 * mem + r;
+    const int col0 = 16 * jx + r;
     float emu[4], elv[4], eox[4], ey[4], emk[4];
-    if (mem < nFt) {
+    if (p0) {
       const uint32_t ef = (uint32_t)bs * Fp * 4u;
       const __amdgpu_buffer_rsrc_t rmu = make_rsrc(a.MU + (size_t)o * Fp, ef), rlv = make_rsrc(a.LV + (size_t)o * Fp, ef),
                                    rox = make_rsrc(a.OUT + (size_t)o * Fp, ef),
@@ -1881,9 +1888,9 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
     if (i > 0) gs.wait(3u * i);
     pin(emu), pin(elv), pin(eox), pin(ey), pin(emk);
     PSTAMP(0);
-    if (mem < nFt) {
+    if (p0) {
       f4 dx = f4zero();
-      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx, mem % M);
+      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(jx) + (uint32_t)lane * 16u, dx, mem % M);
       float dmu[4], dlv[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1897,13 +1904,26 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
       }
       const f4 mq = tp_quad(tb, dmu, lane), lq = tp_quad(tb + TP_FLOATS, dlv, lane);
       if (row0 < bs) {
-        const uint32_t qo = (uint32_t)((row0 + trow) * Fp + 16 * mem + tcol) * 4u;
+        const uint32_t qo = (uint32_t)((row0 + trow) * Fp + 16 * jx + tcol) * 4u;
         st4(make_rsrc(a.dMU + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, mq, true);
         st4(make_rsrc(a.dLV + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, lq, true);
       }
     }
     gs.publish();
     PSTAMP(1);
+    // HX: the dG_{t+1} W_hh half of this step's dh partials needs nothing of
+    // this step -- formed here, in front of the P1 wait
+    f4 dhp[HX ? NHS : 1];
+    if constexpr (HX) {
+      if (dgv) {
+#pragma unroll
+        for (int s = 0; s < NHS; ++s) {
+          const f4* bp = SK + ((NXS + s) * 3) * 64 + lane;
+          dhp[s] = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                          __builtin_bit_cast(bf8, bp[128]));
+        }
+      }
+    }
     PSTAMP(6);
     // ---------------- P1: dZ tile -> this member's dh partials ----------------
     float zpre[4];
@@ -1930,7 +1950,9 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
 #pragma unroll
       for (int s = 0; s < NHS; ++s) {
         f4 pa = f4zero();
-        if (dgv) {
+        if (HX) {
+          if (dgv) pa = dhp[HX ? s : 0];
+        } else if (dgv) {
           const f4* bp = SK + ((NXS + s) * 3) * 64 + lane;
           pa = mma_x6(pa, a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
                       __builtin_bit_cast(bf8, bp[128]));
@@ -2462,13 +2484,13 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   return 0;
 }
 
-template <int NXS, int NHS, bool GRU = false>
-static int launch_dec_bwd_fold(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+template <int NXS, int NHS, bool GRU, bool P0S, bool HX>
+static int launch_dec_bwd_fold_k(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   constexpr int NS = NXS + NHS, M = NHS * 2;
   const size_t lds = (size_t)(NS * 3 + NHS) * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * DSK_WAVE_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_fold<NXS, NHS, GRU>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_fold<NXS, NHS, GRU, P0S, HX>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
@@ -2476,12 +2498,25 @@ static int launch_dec_bwd_fold(hipStream_t s, const PDecBwdArgs& a, bool* launch
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_fold<NXS, NHS, GRU><<<grid, 256, lds, s>>>(b);
+    dec_bwd_fold<NXS, NHS, GRU, P0S, HX><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_DEC_BWD, "dec_bwd_fold<%d,%d,%s> grid %d", NXS, NHS, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
+}
+// By default the P0 units are dealt over every member (same-box A/B at c2:
+// dec_bwd 3.35 / 3.34 -> 3.28 / 3.29 ms) and the x6 half of the P1 partials
+// runs in front of the P1 wait (3.29 / 3.29 -> 3.08 / 3.06 ms, step 10.47 ->
+// 10.27 ms).  ABCD_P0S=0 / ABCD_HX=0 restore either (A/B timing).
+template <int NXS, int NHS, bool GRU = false>
+static int launch_dec_bwd_fold(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+  const char* v = getenv("ABCD_P0S");
+  const char* x = getenv("ABCD_HX");
+  const bool p0s = !(v && v[0] == '0'), hx = !(x && x[0] == '0');
+  if (!p0s) return launch_dec_bwd_fold_k<NXS, NHS, GRU, false, false>(s, a, launched);
+  if (hx) return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, true>(s, a, launched);
+  return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, false>(s, a, launched);
 }
 // dec_bwd_fold by default: same-box A/B at c2, 3.70 / 3.72 -> 3.34 / 3.33 ms
 // per launch, step 10.85 -> 10.50 ms; ABCD_DECBWD=sk: dec_bwd_sk (A/B timing)
