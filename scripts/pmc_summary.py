@@ -11,7 +11,7 @@ out = sys.argv[1]
 tot = defaultdict(float)
 n = defaultdict(set)
 kern = None
-for f in glob.glob(os.path.join(out, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         if "gemm" not in name and "slab" not in name:
