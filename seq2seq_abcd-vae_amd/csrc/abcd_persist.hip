@@ -524,6 +524,15 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
 // after all of them consumed step i-1's partials (slot (i-1)&1).
 // G = 3 (GRU) pads the own-column block to 64 with a zero gate.
 // ---------------------------------------------------------------------------
+// Round 3: wave w forms the partials of consumers 4w..4w+3 (NSUB / 4 of
+// them) for all 64 rows of the member's tile, so its quarter of the W_hh
+// image (2 chunks x 3 planes per consumer) lives in registers for the whole
+// launch instead of every wave re-reading the whole 96 KiB image from LDS
+// each step; the A fragments come from the member's shared dG tile (one
+// barrier) and each consumer's partial leaves as soon as its accumulator is
+// done, under the remaining MFMAs.  Same operands, same accumulation order as
+// the per-wave form it replaced: bit-identical partials (same-box A/B at c2:
+// enc_bwd 1.99 -> 1.93-1.97 ms).
 constexpr int SK_PITCH = 68;  // floats per row of the wave-private dG transpose (conflict-free b128 reads)
 template <int G, int NSUB>
 __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
@@ -563,6 +572,17 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
     Bimg[d + 128] = __builtin_bit_cast(f4, l);
   }
   __syncthreads();
+  constexpr int JW = NSUB / 4;  // consumers per wave
+  static_assert(NSUB % 4 == 0, "the consumers are dealt over the 4 waves");
+  bf8 Br[JW][2][3];  // this wave's quarter of the image, resident for the launch
+#pragma unroll
+  for (int jj = 0; jj < JW; ++jj)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        Br[jj][c][p] = __builtin_bit_cast(bf8, Bimg[(((JW * w + jj) * 2 + c) * 3 + p) * 64 + lane]);
+  const float* const At = reinterpret_cast<const float*>(smem + NSUB * 2 * 3 * 64);  // the member's 64-row dG tile
   const size_t slot_f = (size_t)ng * nut * 4 * nut * 256;  // floats per parity slot
   float carry[4] = {0.f, 0.f, 0.f, 0.f};
   const int* off = a.off;
@@ -667,30 +687,29 @@ __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
       __builtin_amdgcn_wave_barrier();
     }
     // partials for the next step from this step's own dG columns
-    if (i + 1 < T && row0 < bs) {
-      f4 acc[NSUB];
+    if (i + 1 < T) {
+      __syncthreads();  // every wave's dG rows are in the member's tile
+      const __amdgpu_buffer_rsrc_t pw = make_rsrc(a.part + (size_t)((i + 1) & 1) * slot_f, (uint32_t)(slot_f * 4));
 #pragma unroll
-      for (int j = 0; j < NSUB; ++j) acc[j] = f4zero();
+      for (int mt = 0; mt < 4; ++mt) {
+        if (rt * PERSIST_ROWS + 16 * mt >= bs) break;  // uniform: row tiles past the step's batch
+        bf8 av[2][3];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const float* ar = Ast + r * SK_PITCH + 32 * c + 8 * q;
-        const f4 x0 = *reinterpret_cast<const f4*>(ar), x1 = *reinterpret_cast<const f4*>(ar + 4);
-        bf8 a0, a1, a2;
-        split8(x0, x1, a0, a1, a2);
+        for (int c = 0; c < 2; ++c) {
+          const float* ar = At + (16 * mt + r) * SK_PITCH + 32 * c + 8 * q;
+          split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), av[c][0], av[c][1], av[c][2]);
+        }
 #pragma unroll
-        for (int j = 0; j < NSUB; ++j) {
-          const f4* bp = Bimg + ((j * 2 + c) * 3) * 64 + lane;
-          acc[j] = mma_x6(acc[j], a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
-                          __builtin_bit_cast(bf8, bp[128]));
+        for (int jj = 0; jj < JW; ++jj) {
+          f4 acc = f4zero();
+#pragma unroll
+          for (int c = 0; c < 2; ++c) acc = mma_x6(acc, av[c][0], av[c][1], av[c][2], Br[jj][c][0], Br[jj][c][1], Br[jj][c][2]);
+          // consumer j = JW w + jj, its wave mt: (((grp*nut + j)*4 + mt)*nut + mem)*256, lane's 4 floats (sc1)
+          const int j = JW * w + jj;
+          const uint32_t o = (uint32_t)(((((size_t)grp * nut + j) * 4 + mt) * nut + mem) * 256 + lane * 4) * 4u;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc), pw, o, 0, 16);
         }
       }
-      // consumer j's block of this step parity: (((grp*nut + j)*4 + w)*nut + mem)*256, lane's 4 floats (sc1)
-      const __amdgpu_buffer_rsrc_t pw = make_rsrc(a.part + (size_t)((i + 1) & 1) * slot_f, (uint32_t)(slot_f * 4));
-      const uint32_t base = (uint32_t)(((((size_t)grp * nut) * 4 + w) * nut + mem) * 256 + lane * 4) * 4u;
-#pragma unroll
-      for (int j = 0; j < NSUB; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[j]), pw, base + (uint32_t)j * (4u * nut * 1024u),
-                                               0, 16);
     }
     PSTAMP(3);
     group_publish(cnt);
