@@ -106,6 +106,19 @@ int abcd_encoder_forward_dropout(const abcd_encoder_cfg* cfg, const abcd_encoder
 int abcd_encoder_backward_dropout(const abcd_encoder_cfg* cfg, const abcd_encoder_params* p, const abcd_packed* x,
                                   const float* const* noise, const float* d_last_hidden, const abcd_encoder_grads* g,
                                   void* ws, size_t ws_bytes, void* stream, void* wgrad_stream);
+/* The weight gradients of one LSTM layer over its packed frames, every
+ * direction at once: the autograd of nn.LSTM's w_ih, b_ih, b_hh, w_hh
+ * (model.py:53,60-66) given the gate gradients.  For direction d < nd <= 2:
+ *   w_ih[d] = dG[d]^T X,  b_ih[d] = b_hh[d] = colsum(dG[d]),  w_hh[d] = dG[d]^T Hprev[d]
+ * dG[d]: K x 4H (row stride 4H, gate blocks i, f, g, o), X: K x F (row
+ * stride ldx), Hprev[d]: K x H (stride H; the hidden state each frame's step
+ * consumed, zero where it had no predecessor).  b_hh[d] may be NULL.  The
+ * encoder backward runs this after its BPTT (layer 0); at F <= 143 with
+ * roundup16(F) = 144 and H = 256 it is one gemm_wg2 launch + one slab reduction. */
+size_t abcd_lstm_wgrad_workspace_bytes(int nd, int F, int H, int K);
+int abcd_lstm_wgrad(int nd, int F, int H, int K, const float* const* dG, const float* X, long ldx,
+                    const float* const* Hprev, float* const* w_ih, float* const* b_ih, float* const* b_hh,
+                    float* const* w_hh, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * ABCDSampler (model.py:538-639) and the plain Gaussian Sampler
@@ -357,7 +370,8 @@ int abcd_timing_read(double* out);
  * 2 encoder backward, 3 decoder forward, 4 decoder backward (persistent) */
 int abcd_timing_read_kernel(int kid, double* out);
 /* which kernel the last launch of a role ran (same ids as abcd_timing_read_kernel,
- * e.g. "dec_bwd_sk<9,16,16,LSTM> grid 256" or "per-step ..."), and how many
+ * 5 / 6 the sampler head forward / backward, 7 the encoder's layer-0 weight
+ * gradients; e.g. "dec_bwd_sk<9,16,16,LSTM> grid 256" or "per-step ..."), and how many
  * launches of the role since abcd_dispatch_reset; host-side bookkeeping only */
 const char* abcd_dispatch_name(int kid);
 long abcd_dispatch_count(int kid);

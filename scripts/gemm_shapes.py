@@ -3,6 +3,7 @@
 median of 20 launches) -- the frame-parallel input projection / offset head
 (abcd_gemm_nt, both operands K-contiguous) and the weight gradients
 (abcd_gemm_tn, both K-major, K = packed frames)."""
+import ctypes
 import os
 import sys
 
@@ -13,13 +14,33 @@ from modules import _native as Nn  # noqa: E402
 
 L = 65583
 SHAPES = [("nt", "xproj", L, 2048, 144), ("nt", "offset-head", L, 256, 256),
-          ("tn", "dW_hh", 1024, 256, L), ("tn", "dW_ih", 1024, 129, L)]
+          ("tn", "dW_hh", 1024, 256, L), ("tn", "dW_ih", 1024, 129, L), ("wg", "wg2", 1024, 129, L)]
 
 
 def run(kind, M, N, K):
     g = torch.Generator(device="cuda").manual_seed(1)
     ws = Nn.workspace(64 * M * N * 4 + (1 << 22), "cuda")
-    if kind == "nt":
+    if kind == "wg":  # abcd_lstm_wgrad: both directions' [dW_ih | db | dW_hh] (F = N, H = M / 4)
+        H, F = M // 4, N
+        dG = [torch.randn(K, M, device="cuda", generator=g) for _ in range(2)]
+        X = torch.randn(K, F, device="cuda", generator=g)
+        Hp = [torch.randn(K, H, device="cuda", generator=g) for _ in range(2)]
+        wih = [torch.empty(M, F, device="cuda") for _ in range(2)]
+        bih = [torch.empty(M, device="cuda") for _ in range(2)]
+        whh = [torch.empty(M, H, device="cuda") for _ in range(2)]
+        wsb = Nn.workspace(Nn.lib().abcd_lstm_wgrad_workspace_bytes(2, F, H, K), "cuda")
+        arr = lambda ts: (ctypes.c_void_p * 2)(*[t.data_ptr() for t in ts])
+        keep = [arr(dG), arr(Hp), arr(wih), arr(bih), arr(whh)]
+        f = lambda: Nn.lib().abcd_lstm_wgrad(2, F, H, K, keep[0], Nn.ptr(X), F, keep[1], keep[2], keep[3], None,
+                                             keep[4], Nn.ptr(wsb), wsb.numel(), Nn.stream())
+        C = whh[1]
+        ref = lambda: dG[1].double().t() @ Hp[1].double()
+        Nn.check(f(), "wgrad")
+        torch.cuda.synchronize()
+        e1 = ((wih[0].double() - dG[0].double().t() @ X.double()).abs().max() / (dG[0].double().t() @ X.double()).abs().max()).item()
+        e2 = ((bih[0].double() - dG[0].double().sum(0)).abs().max() / dG[0].double().sum(0).abs().max()).item()
+        print(f"  wg2 rel err: w_ih {e1:.2e}  b {e2:.2e}", flush=True)
+    elif kind == "nt":
         A = torch.randn(M, K, device="cuda", generator=g)
         B = torch.randn(N, K, device="cuda", generator=g)
         C = torch.empty(M, N, device="cuda")

@@ -1064,6 +1064,256 @@ static int gemm_x6t_launch(hipStream_t s, int M, int N, int K, const float* A, l
 }
 
 
+// ---------------------------------------------------------------------------
+// gemm_wg2: every weight gradient of a layer-0 LSTM encoder cell, all
+// directions in ONE launch (model.py:60-66's autograd for w_ih, b_ih, b_hh,
+// w_hh):
+//     [dW_ih | db | 0 | dW_hh]_d = dG_d^T [Xp | Hprev_d]      (K = all L frames)
+// Xp is the padded frame copy whose column F holds 1 (set_col_kernel), so its
+// N1 = Fp columns give dW_ih and the bias gradient in one product; the N2 = H
+// columns of Hprev give dW_hh.  The split GEMMs this replaces (x6s dW_ih +
+// x6t dW_hh per direction, two streams, four slab reductions) read dG twice
+// and split every dG fragment twice; here a workgroup owns 128 gate rows x
+// ALL N1 + N2 columns, so dG is read and split once and the B chunk is shared
+// by the 8 row tiles of one K range (XCD-grouped: they run on one L2).
+//   Tile 128 x 16 NB (NB = 25 at Fp = 144, H = 256), 4 waves as 2 x 2: a wave
+// owns 64 rows x 13 column blocks (208 accumulator registers).  Operands are
+// staged fp32 in LDS ([k][col], double-buffered: 139 KiB, one workgroup per
+// CU) and each wave splits its own fragments (4 A + 13 B splits per 32-deep
+// chunk against 312 MFMAs).  Branch-free buffer loads (k >= the K range and
+// rows >= M read 0); the grid's K ranges write fp32 slabs that
+// wg2_reduce_kernel sums in slab order and scatters into the gradients.
+// ---------------------------------------------------------------------------
+template <int N1, int N2>
+struct Wg2 {
+  static constexpr int NT = N1 + N2, NB = (NT + 15) / 16, NBW = (NB + 1) / 2;
+  static constexpr int BM = 128, BK = 32, LA = BM + 4, LB = 32 * NBW + 4;
+  static constexpr int SA = BK * LA + 16 * (BK / 8), SB = BK * LB + 16 * (BK / 8);
+  static constexpr int AVT = BK * BM / 4, V1T = BK * N1 / 4, V2T = BK * N2 / 4;  // f4 per chunk
+  static constexpr int AV = AVT / 256, V1 = (V1T + 255) / 256, V2 = (V2T + 255) / 256;
+  static constexpr size_t LDS = (size_t)2 * (SA + SB) * 4;
+  static_assert(N1 % 4 == 0 && N2 % 4 == 0 && AVT % 256 == 0, "f4 staging");
+};
+
+template <int N1, int N2>
+__global__ __launch_bounds__(256, 1) void gemm_wg2_kernel(WgArgs a) {
+  using G = Wg2<N1, N2>;
+  constexpr int NT = G::NT, NBW = G::NBW, BM = G::BM, BK = G::BK, LA = G::LA, LB = G::LB;
+  constexpr int SA = G::SA, SB = G::SB, AV = G::AV, V1 = G::V1, V2 = G::V2;
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  float* const As = wsm;
+  float* const Bs = wsm + 2 * SA;
+  const dim3 bid = xcd_tile(true);  // the row tiles of one (direction, K range) on one XCD
+  const int dz = bid.z, d = dz / a.Z, z = dz % a.Z;
+  const int m0 = bid.x * BM, M = a.M;
+  const int kb = z * a.kps, ke = min(a.K, kb + a.kps);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.A[d], (uint32_t)((size_t)ke * a.lda * 4));
+  const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.B1[d], (uint32_t)((size_t)ke * a.ldb1 * 4));
+  const __amdgpu_buffer_rsrc_t r2 = make_rsrc(a.B2[d], (uint32_t)((size_t)ke * a.ldb2 * 4));
+  constexpr uint32_t OOB = 0x80000000u;
+  auto ld4 = [](const __amdgpu_buffer_rsrc_t& rs, uint32_t o) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+  };
+  auto gload = [&](int k0, f4 (&xa)[AV], f4 (&x1)[V1], f4 (&x2)[V2]) {
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int x = tid + 256 * u, k = k0 + x / (BM / 4), m = m0 + 4 * (x % (BM / 4));
+      xa[u] = ld4(rA, m < M ? (uint32_t)(((long)k * a.lda + m) * 4) : OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < V1; ++u) {
+      const int x = tid + 256 * u, k = k0 + x / (N1 / 4), c = 4 * (x % (N1 / 4));
+      x1[u] = ld4(r1, x < G::V1T ? (uint32_t)(((long)k * a.ldb1 + c) * 4) : OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < V2; ++u) {
+      const int x = tid + 256 * u, k = k0 + x / (N2 / 4), c = 4 * (x % (N2 / 4));
+      x2[u] = ld4(r2, x < G::V2T ? (uint32_t)(((long)k * a.ldb2 + c) * 4) : OOB);
+    }
+  };
+  // [k][col] slabs, row k at k * LD + 16 (k / 8) (the four 8-k groups of a
+  // fragment read on different bank quarters, as gemm_x6s)
+  auto lstore = [&](int buf, const f4 (&xa)[AV], const f4 (&x1)[V1], const f4 (&x2)[V2]) {
+    float* as = As + buf * SA;
+    float* bs = Bs + buf * SB;
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int x = tid + 256 * u, k = x / (BM / 4), c = 4 * (x % (BM / 4));
+      *reinterpret_cast<f4*>(as + k * LA + 16 * (k >> 3) + c) = xa[u];
+    }
+#pragma unroll
+    for (int u = 0; u < V1; ++u) {
+      const int x = tid + 256 * u, k = x / (N1 / 4), c = 4 * (x % (N1 / 4));
+      if (x < G::V1T) *reinterpret_cast<f4*>(bs + k * LB + 16 * (k >> 3) + c) = x1[u];
+    }
+#pragma unroll
+    for (int u = 0; u < V2; ++u) {
+      const int x = tid + 256 * u, k = x / (N2 / 4), c = 4 * (x % (N2 / 4));
+      if (x < G::V2T) *reinterpret_cast<f4*>(bs + k * LB + 16 * (k >> 3) + N1 + c) = x2[u];
+    }
+  };
+  f4 acc[4][NBW];
+  acc_zero(acc);
+  auto compute = [&](int cur) {
+    // fragment of lane (r, q): row / column r of the block, k = 8q .. 8q + 7
+    const float* as = As + cur * SA + 8 * q * LA + 16 * q + wm * 64 + r;
+    const float* bs = Bs + cur * SB + 8 * q * LB + 16 * q + wn * 16 * NBW + r;
+    bf8 ap[4][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f4 x0, x1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        x0[t] = as[t * LA + 16 * i];
+        x1[t] = as[(4 + t) * LA + 16 * i];
+      }
+      split8(x0, x1, ap[i][0], ap[i][1], ap[i][2]);
+    }
+    constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+    // (an odd block count leaves the last half-wave one block past NB: it
+    // multiplies the zeroed pad columns, never stored -- no branch, so the
+    // block loop stays one basic block the scheduler can interleave)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      f4 x0, x1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        x0[t] = bs[t * LB + 16 * j];
+        x1[t] = bs[(4 + t) * LB + 16 * j];
+      }
+      bf8 bp[3];
+      split8(x0, x1, bp[0], bp[1], bp[2]);
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mfma_bf(ap[i][TA[t]], bp[TB[t]], acc[i][j]);
+    }
+  };
+  // the pad columns NT .. 32 NBW of both B stages read as 0
+  for (int e = tid; e < 2 * BK * (LB - 4 - NT); e += 256) {
+    const int st = e / (BK * (LB - 4 - NT)), x = e % (BK * (LB - 4 - NT)), k = x / (LB - 4 - NT);
+    Bs[st * SB + k * LB + 16 * (k >> 3) + NT + x % (LB - 4 - NT)] = 0.f;
+  }
+  f4 ra[AV], r1v[V1], r2v[V2];
+  gload(kb, ra, r1v, r2v);
+  lstore(0, ra, r1v, r2v);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) gload(k0 + BK, ra, r1v, r2v);
+    compute(cur);
+    if (more) lstore(cur ^ 1, ra, r1v, r2v);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // epilogue: per 16-row block, a wave-private LDS transpose, then whole-row
+  // 16-B stores into this K range's slab [M][NT]
+  constexpr int SW = 16 * NBW, SP = SW + 4;
+  float* stg = wsm + w * 16 * SP;
+  float* const dst = a.slab + (size_t)dz * M * NT;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < NBW; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < NBW; ++p) {  // 16 rows x 4 NBW quads = 64 NBW lanes' worth
+      const int e = lane + 64 * p, lr = e / (4 * NBW), c4 = e % (4 * NBW);
+      const int gcol = wn * SW + 4 * c4, grow = m0 + wm * 64 + 16 * i + lr;
+      if (grow < M && gcol < NT)
+        *reinterpret_cast<f4*>(dst + (size_t)grow * NT + gcol) = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// sum of the Z slabs of each direction (slab order, SR_DEPTH loads in
+// flight) scattered into w_ih (cols < F), b_ih / b_hh (col F), w_hh (cols
+// N1 .. N1 + H)
+__global__ __launch_bounds__(256) void wg2_reduce_kernel(const float* slab, int nd, int Z, int M, int NT, int N1,
+                                                         int F, int H, WgOut o) {
+  const long per = (long)M * NT / 4;  // f4 per slab
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nd * per; i += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(i / per);
+    const long e = i % per;
+    const f4* base = reinterpret_cast<const f4*>(slab) + (long)d * Z * per + e;
+    f4 s = f4zero();
+    for (int z0 = 0; z0 < Z; z0 += SR_DEPTH) {
+      f4 v[SR_DEPTH];
+#pragma unroll
+      for (int k = 0; k < SR_DEPTH; ++k) v[k] = z0 + k < Z ? base[(long)(z0 + k) * per] : f4zero();
+#pragma unroll
+      for (int k = 0; k < SR_DEPTH; ++k) s += v[k];
+    }
+    const int m = (int)(4 * e / NT), n0 = (int)(4 * e % NT);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int n = n0 + t;
+      if (n < F) o.w_ih[d][(long)m * F + n] = s[t];
+      else if (n == F) {
+        o.b_ih[d][m] = s[t];
+        if (o.b_hh[d]) o.b_hh[d][m] = s[t];
+      } else if (n >= N1 && n < N1 + H) o.w_hh[d][(long)m * H + n - N1] = s[t];
+    }
+  }
+}
+
+template <int N1, int N2>
+static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F, float* scratch,
+                            size_t scratch_floats) {
+  using G = Wg2<N1, N2>;
+  const int mt = cdiv(M, G::BM);
+  // one workgroup per CU: about 256 / (nd x mt) K ranges, the grid a multiple of 8
+  int Z = std::max(1, 256 / (nd * mt));
+  while ((nd * mt * Z) % 8) ++Z;
+  Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)nd * M * G::NT)));
+  if (Z < 1) return -1;
+  const int kps = ((cdiv(K, Z) + 31) / 32) * 32;
+  Z = cdiv(K, kps);
+  WgArgs a{};
+  WgOut o{};
+  for (int d = 0; d < nd; ++d) {
+    a.A[d] = dirs[d].dG; a.B1[d] = dirs[d].X; a.B2[d] = dirs[d].Hprev;
+    o.w_ih[d] = dirs[d].w_ih; o.b_ih[d] = dirs[d].b_ih; o.b_hh[d] = dirs[d].b_hh; o.w_hh[d] = dirs[d].w_hh;
+  }
+  a.lda = M; a.ldb1 = N1; a.ldb2 = N2; a.M = M; a.K = K; a.kps = kps; a.Z = Z; a.slab = scratch;
+  static bool attr = false;
+  if (!attr) {
+    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg2_kernel<N1, N2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)G::LDS));
+    attr = true;
+  }
+  gemm_wg2_kernel<N1, N2><<<dim3(mt, 1, nd * Z), 256, G::LDS, s>>>(a);
+  ABCD_CHECK_LAUNCH();
+  const long nq = (long)nd * M * G::NT / 4;
+  wg2_reduce_kernel<<<(int)std::min<long>(2048, cdiv(nq, 256)), 256, 0, s>>>(scratch, nd, Z, M, G::NT, N1, F,
+                                                                             N2, o);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
+int wgrad_lstm_l0(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F, int Fp, int H, float* scratch,
+                  size_t scratch_floats) {
+  if (nd < 1 || nd > 2 || K <= 0 || F >= Fp || !scratch) return -1;
+  const char* ev = getenv("ABCD_WG2");
+  if (ev && ev[0] == '0') return -1;
+  // 32-bit buffer offsets: every operand's K range below 2 GiB
+  if ((size_t)K * M * 4 >= (1ull << 31) || (size_t)K * Fp * 4 >= (1ull << 31) || (size_t)K * H * 4 >= (1ull << 31))
+    return -1;
+  for (int d = 0; d < nd; ++d)
+    if (((uintptr_t)dirs[d].dG | (uintptr_t)dirs[d].X | (uintptr_t)dirs[d].Hprev) & 15) return -1;
+  if (M % 4) return -1;
+  if (Fp == 144 && H == 256) return wgrad_wg2_launch<144, 256>(s, nd, dirs, M, K, F, scratch, scratch_floats);
+  return -1;
+}
+
 template <int MR, int NR, bool AKC, bool BKC>
 static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
                            EpiArgs e, float* scratch, size_t scratch_floats) {

@@ -85,6 +85,33 @@ int reduce_sum(hipStream_t s, const float* x, long n, double* partials, float* o
 
 size_t gemm_scratch_floats_hint(int M, int N, int K);
 
+// The layer-0 LSTM encoder weight gradients of nd <= 2 directions in one
+// launch (gemm_wg2 + one slab reduction): direction d gets
+// w_ih = dG^T X[:, :F], b_ih (and b_hh when set) = dG^T X[:, F] (X's column F
+// holds 1), w_hh = dG^T Hprev; dG: K x M (ld M), X: K x Fp (ld Fp), Hprev: K x H
+// (ld H).  Returns -1 when the shape has no instance (the caller falls back to
+// gemm()), 0 on success, else a hipError_t.
+struct WgDir {
+  const float *dG, *X, *Hprev;
+  float *w_ih, *b_ih, *b_hh, *w_hh;
+};
+struct WgArgs {
+  const float* A[2];
+  const float* B1[2];
+  const float* B2[2];
+  long lda, ldb1, ldb2;
+  int M, K, kps, Z;
+  float* slab;
+};
+struct WgOut {
+  float* w_ih[2];
+  float* b_ih[2];
+  float* b_hh[2];
+  float* w_hh[2];
+};
+int wgrad_lstm_l0(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F, int Fp, int H, float* scratch,
+                  size_t scratch_floats);
+
 // While alive (on this host thread), GEMMs use the co-residency-friendly
 // "side stream" tiling: see abcd_gemm.hip.
 struct GemmSideScope {
@@ -128,7 +155,8 @@ namespace abcd {
 enum TimedKernel {
   TK_STEP = 0, TK_ENC_FWD = 1, TK_ENC_BWD = 2, TK_DEC_FWD = 3, TK_DEC_BWD = 4,
   TK_SAMP_FWD = 5, TK_SAMP_BWD = 6,  // dispatch records only (no live timing)
-  TK_N = 7
+  TK_ENC_WGRAD = 7,                  // the encoder's layer-0 weight-gradient route (dispatch record)
+  TK_N = 8
 };
 bool timing_on();
 void timing_mark(hipStream_t s, int kid);

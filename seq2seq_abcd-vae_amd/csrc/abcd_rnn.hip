@@ -630,7 +630,23 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       set_col_kernel<<<std::max(1, std::min(1024, cdiv(L, 256))), 256, 0, s>>>(w.Xp, Fp, L, F, 1.f);
       ABCD_CHECK_LAUNCH();
     }
-    if (D == 2 && l == 0 && wgrad_stream && wgrad_stream != stream) {
+    int wg2 = -1;  // 0: gemm_wg2 produced every gradient of this layer
+    if (ones_col && G == 4) {
+      WgDir dirs[2] = {};
+      bool all = true;
+      for (int d = 0; d < D; ++d) {
+        const abcd_rnn_g& gr = g->g[l][d];
+        all = all && gr.w_ih && gr.b_ih && gr.w_hh;
+        dirs[d] = WgDir{w.dGX[l][d], w.Xp, w.Hprev[l][d], gr.w_ih, gr.b_ih, gr.b_hh, gr.w_hh};
+      }
+      if (all) {
+        wg2 = wgrad_lstm_l0(s, D, dirs, GH, L, F, Fp, H, w.scratch, w.scratch_floats);
+        if (wg2 > 0) return wg2;
+      }
+    }
+    if (l == 0) note_dispatch(TK_ENC_WGRAD, wg2 == 0 ? "gemm_wg2<%d,%d> x%d" : "gemm split (x6s/x6t)", Fp, H, D);
+    if (wg2 == 0) {
+    } else if (D == 2 && l == 0 && wgrad_stream && wgrad_stream != stream) {
       // the last layer's two directions reduce concurrently: the backward
       // direction on wgrad_stream (forked after the BPTT), the forward one on
       // s, each with half of the split-K scratch; s then waits for
@@ -997,6 +1013,58 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
 static int launch_grid(long n) { return (int)std::max<long>(1, std::min<long>(4096, cdiv(n, 256))); }
 
 }  // namespace abcd
+
+static size_t lstm_wgrad_floats(int nd, int F, int H, int K, size_t* xp_floats) {
+  const size_t xp = (((size_t)K * rup16(F + 1)) + 63) & ~(size_t)63;
+  if (xp_floats) *xp_floats = xp;
+  const size_t M = 4 * (size_t)H;
+  return xp + std::max((size_t)16 * nd * M * (rup16(F + 1) + H), M * std::max(F, H) * 64);
+}
+
+extern "C" size_t abcd_lstm_wgrad_workspace_bytes(int nd, int F, int H, int K) {
+  if (nd < 1 || nd > 2 || F <= 0 || H <= 0 || K < 0) return 0;
+  return lstm_wgrad_floats(nd, F, H, K, nullptr) * 4 + 256;
+}
+
+// C ABI: the LSTM layer's weight gradients (gemm_wg2 when the shape has an
+// instance, else the split GEMM route the encoder backward falls back to)
+extern "C" int abcd_lstm_wgrad(int nd, int F, int H, int K, const float* const* dG, const float* X, long ldx,
+                               const float* const* Hprev, float* const* w_ih, float* const* b_ih,
+                               float* const* b_hh, float* const* w_hh, void* ws, size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(nd >= 1 && nd <= 2 && F > 0 && H > 0 && H % 4 == 0 && K >= 0 && dG && X && ldx >= F && Hprev && w_ih &&
+               b_ih && w_hh && ws);
+  size_t xpf = 0;
+  const size_t need = lstm_wgrad_floats(nd, F, H, K, &xpf);
+  ABCD_REQUIRE(ws_bytes / 4 >= need && ((uintptr_t)ws % 16) == 0);
+  for (int d = 0; d < nd; ++d) ABCD_REQUIRE(dG[d] && Hprev[d] && w_ih[d] && b_ih[d] && w_hh[d]);
+  if (K == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int M = 4 * H, Fp = rup16(F + 1);
+  float* Xp = (float*)ws;
+  float* scratch = Xp + xpf;
+  const size_t scf = need - xpf;
+  // [X | 1 | 0] with the gemm_wg2 row pitch
+  ABCD_TRY((hipError_t)pack2d(s, X, ldx, K, F, false, Xp, Fp, K, Fp));
+  set_col_kernel<<<std::max(1, std::min(1024, cdiv(K, 256))), 256, 0, s>>>(Xp, Fp, K, F, 1.f);
+  ABCD_CHECK_LAUNCH();
+  WgDir dirs[2] = {};
+  for (int d = 0; d < nd; ++d) dirs[d] = WgDir{dG[d], Xp, Hprev[d], w_ih[d], b_ih[d], b_hh ? b_hh[d] : nullptr, w_hh[d]};
+  const int r = wgrad_lstm_l0(s, nd, dirs, M, K, F, Fp, H, scratch, scf);
+  if (r == 0) {
+    note_dispatch(TK_ENC_WGRAD, "gemm_wg2<%d,%d> x%d", Fp, H, nd);
+    return 0;
+  }
+  if (r > 0) return r;
+  note_dispatch(TK_ENC_WGRAD, "gemm split (x6s/x6t)");
+  for (int d = 0; d < nd; ++d) {
+    ABCD_TRY((hipError_t)gemm(s, M, F, K, opKM(dG[d], M, M), opKM(Xp, Fp, F), w_ih[d], F, 1.f, 0.f, nullptr, ACT_NONE,
+                              scratch, scf));
+    ABCD_TRY((hipError_t)gemm(s, M, H, K, opKM(dG[d], M, M), opKM(Hprev[d], H, H), w_hh[d], H, 1.f, 0.f, nullptr,
+                              ACT_NONE, scratch, scf));
+    ABCD_TRY((hipError_t)colsum(s, dG[d], M, K, M, nullptr, b_ih[d], 0.f, scratch, scf, b_hh ? b_hh[d] : nullptr));
+  }
+  return 0;
+}
 
 extern "C" size_t abcd_decoder_workspace_bytes(const abcd_decoder_cfg* c, int T, int L, int B) {
   if (dec_check(c)) return 0;

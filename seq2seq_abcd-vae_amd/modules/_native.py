@@ -143,6 +143,9 @@ _SIGS = {
     "abcd_total_loss": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "abcd_gemm_nt": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p,
                              c_void_p, c_size_t, c_void_p]),
+    "abcd_lstm_wgrad_workspace_bytes": (ctypes.c_size_t, [c_int, c_int, c_int, c_int]),
+    "abcd_lstm_wgrad": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
     "abcd_gemm_tn": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_long, c_void_p,
                              c_size_t, c_void_p]),
     "abcd_linear": (c_int, [c_int, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p, c_int, c_void_p,
@@ -224,7 +227,7 @@ def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
-ENC_FWD, ENC_BWD, DEC_FWD, DEC_BWD, SAMP_FWD, SAMP_BWD = 1, 2, 3, 4, 5, 6
+ENC_FWD, ENC_BWD, DEC_FWD, DEC_BWD, SAMP_FWD, SAMP_BWD, ENC_WGRAD = 1, 2, 3, 4, 5, 6, 7
 
 
 def dispatch():
@@ -232,7 +235,7 @@ def dispatch():
     L = lib()
     return {r: (L.abcd_dispatch_name(k).decode(), int(L.abcd_dispatch_count(k)))
             for r, k in (("enc_fwd", ENC_FWD), ("enc_bwd", ENC_BWD), ("dec_fwd", DEC_FWD), ("dec_bwd", DEC_BWD),
-                                ("samp_fwd", SAMP_FWD), ("samp_bwd", SAMP_BWD))}
+                                ("samp_fwd", SAMP_FWD), ("samp_bwd", SAMP_BWD), ("enc_wgrad", ENC_WGRAD))}
 
 
 def ptr_array(tensors):

@@ -104,6 +104,43 @@ def test_persistent_encoder_vs_stepwise_bench_size(rnn):
         assert torch.equal(g_p[n], g_p2[n]), n
 
 
+def _with_env(key, val, fn):
+    old = os.environ.get(key)
+    os.environ[key] = val
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop(key, None)
+        else:
+            os.environ[key] = old
+
+
+@pytest.mark.parametrize("B,Tmax", [(70, 30), (512, 200)])
+def test_encoder_wgrad_wg2(B, Tmax):
+    """The layer-0 bi-LSTM weight gradients through gemm_wg2 (one launch for
+    both directions: [dW_ih | db | dW_hh] = dG^T [X | 1 | Hprev], F = 129,
+    H = 256) against the split GEMM route (ABCD_WG2=0) and, at the small
+    batch, against torch.nn.LSTM in float64 (model.py:53,60-66)."""
+    from modules import _native as Nn
+    F, H = 129, 256
+    enc = _enc(F, H, "LSTM", 1, True, seed=5)
+    packed = _batch(B, Tmax, F, seed=9)
+    dout = torch.randn(B, enc.hidden_size_total, device="cuda")
+    Nn.lib().abcd_dispatch_reset()
+    out_n, g_n = _run(enc, packed, dout, persist=True)
+    assert Nn.dispatch()["enc_wgrad"] == ("gemm_wg2<144,256> x2", 1)
+    out_o, g_o = _with_env("ABCD_WG2", "0", lambda: _run(enc, packed, dout, persist=True))
+    assert Nn.dispatch()["enc_wgrad"] == ("gemm split (x6s/x6t)", 2)
+    assert torch.equal(out_n, out_o)
+    for n in g_o:
+        assert _rel(g_n[n], g_o[n]) < 1e-5, (n, _rel(g_n[n], g_o[n]))
+    if B <= 128:
+        _, rgrads = _torch_ref(enc, packed, dout)
+        for n, g in rgrads.items():
+            assert _rel(g_n[n], g) < 1e-4, (n, _rel(g_n[n], g))
+
+
 def _fused_run(step, batch, persist, seed=77):
     from modules import _native as Nn, noise
     old = os.environ.get("ABCD_PERSIST")
