@@ -1,9 +1,11 @@
-# GPU box: the gemm_wg2 encoder weight-gradient route -- its tests, the full-shape
-# c2 oracle test, then c2 bench lines with and without it (same box)
+# GPU box: the gemm_wg2 encoder weight-gradient route -- timing alone, its tests,
+# the full-shape c2 oracle test, then c2 bench lines with and without it (same box)
 set -e
 TAG=${1:-wg2}
 mkdir -p gpurun_out/$TAG
 export TMPDIR=/tmp
+timeout -k 10 120 python -u scripts/gemm_shapes.py wg2 > gpurun_out/$TAG/shapes.log 2>&1 || { cat gpurun_out/$TAG/shapes.log; exit 1; }
+cat gpurun_out/$TAG/shapes.log
 timeout -k 10 600 python -u -m pytest tests/test_gpu_persist.py -k "wg2 or bench_size" tests/test_gpu_fullshape.py -x -q --timeout 300 --timeout-method thread > gpurun_out/$TAG/pytest.log 2>&1 || { tail -40 gpurun_out/$TAG/pytest.log; exit 1; }
 tail -3 gpurun_out/$TAG/pytest.log
 for v in 1 0 1 0; do
