@@ -30,6 +30,43 @@ def test_gemm_nt_vs_torch(M, N, K):
     assert err <= 1e-5 * K ** 0.5 * 4 + 1e-5, err
 
 
+@pytest.mark.parametrize("nd,F,H,K", [(2, 129, 256, 65583), (1, 129, 256, 3001), (2, 130, 256, 777), (2, 33, 48, 500),
+                                       (1, 20, 24, 64)])
+def test_lstm_wgrad_vs_torch(nd, F, H, K):
+    """abcd_lstm_wgrad (the LSTM layer's w_ih, b_ih, b_hh, w_hh gradients from
+    the gate gradients, model.py:53,60-66): gemm_wg2 at F <= 143, H = 256
+    (the c2 shape first, both directions), the split-GEMM route elsewhere --
+    against float64 torch."""
+    import ctypes
+    from modules import _native as Nn
+    g = torch.Generator(device="cuda").manual_seed(nd * 7 + F + H + K)
+    M = 4 * H
+    dG = [torch.randn(K, M, device="cuda", generator=g) for _ in range(nd)]
+    X = torch.randn(K, F, device="cuda", generator=g)
+    Hp = [torch.randn(K, H, device="cuda", generator=g) for _ in range(nd)]
+    wih = [torch.full((M, F), float("nan"), device="cuda") for _ in range(nd)]
+    bih = [torch.full((M,), float("nan"), device="cuda") for _ in range(nd)]
+    bhh = [torch.full((M,), float("nan"), device="cuda") for _ in range(nd)]
+    whh = [torch.full((M, H), float("nan"), device="cuda") for _ in range(nd)]
+    ws = Nn.workspace(Nn.lib().abcd_lstm_wgrad_workspace_bytes(nd, F, H, K), "cuda")
+    arr = lambda ts: (ctypes.c_void_p * nd)(*[t.data_ptr() for t in ts])
+    keep = [arr(dG), arr(Hp), arr(wih), arr(bih), arr(bhh), arr(whh)]
+    Nn.lib().abcd_dispatch_reset()
+    Nn.check(Nn.lib().abcd_lstm_wgrad(nd, F, H, K, keep[0], Nn.ptr(X), F, keep[1], keep[2], keep[3], keep[4], keep[5],
+                                      Nn.ptr(ws), ws.numel(), Nn.stream()), "lstm wgrad")
+    torch.cuda.synchronize()
+    route = Nn.dispatch()["enc_wgrad"][0]
+    assert route == (f"gemm_wg2<144,{H}> x{nd}" if (H == 256 and F <= 143 and (F + 16) // 16 * 16 == 144)
+                     else "gemm split (x6s/x6t)"), route
+    rel = lambda a, b: ((a.double() - b).abs().max() / b.abs().max()).item()
+    for d in range(nd):
+        gd = dG[d].double()
+        assert rel(wih[d], gd.t() @ X.double()) < 1e-5
+        assert rel(whh[d], gd.t() @ Hp[d].double()) < 1e-5
+        assert rel(bih[d], gd.sum(0)) < 1e-5
+        assert torch.equal(bih[d], bhh[d])
+
+
 @pytest.mark.parametrize("M,N,K,lda,ldb", [(1024, 256, 64045, 1024, 256), (1024, 129, 20000, 1024, 144),
                                            (129, 256, 7001, 144, 512), (33, 48, 45, 48, 48), (256, 256, 513, 260, 256),
                                            (1024, 1024, 4096, 1024, 1024)])
