@@ -9,8 +9,9 @@ PKG=$(pwd)/seq2seq_abcd-vae_amd
 mkdir -p $OUT
 export TMPDIR=/tmp
 if [ -n "$K" ]; then
+  KS=(); [ "$K" != all ] && KS=(-k "$K")
   ABCD_HIP_LIB=$PKG/$B timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-    $( [ "$K" != all ] && echo -k "$K" ) > $OUT/pytest_B.txt 2>&1
+    "${KS[@]}" > $OUT/pytest_B.txt 2>&1
   tail -3 $OUT/pytest_B.txt
 fi
 for k in 1 2 3; do
