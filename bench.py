@@ -136,6 +136,53 @@ REFERENCE_CPU = {
 }
 
 
+# The same oracle sample timed in the survey container (8 vCPU Xeon, 8 torch
+# threads) by scripts/cpu_calibrate.py: the box-to-box factor between the GPU
+# box's host cores and the machine the reference's own CPU numbers
+# (REFERENCE_CPU) were measured on ("CPU baseline calibration").
+PORT_HERE = {  # round 4: python scripts/cpu_calibrate.py --threads 8 (b = 64 sample, same seeds as below)
+    "c2": {"value": 31.221, "cores": 8}, "c4": {"value": 38.695, "cores": 8},
+    "c5": {"value": 10.853, "cores": 8}, "c5gru": {"value": 12.172, "cores": 8},
+}
+
+
+def oracle_sample(cfg, b=64):
+    """The bounded CPU sample of a workload: b segments of it, seed-1111
+    weights, fixed replayed noise (oracle inputs)."""
+    from oracle import abcd_oracle as O
+    ocfg = O.default_cfg(F=cfg["F"], H=cfg["H"], Hdec=cfg["H"], Hm=cfg["Hm"], D=cfg["D"], K=cfg["K"] or 16,
+                         rnn=cfg["rnn"], plain=cfg["plain"], fplain=cfg["D"],
+                         num_speakers=cfg["spk"] or None, speaker_dim=cfg["sdim"])
+    P = O.init_params(ocfg, 1111)
+    sub = dict(cfg, B=b)
+    batch = make_batch(sub, 4321, "cpu")
+    g = torch.Generator().manual_seed(99)
+    feat = torch.randn(b, cfg["D"], generator=g) if cfg["plain"] else \
+        -torch.empty(b, cfg["K"]).exponential_(generator=g).log()
+    eps = torch.randn(batch["L"], cfg["F"], generator=g)
+    obatch = dict(data=batch["data"], batch_sizes=batch["batch_sizes"], is_offset=batch["is_offset"],
+                  speakers=batch["speakers"])
+    return dict(ocfg=ocfg, P=P, sub=sub, batch=batch, obatch=obatch, feat=feat, eps=eps, b=b)
+
+
+def time_oracle(cfg, smp, target_s=10.0, budget_s=25.0, min_steps=3):
+    """One untimed warm-up oracle step (returned: the parity anchor's
+    reference), then timed steps until ~target_s of CPU work (at least
+    min_steps, stopping past budget_s) -> (warm-up outputs, steps, seconds)."""
+    from oracle import abcd_oracle as O
+    noise = dict(feat=smp["feat"], eps=smp["eps"])
+    ref, _, _, _, _ = O.train_step(smp["P"], smp["obatch"], smp["ocfg"], noise, cfg["N"])
+    steps, t_total = 0, 0.0
+    while steps < min_steps or (min_steps and t_total < target_s):
+        t0 = time.perf_counter()
+        O.train_step(smp["P"], smp["obatch"], smp["ocfg"], noise, cfg["N"])
+        t_total += time.perf_counter() - t0
+        steps += 1
+        if t_total > budget_s:
+            break
+    return ref, steps, t_total
+
+
 def cpu_baseline(cfg, cfg_name, device, target_s=10.0, budget_s=25.0, min_steps=3):
     """Time the CPU oracle on a bounded sample of the same workload: one
     untimed warm-up step, then b = 64 steps until ~target_s of CPU work
@@ -146,35 +193,25 @@ def cpu_baseline(cfg, cfg_name, device, target_s=10.0, budget_s=25.0, min_steps=
     and replayed noise gives the reconstruction-loss (Gaussian emission NLL,
     learning.py:153-157 ``em``) and total-loss relative deltas and the argmax
     category agreement.  Returns (cpu_baseline, parity)."""
-    from oracle import abcd_oracle as O
     from modules import noise as _noise, engine as E
     threads = max(1, min(16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
-    ocfg = O.default_cfg(F=cfg["F"], H=cfg["H"], Hdec=cfg["H"], Hm=cfg["Hm"], D=cfg["D"], K=cfg["K"] or 16,
-                         rnn=cfg["rnn"], plain=cfg["plain"], fplain=cfg["D"],
-                         num_speakers=cfg["spk"] or None, speaker_dim=cfg["sdim"])
-    P = O.init_params(ocfg, 1111)
-    b = 64
-    sub = dict(cfg, B=b)
-    batch = make_batch(sub, 4321, "cpu")
+    smp = oracle_sample(cfg)
+    b, sub, batch, feat, eps = smp["b"], smp["sub"], smp["batch"], smp["feat"], smp["eps"]
     bsz = batch["batch_sizes"]
-    g = torch.Generator().manual_seed(99)
-    feat = torch.randn(b, cfg["D"], generator=g) if cfg["plain"] else \
-        -torch.empty(b, cfg["K"]).exponential_(generator=g).log()
-    eps = torch.randn(batch["L"], cfg["F"], generator=g)
-    noise = dict(feat=feat, eps=eps)
-    obatch = dict(data=batch["data"], batch_sizes=bsz, is_offset=batch["is_offset"], speakers=batch["speakers"])
-    ref, _, _, _, _ = O.train_step(P, obatch, ocfg, noise, cfg["N"])
-    steps, t_total = 0, 0.0
-    while steps < min_steps or (min_steps and t_total < target_s):
-        t0 = time.perf_counter()
-        O.train_step(P, obatch, ocfg, noise, cfg["N"])
-        t_total += time.perf_counter() - t0
-        steps += 1
-        if t_total > budget_s:
-            break
+    ref, steps, t_total = time_oracle(cfg, smp, target_s, budget_s, min_steps)
     rc = REFERENCE_CPU.get(cfg_name)
-    base = {"value": round(steps * b / t_total, 3) if steps else None, "unit": "segments/s", "cores": threads, "kind": "port",
+    value = round(steps * b / t_total, 3) if steps else None
+    here = PORT_HERE.get(cfg_name)
+    calib = None
+    if here and value:
+        ratio = value / here["value"]
+        calib = {"port_here_seg_s": here["value"], "port_here_cores": here["cores"],
+                 "box_over_here": round(ratio, 3),
+                 "reference_on_box_est_seg_s": None if rc is None else round(rc["value"] * ratio, 2),
+                 "what": "the same oracle sample timed in the container the reference's CPU numbers come from "
+                         "(scripts/cpu_calibrate.py); reference_on_box_est = reference_cpu x box_over_here"}
+    base = {"value": value, "calibration": calib, "unit": "segments/s", "cores": threads, "kind": "port",
             "sample": f"{steps} oracle train steps of b={b} segments (T_max={cfg['tmax']}, L={batch['L']} frames) "
                       f"of the {cfg['workload']} workload, torch-CPU fp32, {threads} threads",
             "reference_cpu_seg_s": None if rc is None else rc["value"],
@@ -246,7 +283,7 @@ def dryrun_rank():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE under a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
@@ -255,16 +292,18 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    explicit = args.gpus is not None
+    if not explicit:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
-    if os.environ.get("ABCD_BENCH_DRYRUN"):
-        return dryrun_rank()
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world:
+    if explicit and args.gpus != world:
         raise SystemExit(f"bench.py --gpus {args.gpus} under WORLD_SIZE={world}")
+    if os.environ.get("ABCD_BENCH_DRYRUN"):
+        return dryrun_rank()
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -378,6 +417,27 @@ def load_traffic(kernel, cfg_name):
         return None
 
 
+def load_mfma(kernel, cfg_name):
+    """MFMA utilisation of `kernel` from the rocprofv3 PMC pass committed under
+    profiles/ (scripts/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x
+    GRBM_GUI_ACTIVE / 8), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_mfma.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("config", "c2") != cfg_name:
+            return None
+        return float(t["kernels"][kernel]["mfma_busy"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+# The split-fp32 products (abcd_x6.h) issue 6 bf16 MFMAs per fp32 product:
+# their instruction ceiling is the dense bf16 MFMA peak / 6 in fp32-equivalent FLOPs
+PEAK_BF16_MFMA_TFLOPS = 16 * PEAK_FP32_MFMA_TFLOPS  # MI355X_MICROARCH.md: f32 MFMA = 1/16 of bf16
+X6_CEILING_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
+
+
 def kernel_roofline(step, batches, cfg, run, cfg_name):
     """Roofline of the dominant kernel: the persistent recurrent kernel with
     the largest device time.  Its launches are bracketed live with HIP events
@@ -416,6 +476,9 @@ def kernel_roofline(step, batches, cfg, run, cfg_name):
             "achieved": achieved,
             "peak": PEAK_FP32_MFMA_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
+            "mfma_busy": load_mfma(dom, cfg_name),
+            "x6_ceiling": {"peak": round(X6_CEILING_TFLOPS, 1), "frac": round(achieved / X6_CEILING_TFLOPS, 4),
+                           "what": "bf16 dense MFMA peak / 6: the split-fp32 products' instruction ceiling"},
             "avg_launch_us": d["avg_launch_us"], "launches": d["launches"],
             "flops_per_launch": d["flops_per_launch"], "all_kernels": per}
 

@@ -131,8 +131,9 @@ typedef struct abcd_sampler_cfg {
    * "Shape support" above): the model's own category count (the first
    * valid_categories of the num_categories logit columns are categories, the
    * rest are masked out of every softmax, KL and perplexity) and feature dim
-   * (the logits scale 1 / sqrt(valid_feature_dim), model.py:589).  0: the
-   * padded size itself. */
+   * (the logits scale 1 / sqrt(valid_feature_dim), model.py:589; plain: the
+   * feature columns >= valid_feature_dim draw zero noise, so their samples are
+   * the padding mean 0).  0: the padded size itself. */
   int valid_categories, valid_feature_dim;
 } abcd_sampler_cfg;
 typedef struct abcd_sampler_params {

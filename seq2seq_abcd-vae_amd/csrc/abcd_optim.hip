@@ -131,7 +131,13 @@ extern "C" int abcd_fill_normal(float* out, long n, uint64_t seed, uint64_t offs
   return 0;
 }
 
-extern "C" const char* abcd_version(void) { return "abcd_hip 0.1 gfx950 fp32-mfma16x16x4"; }
+#include "abcd_srchash.h"
+// fp32 arithmetic: split-fp32 "x6" products on the bf16 matrix cores
+// (v_mfma_f32_16x16x32_bf16, abcd_x6.h) for the recurrences and the big GEMMs,
+// exact-fp32 v_mfma_f32_16x16x4_f32 elsewhere; src = ABCD_SRC_HASH (Makefile)
+extern "C" const char* abcd_version(void) {
+  return "abcd_hip 0.4 gfx950 fp32 (split-bf16x6 mfma_16x16x32_bf16 + mfma_16x16x4_f32) src " ABCD_SRC_HASH;
+}
 
 // ---------------------------------------------------------------------------
 // live kernel timing (bench.py): event pairs around recurrent-kernel launches

@@ -39,6 +39,7 @@ namespace abcd {
 
 __device__ unsigned g_persist_status = 0;
 __device__ unsigned g_persist_sticky = 0;       // OR of every status abcd_step_status folded (abcd_device_status)
+__device__ unsigned g_persist_abort = 0;        // a wait of the CURRENT launch timed out (zeroed by persist_reset)
 __device__ unsigned g_spin_limit = 1u << 22;    // polls before a hand-off wait gives up (ABCD_SPIN_LIMIT, tests)
 
 // ---------------------------------------------------------------------------
@@ -131,16 +132,41 @@ DEV void pin(float (&v)[N]) {
 #pragma unroll
   for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
 }
-// Once any wait has timed out (this launch: g_persist_status; an earlier
-// step not yet read back by abcd_device_status: g_persist_sticky) the results
-// are invalid anyway, so a wait that is still unsatisfied after
-// SPIN_PROBE_MASK + 1 polls gives up at once instead of spinning to its own
-// limit: a failed step drains in ~one wait instead of one limit per wait.
-// Probed every 1024 polls only, off the fast path of a healthy hand-off.
+// XCD-local exchange (dec_bwd_fold LX): each member ORs its XCC id bit into
+// its group's registry word before its first publish (a returning atomic, so
+// the publish's vmcnt(0) covers it); after a wait that saw every member's
+// first publish, one bit set = every member shares this XCD's L2
+DEV void xcc_note(unsigned* w) {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  const unsigned old = __hip_atomic_fetch_or(w, 1u << (x & 15u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("" ::"v"(old));
+}
+DEV bool xcc_single(const unsigned* w) {
+  const unsigned m = __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return m != 0u && (m & (m - 1u)) == 0u;
+}
+// hand-off payload store: plain (the line stays in this XCD's L2, where the
+// same-XCD consumers' sc1 loads find it) or write-through (sc1)
+DEV void st_part(__amdgpu_buffer_rsrc_t rs, uint32_t off, f4 v, bool l2) {
+  if (l2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, off, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, off, 0, 16);
+}
+// Once a wait of this launch has timed out the launch's results are invalid
+// anyway, so a wait that is still unsatisfied after SPIN_PROBE_MASK + 1
+// polls gives up at once instead of spinning to its own limit: a failed
+// launch drains in ~one wait instead of one limit per wait.  The word is the
+// launch's own (persist_reset zeroes it in front of every persistent launch),
+// so a timeout never shortens the waits of a later, healthy launch whatever
+// reads or does not read the status words in between.  Probed every 1024
+// polls only, off the fast path of a healthy hand-off.
 constexpr unsigned SPIN_PROBE_MASK = 1023;
 DEV bool spin_abandoned() {
-  return (__hip_atomic_load(&g_persist_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-          __hip_atomic_load(&g_persist_sticky, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+  return __hip_atomic_load(&g_persist_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+DEV void spin_timed_out() {
+  __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&g_persist_abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // lane 0 of the workgroup polls until *cnt >= target (bounded), then the
 // barrier releases every wave
@@ -151,7 +177,7 @@ DEV void group_wait(unsigned* cnt, unsigned target, int pw = 0) {
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > lim) {
-        __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spin_timed_out();
         break;
       }
       if ((spins & SPIN_PROBE_MASK) == 0 && spin_abandoned()) break;
@@ -193,7 +219,7 @@ DEV void flags_wait(const unsigned* fl, int M, unsigned epoch, int pw = 0) {
       if (__all(ok)) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > lim) {
-        if (lane == 0) __hip_atomic_store(&g_persist_status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) spin_timed_out();
         break;
       }
       if ((spins & SPIN_PROBE_MASK) == 0 && spin_abandoned()) break;
@@ -1832,7 +1858,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
 // ---------------------------------------------------------------------------
 // (Forming the dG_{t+1} W_hh half at the end of the previous P2 and carrying
 // it in 16 accumulators into P1 measured 3.34 -> 4.24 ms: register pressure.)
-template <int NXS, int NHS, bool GRU = false, bool P0S = true, bool HX = true>
+template <int NXS, int NHS, bool GRU = false, bool P0S = true, bool HX = true, bool LX = false>
 __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   constexpr int H = NHS * 16, GH = (GRU ? 3 : 4) * H, M = H / 8, NS = NXS + NHS;
@@ -1882,10 +1908,17 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
   if (ismu) stage_b_frag(B1, a.W2mT, Fp, 1, nchx, [&](int) { return 16 * mem; });
   else stage_b_frag(B1, a.W2lT, Fp, 1, nchx, [&](int) { return 16 * (mem - Hm / 16); });
   const float s_em = *a.s_em;
+  // LX: the group's XCC ids are OR-ed into its registry word; once every
+  // member has published P0 of step 0 (P1 wait), a single bit means the
+  // whole group shares one L2 and the partials are stored plain (kept in
+  // the L2) instead of write-through
+  unsigned* const xreg = a.sync + (size_t)2 * a.nrt * PERSIST_SYNC_STRIDE + grp;
+  if (LX && threadIdx.x == 0) xcc_note(xreg);
+  bool lx = false;
   __syncthreads();
   const size_t slot_f = (size_t)a.nrt * NS * 4 * M * 256;  // floats per parity slot
   const __amdgpu_buffer_rsrc_t pr0 = make_rsrc(a.part, (uint32_t)(slot_f * 4));
-  const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
+  const __amdgpu_buffer_rsrc_t pr1 = LX ? pr0 : make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
   // this wave's block of subtile s: (((grp*NS + s)*4 + w)*M + producer)*256 floats
   auto blk = [&](int s) { return (uint32_t)((((size_t)grp * NS + s) * 4 + w) * M) * 1024u; };
   // P0 unit of this wave: dx tile jx (16 F columns) of its 16 rows.  P0S: the
@@ -1980,6 +2013,7 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
     }
     gs.wait(3u * i + 1);
     pin(zpre);
+    if (LX && i == 0) lx = xcc_single(xreg);
     PSTAMP(2);
     if (row0 < bs) {
       f4 acc[2][1];
@@ -2006,8 +2040,7 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
         const f4 wv = W1I[s * 64 + lane];
 #pragma unroll
         for (int k = 0; k < 4; ++k) pa = mfma4(za[k], wv[k], pa);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pa), pw,
-                                               blk(NXS + s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+        st_part(pw, blk(NXS + s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, pa, LX && lx);
       }
       // the dZ stash: read only by the weight-gradient GEMMs after the launch
       st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
@@ -2097,8 +2130,7 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
         const f4* bp = SK + (s * 3) * 64 + lane;
         const f4 v = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
                             __builtin_bit_cast(bf8, bp[128]));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
-                                               blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+        st_part(pw, blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, v, LX && lx);
       }
     }
     gs.publish();
@@ -2234,8 +2266,15 @@ int flush_offsets() {
 }
 
 // a table staged by a call that returned early (error path) is dropped, never
-// copied: its destination workspace may be gone
-static void drop_stale_offsets() { g_pend.on = false; }
+// copied: its destination workspace may be gone.  Its slot is still released,
+// so a group whose last slot is dropped records its events like any other
+// (otherwise the group's next lap would refill slots without waiting for the
+// reads of the earlier ones still queued on the GPU)
+static void drop_stale_offsets() {
+  if (!g_pend.on) return;
+  g_pend.on = false;
+  (void)off_release(g_pend.s, g_pend.dev, g_pend.slot);
+}
 
 int upload_offsets(hipStream_t s, const std::vector<int>& off, int* dst) {
   drop_stale_offsets();
@@ -2295,6 +2334,7 @@ static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
 __global__ __launch_bounds__(256) void persist_reset(unsigned* sync, long nwords, const int* off_src,
                                                      int* off_dst, int noff) {
   const long i0 = (long)blockIdx.x * 256 + threadIdx.x, stride = (long)gridDim.x * 256;
+  if (i0 == 0) __hip_atomic_store(&g_persist_abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (long i = i0; i < nwords / 4; i += stride) {
     uint4 z = make_uint4(0u, 0u, 0u, 0u);
     reinterpret_cast<uint4*>(sync)[i] = z;
@@ -2563,13 +2603,13 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   return 0;
 }
 
-template <int NXS, int NHS, bool GRU, bool P0S, bool HX>
+template <int NXS, int NHS, bool GRU, bool P0S, bool HX, bool LX = false>
 static int launch_dec_bwd_fold_k(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   constexpr int NS = NXS + NHS, M = NHS * 2;
   const size_t lds = (size_t)(NS * 3 + NHS) * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * DSK_WAVE_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_fold<NXS, NHS, GRU, P0S, HX>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_fold<NXS, NHS, GRU, P0S, HX, LX>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
@@ -2577,9 +2617,9 @@ static int launch_dec_bwd_fold_k(hipStream_t s, const PDecBwdArgs& a, bool* laun
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_fold<NXS, NHS, GRU, P0S, HX><<<grid, 256, lds, s>>>(b);
+    dec_bwd_fold<NXS, NHS, GRU, P0S, HX, LX><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_DEC_BWD, "dec_bwd_fold<%d,%d,%s> grid %d", NXS, NHS, GRU ? "GRU" : "LSTM", grid);
+  note_dispatch(TK_DEC_BWD, "dec_bwd_fold<%d,%d,%s%s> grid %d", NXS, NHS, GRU ? "GRU" : "LSTM", LX ? ",LX" : "", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -2592,7 +2632,9 @@ template <int NXS, int NHS, bool GRU = false>
 static int launch_dec_bwd_fold(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   const char* v = getenv("ABCD_P0S");
   const char* x = getenv("ABCD_HX");
-  const bool p0s = !(v && v[0] == '0'), hx = !(x && x[0] == '0');
+  const char* l = getenv("ABCD_LX");
+  const bool p0s = !(v && v[0] == '0'), hx = !(x && x[0] == '0'), lx = l && l[0] == '1' && a.nrt <= 32;
+  if (lx && p0s && hx) return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, true, true>(s, a, launched);
   if (!p0s) return launch_dec_bwd_fold_k<NXS, NHS, GRU, false, false>(s, a, launched);
   if (hx) return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, true>(s, a, launched);
   return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, false>(s, a, launched);

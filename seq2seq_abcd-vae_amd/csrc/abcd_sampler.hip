@@ -268,13 +268,15 @@ __global__ void tanh_bwd_inplace(float* dz, const float* z, long n) {
 }
 
 // ---- plain Gaussian sampler helpers ----------------------------------------
-__global__ void plain_sample(const float* MV, int B, int f, const float* noise, uint64_t seed, uint64_t offset,
-                             float* feats, float* EPS) {
+// fv: the model's feature dim (a zero-padded twin's real f): columns j >= fv
+// are padding, their noise is 0 and their sample mu + 0 = 0 (padding mu = 0)
+__global__ void plain_sample(const float* MV, int B, int f, int fv, const float* noise, uint64_t seed,
+                             uint64_t offset, float* feats, float* EPS) {
   const int n = B * f;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int b = i / f, j = i % f;
     const float mu = MV[(long)b * 2 * f + j], lv = MV[(long)b * 2 * f + f + j];
-    const float e = noise ? noise[i] : philox_normal(seed, offset + (uint64_t)i);
+    const float e = j >= fv ? 0.f : noise ? noise[i] : philox_normal(seed, offset + (uint64_t)i);
     EPS[i] = e;
     feats[i] = mu + __expf(0.5f * lv) * e;
   }
@@ -1070,8 +1072,8 @@ extern "C" int abcd_sampler_sample(const abcd_sampler_cfg* c, const abcd_sampler
   const int D = c->feature_dim, K = c->num_categories;
   if (c->plain) {  // logits = [mean | log_var] (B x 2f); keep the stash self-contained for the backward
     if (logits != w.MV) ABCD_TRY(hipMemcpyAsync(w.MV, logits, (size_t)B * 2 * D * 4, hipMemcpyDeviceToDevice, s));
-    plain_sample<<<std::max(1, std::min(4096, cdiv((long)B * D, 256))), 256, 0, s>>>(w.MV, B, D, noise, seed, offset,
-                                                                                     feats, w.EPS);
+    plain_sample<<<std::max(1, std::min(4096, cdiv((long)B * D, 256))), 256, 0, s>>>(
+        w.MV, B, D, c->valid_feature_dim ? c->valid_feature_dim : D, noise, seed, offset, feats, w.EPS);
     ABCD_CHECK_LAUNCH();
     return 0;
   }

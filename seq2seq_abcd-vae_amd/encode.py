@@ -21,7 +21,7 @@ import pandas as pd
 import torch
 
 import learning
-from modules import data_utils
+from modules import _native, data_utils
 from modules.data_utils import Compose
 
 OUTPUT = "probs"  # encode_logit.py -> "logits", encode_features.py -> "features"
@@ -97,6 +97,7 @@ class Encoder(learning.Learner):
             pending = (host, event, np.asarray(ix, dtype=np.int64))
         if pending is not None:
             write(*pending)
+        _native.op_status.sync("encode_dataset")  # a timed-out persistent launch fails the run, not the table
 
 
 def rename_existing_file(filepath):

@@ -202,6 +202,69 @@ def raise_on_status(status, where):
                              f"(status {int(status)}); the results of that step are invalid")
 
 
+def source_hash():
+    """sha256 (first 16 hex digits) of the sources libabcd_hip.so is built
+    from, concatenated in the Makefile's sorted HASHED order; abcd_version()
+    ends with the same digits when the loaded library was built from this tree."""
+    import hashlib
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+    names = ["abcd_gemm.hip", "abcd_rnn.hip", "abcd_persist.hip", "abcd_sampler.hip", "abcd_optim.hip",
+             "abcd_feat.hip", "abcd_common.h", "abcd_internal.h", "abcd_persist.h", "abcd_x6.h",
+             "../../include/abcd_hip.h"]
+    h = hashlib.sha256()
+    for n in sorted(names):
+        with open(os.path.join(csrc, n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def library_hash():
+    """The source hash abcd_version() of the loaded library reports."""
+    return lib().abcd_version().decode().rsplit(" ", 1)[-1]
+
+
+class _OpStatus:
+    """Bounded-latency timeout check for the op surface (ops.encoder /
+    ops.decoder and their backwards, encode.py): after each persistent
+    launch the device's timeout word is folded into a device slot
+    (abcd_step_status) and copied without blocking into pinned host memory;
+    the next probe reads the previous copy once its event has completed and
+    raises PersistTimeout on a non-zero value.  sync() is the blocking form
+    for the end of a batch of work (encode.py)."""
+
+    def __init__(self):
+        self.host = None
+        self.event = None
+        self.where = None
+
+    def _read(self, block):
+        if self.event is None or not (block or self.event.query()):
+            return
+        self.event.synchronize()
+        self.event = None
+        raise_on_status(float(self.host[0]), self.where)
+
+    def probe(self, device, where):
+        self._read(False)
+        if self.event is not None:  # the previous copy is still in flight; the word keeps any new timeout
+            return
+        if self.host is None:
+            self.host = torch.zeros(1, pin_memory=True)
+        slot = torch.empty(1, device=device)
+        check(lib().abcd_step_status(ptr(slot), stream()), "status probe")
+        self.host.copy_(slot, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record()
+        self.where = where
+
+    def sync(self, where):
+        self._read(True)
+        raise_on_status(lib().abcd_device_status(), where)
+
+
+op_status = _OpStatus()
+
+
 def check(rc, what):
     if rc != 0:
         if rc == ABCD_EINVAL:

@@ -329,8 +329,15 @@ class StatusWatch:
     ``spin_abandoned`` in abcd_persist.hip, so the steps in between are cheap.)
     """
 
-    def __init__(self, device, every=16, where="training batch"):
+    def __init__(self, device, every=16, where="training batch", group=None):
+        """group: under data parallelism the process group whose ranks step
+        together; each window's STATUS is MAX-reduced over it (one 4-byte
+        all-reduce per window), so a timeout on one rank stops every rank."""
         self.every, self.where = int(every), where
+        ws = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
+        self.group = group if ws > 1 else None
+        if ws > 1 and group is None:
+            self.group = torch.distributed.group.WORLD
         self.host = torch.zeros(1, pin_memory=torch.cuda.is_available())
         self.event = None
         self.first = 0   # first record of the window in flight
@@ -351,6 +358,8 @@ class StatusWatch:
             return
         self._read()
         window = torch.stack(records[self.done:n])[:, STATUS].amax().reshape(1)
+        if self.group is not None:  # every rank raises at the same batch (no rank left in the next all-reduce)
+            torch.distributed.all_reduce(window, op=torch.distributed.ReduceOp.MAX, group=self.group)
         self.host.copy_(window, non_blocking=True)
         self.event = torch.cuda.Event()
         self.event.record()

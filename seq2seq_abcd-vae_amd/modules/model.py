@@ -336,7 +336,8 @@ class _SamplerBase(torch.nn.Module):
         """A padded twin (padding.sampler_twin) carries its model's real (K, D)."""
         vs = self.__dict__.get("valid_sizes")
         if vs is not None:
-            c.valid_categories, c.valid_feature_dim = (int(vs[0]), int(vs[1])) if not c.plain else (0, 0)
+            # plain: no categories; the real feature dim masks the padding columns' noise (plain_sample)
+            c.valid_categories, c.valid_feature_dim = (int(vs[0]), int(vs[1])) if not c.plain else (0, int(vs[1]))
         return c
 
     def _mlp_weights(self):
@@ -499,7 +500,8 @@ class Sampler(_SamplerBase):
         B, f = mu.shape
         mp = _module_pad(self, "sampler")
         cfg = self._cfg_list() if mp is None else mp.cfg
-        # padding columns draw zero noise, so their samples are exactly 0 as well
+        # padding columns (a zero-padded twin's, valid_feature_dim) draw zero noise in both noise modes,
+        # so their samples are exactly mu = 0 (plain_sample); only the real f columns are returned
         nt, seed, off = _noise.normal(B, f, mu.device, width=mv.shape[1] // 2)
         return ops.sampler_sample(mv, None, cfg, 0, 1.0, nt, ops._i64(seed), ops._i64(off))[0][:, :f]
 

@@ -113,6 +113,7 @@ def encoder(data: Tensor, batch_sizes: Tensor, weights: List[Tensor], noise: Lis
     out = torch.empty(pk.B, _enc_out_width(cfg), device=data.device)
     N.check(L.abcd_encoder_forward_dropout(c, _enc_struct(cfg, weights), pk, N.ptr_array(list(noise) or None), N.ptr(out),
                                            N.ptr(ws), ws.numel(), N.stream()), "encoder forward")
+    N.op_status.probe(data.device, "encoder forward")
     return [out, ws]
 
 
@@ -131,6 +132,7 @@ def encoder_bwd(data: Tensor, batch_sizes: Tensor, weights: List[Tensor], noise:
     N.check(N.lib().abcd_encoder_backward_dropout(c, _enc_struct(cfg, weights), pk, N.ptr_array(list(noise) or None),
                                                   N.ptr(d_out.contiguous()), _enc_struct(cfg, grads), N.ptr(ws),
                                                   ws.numel(), N.stream(), None), "encoder backward")
+    N.op_status.probe(data.device, "encoder backward")
     return grads
 
 
@@ -404,6 +406,7 @@ def decoder(features: Tensor, batch_sizes: Tensor, speaker: Optional[Tensor], gt
                                             N.ptr(xmask), _u64(seed), _u64(offset), N.ptr(flat), N.ptr(mu),
                                             N.ptr(lv), N.ptr(offl), N.ptr(losses), N.ptr(ws), ws.numel(),
                                             N.stream()), "decoder forward")
+    N.op_status.probe(dev, "decoder forward")
     return [losses[0].clone(), losses[1].clone(), flat, mu, lv, offl, ws]
 
 
@@ -432,6 +435,7 @@ def decoder_bwd(features: Tensor, batch_sizes: Tensor, speaker: Optional[Tensor]
                                                   N.ptr(d_off.reshape(()).contiguous()), N.ptr(d_features),
                                                   _dec_struct(cfg, grads), N.ptr(ws), ws.numel(), N.stream(), None),
             "decoder backward")
+    N.op_status.probe(dev, "decoder backward")
     return [d_features] + grads
 
 

@@ -45,7 +45,10 @@ Fixtures written (all small, committed):
   by the reference CLI (small widths, toy data, 1 epoch) and the reference
   ``encode.py``'s probabilities for it.
 
-Usage: ``python tests/golden/make_golden.py [--only small|prod|toy|cli|ckpt]``.
+* ``ref_ckpt_plain.pt`` + ``ref_plain_encode{,_named}.csv``  a plain-VAE
+  checkpoint written by plain/learning.py and plain/encode.py's tables for it.
+
+Usage: ``python tests/golden/make_golden.py [--only small|prod|toy|cli|ckpt|ckpt_plain]``.
 """
 import argparse
 import hashlib
@@ -591,13 +594,40 @@ def run_ckpt():
     print("wrote ref_ckpt_small.pt / ref_ckpt_small_encode.npz", probs.argmax(1))
 
 
+PLAIN_CKPT_FLAGS = ["-e", "1", "-b", "4", "-R", "LSTM", "-f", "8", "--encoder_rnn_hidden_size", "32",
+                    "--decoder_rnn_hidden_size", "32", "--mlp_hidden_size", "32"]
+
+
+def run_ckpt_plain():
+    """A plain-VAE checkpoint.pt written by the reference CLI
+    (plain/learning.py) on the toy data at small widths, and the tables the
+    reference's plain/encode.py writes for it: without parameter names
+    (-b 3) and with ``-p mean,log_variance`` (-b 4).  The CSVs are the
+    reference's output files as written (data: data_ix, parameter_name,
+    feature_dim, parameter_value + the annotation columns)."""
+    import shutil
+    root = os.path.join(REF, "toy_data")
+    ann = os.path.join(root, "annotation_20170806-080002_89.2-94.22.csv")
+    with tempfile.TemporaryDirectory() as tmp:
+        save_root = os.path.join(tmp, "ckpt")
+        subprocess.run([sys.executable, __file__, "--child", "plain", "learning.py", "--", root, ann, "-S",
+                        save_root, "-j", "run"] + PLAIN_CKPT_FLAGS, check=True)
+        ckpt = os.path.join(save_root, "run", "checkpoint.pt")
+        shutil.copy(ckpt, os.path.join(HERE, "ref_ckpt_plain.pt"))
+        for out, extra in (("ref_plain_encode.csv", ["-b", "3"]),
+                           ("ref_plain_encode_named.csv", ["-b", "4", "-p", "mean,log_variance"])):
+            subprocess.run([sys.executable, __file__, "--child", "plain", "encode.py", "--", ckpt, root, ann, "1.0",
+                            "-S", os.path.join(HERE, out)] + extra, check=True)
+    print("wrote ref_ckpt_plain.pt / ref_plain_encode*.csv")
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         vdir, script = sys.argv[2], sys.argv[3]
         cli_child(vdir, script, sys.argv[5:])
         return
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=["small", "prod", "toy", "cli", "ckpt"], default=None)
+    ap.add_argument("--only", choices=["small", "prod", "toy", "cli", "ckpt", "ckpt_plain"], default=None)
     ap.add_argument("--variant", default=None)
     ap.add_argument("--case", default=None, help="cli: regenerate only this trajectory")
     a = ap.parse_args()
@@ -627,6 +657,8 @@ def main():
         run_cli(a.case)
     if a.only in (None, "ckpt"):
         run_ckpt()
+    if a.only in (None, "ckpt_plain"):
+        run_ckpt_plain()
 
 
 if __name__ == "__main__":

@@ -37,3 +37,18 @@ def test_gpus_mismatch_under_launcher_is_an_error():
     p = _run(["--gpus", "4"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "WORLD_SIZE=2" in (p.stderr + p.stdout)
+
+
+def test_driver_launcher_without_gpus_flag():
+    # the driver's own form: torch.distributed.run --nproc-per-node N bench.py (no --gpus):
+    # --gpus defaults to WORLD_SIZE instead of failing the rank
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update({"ABCD_BENCH_DRYRUN": "1", "OMP_NUM_THREADS": "1"})
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
+                        "--steps", "2", "--warmup", "1"], env=env, cwd=REPO, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and lines[0]["world_size"] == 2 and lines[0]["env_world"] == 2, p.stdout

@@ -84,3 +84,30 @@ def test_dataloader_featurizer_batches(tmp_path):
         assert torch.equal(hb, db)
         assert torch.equal(ho, do)
         assert (hd - dd).abs().max().item() < 1e-3
+
+
+def test_featurizer_matches_reference_toy_batch():
+    """Pinned to the REFERENCE pipeline's own output: the first toy training
+    batch as the reference's data_utils built it (Data_Parser -> STFT ->
+    log_and_normalize -> DataLoader pop-from-end -> pack_sequence;
+    tests/golden/toy_step.npz, make_golden.py:run_toy_step) against
+    DeviceFeaturizer on the same segments' raw samples: identical
+    batch_sizes and is_offset, log-amplitudes within 1e-4."""
+    from modules import data_utils as du
+    from golden_io import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "toy_step.npz"), allow_pickle=False)
+    toy = os.path.join(GOLDEN, "toy_data")
+    parser = du.Data_Parser(toy, os.path.join(toy, "annotation_20170806-080002_89.2-94.22.csv"))
+    fs = parser.get_sample_freq()
+    frame, hop = int(np.floor(0.008 * fs)), int(np.floor(0.004 * fs))
+    raw = parser.get_data(data_type="train", transform=None)
+    ixs = [int(i) for i in z["ixs"]]
+    assert list(raw.sort_indices_by_length(ixs)) == ixs  # the fixture's batch is already in packed order
+    waves = [raw[ix][0] for ix in ixs]
+    fz = du.DeviceFeaturizer(frame, hop, eps=2 ** (-15), normalizer=1.0, device="cuda")
+    data, bs, is_off = fz(waves)
+    torch.cuda.synchronize()
+    assert torch.equal(bs, torch.from_numpy(z["batch_sizes"]))
+    assert torch.equal(is_off.cpu(), torch.from_numpy(z["is_offset"]))
+    err = (data.cpu() - torch.from_numpy(z["data"])).abs().max().item()
+    assert err <= 1e-4, err

@@ -46,6 +46,8 @@ KERNELS = {
 
 if os.environ.get("ABCD_DECBWD", "").startswith("s"):  # the unfolded decoder BPTT (A/B runs)
     KERNELS = {r: k[:3] + (f"dec_bwd_sk<9,16,16,{r}>",) for r, k in KERNELS.items()}
+if os.environ.get("ABCD_LX") == "1":  # the XCD-local exchange form of the decoder BPTT (A/B runs)
+    KERNELS = {r: k[:3] + (k[3].replace(">", ",LX>"),) for r, k in KERNELS.items()}
 
 # (bench config, batch, seed of the synthetic batch)
 CASES = [("c2", 512, 2024), ("c4", 512, 2025), ("c5", 128, 2026), ("c5gru", 128, 2027)]

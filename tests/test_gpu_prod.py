@@ -36,6 +36,9 @@ EXPECT = {
 if os.environ.get("ABCD_DECBWD", "").startswith("s"):  # the unfolded decoder BPTT (A/B runs)
     for _r in EXPECT:
         EXPECT[_r]["dec_bwd"] = f"dec_bwd_sk<9,16,16,{_r}>"
+if os.environ.get("ABCD_LX") == "1":  # the XCD-local exchange form of the decoder BPTT (A/B runs)
+    for _r in EXPECT:
+        EXPECT[_r]["dec_bwd"] = EXPECT[_r]["dec_bwd"].replace(">", ",LX>")
 
 
 def _noise(inp):
@@ -151,3 +154,32 @@ def test_persist_timeout_is_fatal(monkeypatch):
     assert float(sc[engine.STATUS]) == 0.0
     assert N.lib().abcd_device_status() == 0
     engine.check_status(sc.cpu())
+
+
+def test_op_surface_timeout_does_not_poison_later_launches(monkeypatch):
+    """a hand-off timeout on the op surface (ops.encoder through
+    the nn.Module, which never runs FusedStep's status fold) is reported by
+    the op-surface probe (PersistTimeout), and the NEXT launch with the
+    default spin bound is unaffected: its waits are not abandoned because of
+    the earlier launch's timeout (the abort word is per launch), so it
+    reproduces the healthy result bit for bit."""
+    from modules import _native as N
+    meta, _ = load_prod("lstm_k128")
+    enc, samp, dec = build_product(meta, "cuda")
+    inp = prod_inputs(meta)
+    packed = torch.nn.utils.rnn.PackedSequence(inp["data"].cuda(), inp["batch_sizes"])
+    N.op_status.sync("setup")
+    with torch.no_grad():
+        good = enc(packed).clone()
+        torch.cuda.synchronize()
+        N.op_status.sync("healthy launch")
+        monkeypatch.setenv("ABCD_SPIN_LIMIT", "0")
+        enc(packed)
+        torch.cuda.synchronize()
+        with pytest.raises(N.PersistTimeout):
+            N.op_status.sync("forced timeout")
+        monkeypatch.delenv("ABCD_SPIN_LIMIT")
+        again = enc(packed)
+        torch.cuda.synchronize()
+    N.op_status.sync("launch after the timeouts")
+    assert torch.equal(again, good)

@@ -115,3 +115,46 @@ def test_reference_checkpoint_encodes_like_reference(tmp_path):
     probs[df["data_ix"].to_numpy(), df["category_ix"].to_numpy().astype(int)] = df["prob"].to_numpy()
     assert np.abs(probs - z["probs"]).max() <= 1e-5
     assert (probs.argmax(1) == z["argmax"]).all()
+
+
+@pytest.mark.parametrize("ref_csv,flags", [("ref_plain_encode.csv", ["-b", "3"]),
+                                           ("ref_plain_encode_named.csv", ["-b", "4", "-p", "mean,log_variance"])])
+def test_reference_plain_checkpoint_encodes_like_reference(tmp_path, ref_csv, flags):
+    """plain/encode.py:12-61 drop-in: a plain-VAE checkpoint WRITTEN BY THE
+    REFERENCE CLI (tests/golden/ref_ckpt_plain.pt, make_golden.py:run_ckpt_plain)
+    is opened through plain_learning.Learner.retrieve_model and plain_encode.py
+    writes the reference's table: identical columns and column order, identical
+    (data_ix, parameter_name, feature_dim) rows in the same order, identical
+    annotation columns (speaker mapped as plain/modules/data_utils.py:17-22),
+    parameter values (encoder + plain Sampler MLP kernels) <= 1e-5."""
+    import numpy as np
+    import plain_encode
+    ref = pd.read_csv(os.path.join(GOLDEN, ref_csv))
+    out = plain_encode.main([os.path.join(GOLDEN, "ref_ckpt_plain.pt"), TOY, ANN, "1.0", "-S",
+                             os.path.join(str(tmp_path), "enc.csv")] + flags)
+    got = pd.read_csv(out)
+    assert list(got.columns) == list(ref.columns)
+    assert len(got) == len(ref)
+    for c in ref.columns:
+        if c == "parameter_value":
+            continue
+        assert got[c].astype(str).tolist() == ref[c].astype(str).tolist(), c
+    err = np.abs(got["parameter_value"].to_numpy() - ref["parameter_value"].to_numpy()).max()
+    assert err <= 1e-5, err
+
+
+def test_toy_trajectory_gpu_featurize_matches_reference(tmp_path):
+    """The reference CLI's lstm_softmax_e2 trajectory with the STFT + log +
+    packing on the GPU (--gpu_featurize, DeviceFeaturizer) instead of the host
+    torch.stft chain: every logged training batch loss and the epoch totals
+    within 1e-4 of the reference run (data_utils.py:88-103, 124-139, 165-182)."""
+    ka = known_answers()["lstm_softmax_e2"]
+    learner, _ = _run(tmp_path, ka["flags"] + ["--gpu_featurize"], "gpufeat")
+    hist = learner.history
+    for e in range(2):
+        assert _rel(hist[e]["train"]["total"], ka["train_total"][e]) < 1e-4, (e, hist[e]["train"], ka)
+        assert _rel(hist[e]["valid"]["total"], ka["valid_total"][e]) < 1e-4, (e, hist[e]["valid"], ka)
+    losses = [x for e in range(2) for x in hist[e]["train"]["batch_loss"]]
+    assert len(losses) == len(ka["batch_loss"])
+    for a, b in zip(losses, ka["batch_loss"]):
+        assert _rel(a, b) < 1e-4

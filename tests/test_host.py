@@ -31,6 +31,8 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, s), s
     assert set(N.EXPORTED) == set(syms), set(N.EXPORTED) ^ set(syms)
     assert b"gfx950" in lib.abcd_version()
+    from modules import _native
+    assert _native.library_hash() == _native.source_hash()  # the loaded library is this tree's build
 
 
 def test_workspace_queries_without_gpu():
@@ -156,3 +158,51 @@ def test_custom_ops_registered():
         assert schema.startswith(f"abcd::{name}("), schema
         assert "(a!)" not in schema and "(a1!)" not in schema, schema  # functional: no mutated inputs
     assert ops._u64(ops._i64(0xF00DF00DF00DF00D)) == 0xF00DF00DF00DF00D
+
+
+def test_reference_plain_checkpoint_oracle_encode():
+    """The plain-VAE checkpoint written by the reference CLI
+    (tests/golden/ref_ckpt_plain.pt) loads with weights_only=True into the
+    product's plain modules, and the oracle's encoder + plain sampler
+    (oracle/abcd_oracle.py: encoder_forward, plain_params) on the host data
+    pipeline reproduce the reference plain/encode.py table
+    (tests/golden/ref_plain_encode.csv) to <= 1e-5: this pins the checker the
+    GPU test of plain_encode.py stands beside."""
+    import numpy as np
+    import pandas as pd
+    from modules import data_utils, model as M
+    from modules.data_utils import Compose
+    from oracle import abcd_oracle as O
+    g = os.path.join(REPO, "tests", "golden")
+    ck = torch.load(os.path.join(g, "ref_ckpt_plain.pt"), map_location="cpu", weights_only=True)
+    enc = M.RNN_Variational_Encoder(**ck["encoder_init_parameters"])
+    samp = M.Sampler(**ck["feature_sampler_init_parameters"])
+    enc.load_state_dict(ck["encoder"], strict=False)
+    samp.load_state_dict(ck["feature_sampler"])
+    P = {f"encoder/{k}": v for k, v in ck["encoder"].items()}
+    P.update({f"feature_sampler/{k}": v for k, v in ck["feature_sampler"].items()})
+    ei = ck["encoder_init_parameters"]
+    cfg = dict(bidirectional=ei.get("bidirectional", True), layers=ei.get("rnn_layers", 1),
+               rnn=ei.get("rnn_type", "LSTM"))
+    toy = os.path.join(g, "toy_data")
+    parser = data_utils.Data_Parser(toy, os.path.join(toy, "annotation_20170806-080002_89.2-94.22.csv"))
+    fs = parser.get_sample_freq()
+    frame, hop = int(np.floor(0.008 * fs)), int(np.floor(0.004 * fs))
+    tfm = Compose([data_utils.ToTensor(), data_utils.STFT(frame, hop),
+                   data_utils.Transform(lambda x: (x + 2 ** (-15)).log() / 1.0)])
+    ref = pd.read_csv(os.path.join(g, "ref_plain_encode.csv"))
+    f = ck["feature_sampler_init_parameters"]["output_size"]
+    want = {}
+    for p in (0, 1):
+        sub = ref[ref.parameter_name == p]
+        want[p] = sub.pivot(index="data_ix", columns="feature_dim", values="parameter_value").to_numpy()
+    got = {0: np.zeros_like(want[0]), 1: np.zeros_like(want[1])}
+    with torch.no_grad():
+        for packed, _, _, ix in data_utils.DataLoader(parser.get_data(transform=tfm), batch_size=3):
+            h = O.encoder_forward(P, packed.data, packed.batch_sizes, cfg)
+            mu, lv = O.plain_params(P, h)
+            got[0][np.asarray(ix)] = mu.numpy()
+            got[1][np.asarray(ix)] = lv.numpy()
+    assert want[0].shape[1] == f
+    for p in (0, 1):
+        assert np.abs(got[p] - want[p]).max() <= 1e-5, p
