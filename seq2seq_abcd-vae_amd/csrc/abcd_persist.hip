@@ -132,26 +132,6 @@ DEV void pin(float (&v)[N]) {
 #pragma unroll
   for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k]));
 }
-// XCD-local exchange (dec_bwd_fold LX): each member ORs its XCC id bit into
-// its group's registry word before its first publish (a returning atomic, so
-// the publish's vmcnt(0) covers it); after a wait that saw every member's
-// first publish, one bit set = every member shares this XCD's L2
-DEV void xcc_note(unsigned* w) {
-  unsigned x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  const unsigned old = __hip_atomic_fetch_or(w, 1u << (x & 15u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("" ::"v"(old));
-}
-DEV bool xcc_single(const unsigned* w) {
-  const unsigned m = __builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  return m != 0u && (m & (m - 1u)) == 0u;
-}
-// hand-off payload store: plain (the line stays in this XCD's L2, where the
-// same-XCD consumers' sc1 loads find it) or write-through (sc1)
-DEV void st_part(__amdgpu_buffer_rsrc_t rs, uint32_t off, f4 v, bool l2) {
-  if (l2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, off, 0, 0);
-  else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, off, 0, 16);
-}
 // Once a wait of this launch has timed out the launch's results are invalid
 // anyway, so a wait that is still unsatisfied after SPIN_PROBE_MASK + 1
 // polls gives up at once instead of spinning to its own limit: a failed
@@ -1858,7 +1838,7 @@ __global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
 // ---------------------------------------------------------------------------
 // (Forming the dG_{t+1} W_hh half at the end of the previous P2 and carrying
 // it in 16 accumulators into P1 measured 3.34 -> 4.24 ms: register pressure.)
-template <int NXS, int NHS, bool GRU = false, bool P0S = true, bool HX = true, bool LX = false>
+template <int NXS, int NHS, bool GRU = false, bool P0S = true, bool HX = true>
 __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   constexpr int H = NHS * 16, GH = (GRU ? 3 : 4) * H, M = H / 8, NS = NXS + NHS;
@@ -1908,17 +1888,10 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
   if (ismu) stage_b_frag(B1, a.W2mT, Fp, 1, nchx, [&](int) { return 16 * mem; });
   else stage_b_frag(B1, a.W2lT, Fp, 1, nchx, [&](int) { return 16 * (mem - Hm / 16); });
   const float s_em = *a.s_em;
-  // LX: the group's XCC ids are OR-ed into its registry word; once every
-  // member has published P0 of step 0 (P1 wait), a single bit means the
-  // whole group shares one L2 and the partials are stored plain (kept in
-  // the L2) instead of write-through
-  unsigned* const xreg = a.sync + (size_t)2 * a.nrt * PERSIST_SYNC_STRIDE + grp;
-  if (LX && threadIdx.x == 0) xcc_note(xreg);
-  bool lx = false;
   __syncthreads();
   const size_t slot_f = (size_t)a.nrt * NS * 4 * M * 256;  // floats per parity slot
   const __amdgpu_buffer_rsrc_t pr0 = make_rsrc(a.part, (uint32_t)(slot_f * 4));
-  const __amdgpu_buffer_rsrc_t pr1 = LX ? pr0 : make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
+  const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
   // this wave's block of subtile s: (((grp*NS + s)*4 + w)*M + producer)*256 floats
   auto blk = [&](int s) { return (uint32_t)((((size_t)grp * NS + s) * 4 + w) * M) * 1024u; };
   // P0 unit of this wave: dx tile jx (16 F columns) of its 16 rows.  P0S: the
@@ -2013,7 +1986,6 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
     }
     gs.wait(3u * i + 1);
     pin(zpre);
-    if (LX && i == 0) lx = xcc_single(xreg);
     PSTAMP(2);
     if (row0 < bs) {
       f4 acc[2][1];
@@ -2040,7 +2012,8 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
         const f4 wv = W1I[s * 64 + lane];
 #pragma unroll
         for (int k = 0; k < 4; ++k) pa = mfma4(za[k], wv[k], pa);
-        st_part(pw, blk(NXS + s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, pa, LX && lx);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pa), pw,
+                                               blk(NXS + s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
       }
       // the dZ stash: read only by the weight-gradient GEMMs after the launch
       st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
@@ -2130,7 +2103,8 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
         const f4* bp = SK + (s * 3) * 64 + lane;
         const f4 v = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
                             __builtin_bit_cast(bf8, bp[128]));
-        st_part(pw, blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, v, LX && lx);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
+                                               blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
       }
     }
     gs.publish();
@@ -2603,13 +2577,13 @@ static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched
   return 0;
 }
 
-template <int NXS, int NHS, bool GRU, bool P0S, bool HX, bool LX = false>
+template <int NXS, int NHS, bool GRU, bool P0S, bool HX>
 static int launch_dec_bwd_fold_k(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   constexpr int NS = NXS + NHS, M = NHS * 2;
   const size_t lds = (size_t)(NS * 3 + NHS) * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * DSK_WAVE_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_fold<NXS, NHS, GRU, P0S, HX, LX>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_fold<NXS, NHS, GRU, P0S, HX>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecBwdArgs b = a;
@@ -2617,9 +2591,9 @@ static int launch_dec_bwd_fold_k(hipStream_t s, const PDecBwdArgs& a, bool* laun
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_fold<NXS, NHS, GRU, P0S, HX, LX><<<grid, 256, lds, s>>>(b);
+    dec_bwd_fold<NXS, NHS, GRU, P0S, HX><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_DEC_BWD, "dec_bwd_fold<%d,%d,%s%s> grid %d", NXS, NHS, GRU ? "GRU" : "LSTM", LX ? ",LX" : "", grid);
+  note_dispatch(TK_DEC_BWD, "dec_bwd_fold<%d,%d,%s> grid %d", NXS, NHS, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -2632,9 +2606,7 @@ template <int NXS, int NHS, bool GRU = false>
 static int launch_dec_bwd_fold(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   const char* v = getenv("ABCD_P0S");
   const char* x = getenv("ABCD_HX");
-  const char* l = getenv("ABCD_LX");
-  const bool p0s = !(v && v[0] == '0'), hx = !(x && x[0] == '0'), lx = l && l[0] == '1' && a.nrt <= 32;
-  if (lx && p0s && hx) return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, true, true>(s, a, launched);
+  const bool p0s = !(v && v[0] == '0'), hx = !(x && x[0] == '0');
   if (!p0s) return launch_dec_bwd_fold_k<NXS, NHS, GRU, false, false>(s, a, launched);
   if (hx) return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, true>(s, a, launched);
   return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, false>(s, a, launched);
@@ -2701,6 +2673,32 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
 }
 
 }  // namespace abcd
+
+// diagnostics only (not in the public header): which XCD (HW_REG_XCC_ID) and
+// which CU (HW_REG_HW_ID) each workgroup of a one-per-CU grid runs on, the
+// placement the persistent kernels' group_role assumes (blocks b and b + 8
+// share an XCD)
+namespace abcd {
+__global__ __launch_bounds__(256) void xcc_map_kernel(unsigned* out) {
+  extern __shared__ float pad_lds[];
+  if (threadIdx.x == 0) {
+    unsigned x, h;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(h));
+    pad_lds[0] = 0.f;
+    out[2 * blockIdx.x] = x;
+    out[2 * blockIdx.x + 1] = h;
+  }
+}
+}  // namespace abcd
+extern "C" int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream) {
+  const size_t lds = 100 * 1024;  // one workgroup per CU, as the persistent kernels
+  if (hipFuncSetAttribute((const void*)abcd::xcc_map_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+      hipSuccess)
+    return -1;
+  abcd::xcc_map_kernel<<<blocks, 256, lds, (hipStream_t)stream>>>(dev_out);
+  return (int)hipGetLastError();
+}
 
 // diagnostics only (not in the public header): stamp buffer for the
 // persistent kernels selected by mask, grid x T x 5 u64, or null to disable

@@ -36,9 +36,6 @@ EXPECT = {
 if os.environ.get("ABCD_DECBWD", "").startswith("s"):  # the unfolded decoder BPTT (A/B runs)
     for _r in EXPECT:
         EXPECT[_r]["dec_bwd"] = f"dec_bwd_sk<9,16,16,{_r}>"
-if os.environ.get("ABCD_LX") == "1":  # the XCD-local exchange form of the decoder BPTT (A/B runs)
-    for _r in EXPECT:
-        EXPECT[_r]["dec_bwd"] = EXPECT[_r]["dec_bwd"].replace(">", ",LX>")
 
 
 def _noise(inp):
