@@ -88,7 +88,11 @@ def main():
                 return float(v.median()) if v.numel() else float("nan")
             # critical path: per (group, step) the LAST member to reach each
             # stamp (groups = blockIdx % 8 under the fallback roles)
-            g8 = st[:, :, :6].reshape(32, 8, T, 6)  # [member][group][step][stamp]
+            w16 = name == "dec_bwd" and "w16" in N.dispatch().get("dec_bwd", ("",))[0]
+            if w16:  # dec_bwd_w16: 16 groups of 16 members (block b: member (b >> 3) % 16, group b % 8 + 8 (b >> 7))
+                g8 = st[:, :, :6].reshape(2, 16, 8, T, 6).permute(1, 0, 2, 3, 4).reshape(16, 16, T, 6)
+            else:
+                g8 = st[:, :, :6].reshape(32, 8, T, 6)  # [member][group][step][stamp]
             okg = (g8 > 0).all(dim=3).all(dim=0)
             last = g8.max(dim=0).values  # [group][step][stamp]
             first = g8.min(dim=0).values
@@ -101,7 +105,7 @@ def main():
                   f"3->4 {cp(4, 3):.0f}  4->5 {cp(5, 4):.0f}  5->next0 {float(nxt[okn].median()):.0f}")
             for k in (1, 3, 5):
                 am = g8[:, :, :, k].argmax(dim=0)[okg]
-                h = torch.bincount(am, minlength=32)
+                h = torch.bincount(am, minlength=g8.shape[0])
                 top = torch.argsort(h, descending=True)[:6]
                 print(f"   last member at stamp {k}: " + " ".join(f"m{int(m)}:{int(h[m])}" for m in top))
             sp = [(last[:, :, k] - first[:, :, k])[okg] for k in range(6)]

@@ -75,6 +75,7 @@ struct PDecFwdArgs {
 //   P2: dh = dZ W1cat + dh_rec + dh_offset -> LSTM cell backward -> dG_t
 struct PDecBwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
+  int B;                           // batch (rows of step 0): the 32-row groups of dec_bwd_w16
   int flags;                       // hand-off form: 1 per-member flags, 0 group counter
   const int* off;
   unsigned* sync;
@@ -106,7 +107,8 @@ inline size_t persist_part_floats(int nd, int B, int H) {
 // group counters + the role registry (abcd_persist.hip: 8 XCD ticket lines + 1
 // arrival line) + a second counter per group (dec_bwd_sk: split-K partials
 // drained) + 64 per-member flag lines per group (flag-form hand-offs)
-inline size_t persist_sync_uints(int nd, int B) { return (size_t)(66 * persist_groups(nd, B) + 9) * PERSIST_SYNC_STRIDE; }
+// sized for 32-row groups (dec_bwd_w16), a superset of the 64-row layouts
+inline size_t persist_sync_uints(int nd, int B) { return (size_t)(66 * nd * cdiv(B, 32) + 9) * PERSIST_SYNC_STRIDE; }
 
 // Copy off[0..T] to device memory `dst` on stream s through a pinned ring
 // (asynchronous, no host/device synchronisation).

@@ -2130,6 +2130,388 @@ __global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// dec_bwd_w16 (round 4): dec_bwd_fold's split-K BPTT with HALF the exchange.
+//
+// Per step a split-K member writes one partial of every output column for
+// every row of its group, so the bytes a step moves chip-wide are
+//     (CUs) x (rows per group) x (H + Fp output columns) x 4 B
+// -- 25 MiB at c2 with 64-row groups of 32 members (8 units each), the
+// write-through volume that makes dec_bwd_fold store-bound and slows it by a
+// third when all 8 groups exchange at once.  Here a group is
+// a 32-ROW tile of 16 members that own 16 units each (K = 64 gate columns,
+// two 32-deep x6 chunks): the same 256 CUs, half the rows per group, half the
+// partial bytes (12.5 MiB per step; a member writes 32 KiB of dh partials and
+// 18 KiB of dx partials per step instead of 64 + 36) and half the fan-in of
+// every reduction (16 producers).  The doubled K per member would not fit
+// dec_bwd_fold's LDS images (150 KiB of x6 W_hh / W_ih rows alone), so the
+// waves split the OUTPUT columns instead of the rows: wave w forms the dh
+// partials of units 64w .. 64w + 63 (four subtiles, both 16-row blocks) and
+// keeps that quarter of the W_hh image in registers for the whole launch
+// (96 VGPRs); the W_ih (dx) image, the W1cat fold image and the dZ tile's W2
+// fragments stay in LDS (145 KiB).
+//   P0  (18 units = 2 row blocks x 9 column tiles, one wave each): sum the 16
+//       dx partials of the tile -> dMU, dLV (+ the emission NLL terms)
+//   P1  wave (rb, jj): the member's dZ column tile 2 mem + jj of row block rb
+//       (fp32 MFMA, K = Fp); then every wave: its 8 dh partial tiles
+//       = dG_{t+1}[:, own 64] W_hh[own 64, its 64 units]   (x6, before the wait)
+//       + dZ_t[:, own 32]   W1cat[own 32, its 64 units]   (x6)
+//  P2  waves (rb, half) sum 8 of the 16 dh partials of the member's 16
+//       units; waves 0 / 1 add the other half through LDS and run the cell
+//       backward of row block 0 / 1; every wave splits the 32 x 64 dG tile
+//       and forms its share of the 18 dx partial tiles (x6, K = 64)
+// Partials are double-buffered by step parity as in dec_bwd_fold.  Reference:
+// the decoder BPTT of model.py:174-183 (LSTMCell / GRUCell, the emission MLPs
+// 303-314 and the Gaussian NLL 30-37).
+// ---------------------------------------------------------------------------
+constexpr int W16_ROWS = 32;    // rows per group
+constexpr int W16_M = 16;       // members per group (16 units each)
+constexpr int W16_DTP = 68;     // pitch (floats) of the group's 32 x 64 dG tile in LDS
+constexpr int W16_ZTP = 36;     // pitch of the 32 x 32 dZ tile
+template <int NXS, bool GRU = false>
+__global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  constexpr int H = 256, NHS = 16, GH = (GRU ? 3 : 4) * H, M = W16_M;
+  const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
+  const int nchx = Fp / 16, nFt = Fp / 16;
+  const int ng = a.nrt;  // 32-row groups (the launcher's count)
+  const Role role = assign_role(ng, M);
+  const int grp = role.grp, mem = role.mem;
+  const int rowg = grp * W16_ROWS;
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  GSync gs{a.sync + grp * PERSIST_SYNC_STRIDE,
+           a.sync + ((size_t)2 * ng + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
+           M, mem, a.flags, 0u};
+  const int u0 = mem * 16;
+  // LDS: dx image [NXS][2][3][64] | fold image [NHS][3][64] | P1 W2 fragments [2][nchx][64]
+  //      | dG tile [32][68] | dZ tile [32][36] | dh half-sums [2][64] | wave transposes [4][2 TP]
+  f4* DXI = smem;
+  f4* W1X = DXI + NXS * 2 * 3 * 64;
+  f4* B1 = W1X + NHS * 3 * 64;
+  float* DT = reinterpret_cast<float*>(B1 + 2 * nchx * 64);
+  float* ZT = DT + W16_ROWS * W16_DTP;
+  f4* DHX = reinterpret_cast<f4*>(ZT + W16_ROWS * W16_ZTP);
+  float* tb = reinterpret_cast<float*>(DHX + 2 * 64) + w * 2 * TP_FLOATS;
+  const int trow = lane >> 2, tcol = 4 * (lane & 3);
+  // gate-slot column of W for K index kappa = 16 slot + ju of this member
+  // (xs: the W_ih image, else W_hh); GRU slots (r, z, n_x, n_h): n_x has no
+  // W_hh part, n_h no W_ih part (-1: a zero row)
+  auto kcol = [&](int slot, bool xs) -> int {
+    if (GRU && slot >= 2) return (slot == 2) == xs ? 2 * H + u0 : -1;
+    return slot * H + u0;
+  };
+  // dx image: column tile s, chunk c, lane (rr, qq): kappa = 32c + 8qq + 0..7
+  for (int e = threadIdx.x; e < NXS * 2 * 64; e += 256) {
+    const int s = e >> 7, c = (e >> 6) & 1, ln = e & 63, rr = ln & 15, qq = ln >> 4;
+    const int col = kcol(2 * c + (qq >> 1), true);
+    const float* src = a.WihT + (long)(16 * s + rr) * GH + (col < 0 ? 0 : col + 8 * (qq & 1));
+    bf8 h, m, l;
+    split8(col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src), col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src + 4),
+           h, m, l);
+    f4* d = DXI + ((s * 2 + c) * 3) * 64 + ln;
+    d[0] = __builtin_bit_cast(f4, h);
+    d[64] = __builtin_bit_cast(f4, m);
+    d[128] = __builtin_bit_cast(f4, l);
+  }
+  // fold image: unit subtile s, lane (rr, qq): W1cat[unit 16s + rr][dZ column 32 mem + 8qq + 0..7]
+  for (int e = threadIdx.x; e < NHS * 64; e += 256) {
+    const int s = e >> 6, ln = e & 63, rr = ln & 15, qq = ln >> 4;
+    const float* src = a.W1T + (long)(16 * s + rr) * 2 * Hm + 32 * mem + 8 * qq;
+    bf8 h, m, l;
+    split8(*reinterpret_cast<const f4*>(src), *reinterpret_cast<const f4*>(src + 4), h, m, l);
+    f4* d = W1X + (s * 3) * 64 + ln;
+    d[0] = __builtin_bit_cast(f4, h);
+    d[64] = __builtin_bit_cast(f4, m);
+    d[128] = __builtin_bit_cast(f4, l);
+  }
+  // P1 dZ column tiles 2 mem, 2 mem + 1 (mu tiles for mem < Hm / 32, else lv)
+  const bool ismu = 2 * mem < Hm / 16;
+  stage_b_frag(B1, ismu ? a.W2mT : a.W2lT, Fp, 2, nchx,
+               [&](int j) { return 16 * (2 * mem + j) - (ismu ? 0 : Hm); });
+  // this wave's quarter of the W_hh image (units 64w .. 64w + 63), resident in registers
+  bf8 Bh[4][2][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int col = kcol(2 * c + (q >> 1), false);
+      const float* src = a.WhhT + (long)(16 * (4 * w + j) + r) * GH + (col < 0 ? 0 : col + 8 * (q & 1));
+      split8(col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src), col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src + 4),
+             Bh[j][c][0], Bh[j][c][1], Bh[j][c][2]);
+    }
+  const float s_em = *a.s_em;
+  __syncthreads();
+  const size_t slot_f = (size_t)ng * (NXS + NHS) * 2 * M * 256;  // floats per parity slot
+  const __amdgpu_buffer_rsrc_t pr0 = make_rsrc(a.part, (uint32_t)(slot_f * 4));
+  const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
+  // 1-KiB block of (output tile, row block rb, producer p); dx tiles first, then dh
+  auto xblk = [&](int jx, int rb) { return (uint32_t)((((size_t)grp * NXS + jx) * 2 + rb) * M) * 1024u; };
+  auto hblk = [&](int s, int rb) {
+    return (uint32_t)(((size_t)ng * NXS * 2 * M + (((size_t)grp * NHS + s) * 2 + rb) * M)) * 1024u;
+  };
+  // P0 unit of this wave: k = 16 w + mem < 2 nFt -> (row block k / nFt, column tile k % nFt)
+  const int pk = M * w + mem;
+  const bool p0 = pk < 2 * nFt;
+  const int prb = p0 ? pk / nFt : 0, jx = p0 ? pk % nFt : 0;
+  const int prow0 = rowg + 16 * prb;
+  // P1 dZ unit of this wave: row block w >> 1, column tile 2 mem + (w & 1)
+  const int zrb = w >> 1, zj = w & 1;
+  const int zrow0 = rowg + 16 * zrb;
+  // P2: dh half-sum of row block w & 1 over producers 8 (w >> 1) .. + 7; waves 0 / 1 run the cell
+  const int crb = w & 1;
+  const int crow0 = rowg + 16 * crb;
+  const bool cellw = w < 2;
+  const int unit = u0 + r;
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+  bool dgv = false;  // DT holds the previous step's dG tile (rows < its batch) for the HX half
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = T - 1 - i;
+    const int o = off[t], bs = off[t + 1] - o;
+    const int succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+    const __amdgpu_buffer_rsrc_t prd = (i & 1) ? pr0 : pr1;  // step t+1's slot
+    const __amdgpu_buffer_rsrc_t pw = (i & 1) ? pr1 : pr0;   // this step's slot
+    // ---------------- P0: dx_{t+1} tile -> dMU, dLV ----------------
+    const int col0 = 16 * jx + r;
+    float emu[4], elv[4], eox[4], ey[4], emk[4];
+    if (p0) {
+      const uint32_t ef = (uint32_t)bs * Fp * 4u;
+      const __amdgpu_buffer_rsrc_t rmu = make_rsrc(a.MU + (size_t)o * Fp, ef), rlv = make_rsrc(a.LV + (size_t)o * Fp, ef),
+                                   rox = make_rsrc(a.OUT + (size_t)o * Fp, ef),
+                                   ryy = make_rsrc(a.Y + (size_t)o * F, (uint32_t)bs * F * 4u);
+      const __amdgpu_buffer_rsrc_t rmk =
+          make_rsrc(a.xmask ? a.xmask + (size_t)(o + bs) * F : a.Y, a.xmask ? (uint32_t)succ_valid * F * 4u : 0u);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b = (uint32_t)(prow0 + 4 * q + g);
+        const uint32_t of = col0 < F ? (b * Fp + col0) * 4u : 0x80000000u;
+        const uint32_t oy = col0 < F ? (b * F + col0) * 4u : 0x80000000u;
+        emu[g] = bld(rmu, of);
+        elv[g] = bld(rlv, of);
+        eox[g] = bld(rox, of);
+        ey[g] = bld(ryy, oy);
+        emk[g] = a.xmask ? bld(rmk, oy) : 1.f;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) emu[g] = elv[g] = eox[g] = ey[g] = 0.f, emk[g] = 1.f;
+    }
+    if (i > 0) gs.wait(3u * i);
+    pin(emu), pin(elv), pin(eox), pin(ey), pin(emk);
+    PSTAMP(0);
+    if (p0) {
+      f4 dx = f4zero();
+      if (NXS > 0 && i > 0 && prow0 < succ_valid) sum_partials<M>(prd, xblk(jx, prb) + (uint32_t)lane * 16u, dx, mem % M);
+      float dmu[4], dlv[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        dmu[g] = dlv[g] = 0.f;
+        if (col0 < F) {
+          const float dxv = dx[g] * emk[g], mu = emu[g], lv = elv[g];
+          const float iv = __expf(-lv), d = ey[g] - mu;
+          dmu[g] = dxv + s_em * (-d) * iv;
+          dlv[g] = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);
+        }
+      }
+      const f4 mq = tp_quad(tb, dmu, lane), lq = tp_quad(tb + TP_FLOATS, dlv, lane);
+      if (prow0 < bs) {
+        const uint32_t qo = (uint32_t)((prow0 + trow) * Fp + 16 * jx + tcol) * 4u;
+        st4(make_rsrc(a.dMU + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, mq, true);
+        st4(make_rsrc(a.dLV + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, lq, true);
+      }
+    }
+    gs.publish();
+    PSTAMP(1);
+    // HX: the dG_{t+1} W_hh half of this step's dh partials needs nothing of
+    // this step -- formed in front of the P1 wait from the previous step's dG
+    // tile (still in LDS)
+    f4 hx[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hx[j][0] = hx[j][1] = f4zero();
+    if (dgv) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        if (rowg + 16 * rb >= succ_valid) continue;  // uniform: rows without a successor have no dG_{t+1}
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float* ar = DT + (16 * rb + r) * W16_DTP + 32 * c + 8 * q;
+          bf8 a0, a1, a2;
+          split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hx[j][rb] = mma_x6(hx[j][rb], a0, a1, a2, Bh[j][c][0], Bh[j][c][1], Bh[j][c][2]);
+        }
+      }
+    }
+    PSTAMP(6);
+    // ---------------- P1: dZ tile -> this member's dh partials ----------------
+    float zpre[4];
+    {
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        zpre[g] = bld(rz, ((uint32_t)(zrow0 + 4 * q + g) * 2 * Hm + 32 * mem + 16 * zj + r) * 4u);
+    }
+    gs.wait(3u * i + 1);
+    pin(zpre);
+    PSTAMP(2);
+    {
+      f4 acc[2][1];
+      acc2_zero(acc);
+      if (zrow0 < bs) {
+        const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
+        mma16<1>(acc, A, zrow0 + r, B1 + zj * nchx * 64, nchx, lane, q);
+      }
+      acc2_fold(acc);
+      float dz[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) dz[g] = acc[0][0][g] * (1.f - zpre[g] * zpre[g]);
+      // the dZ tile for the fold (rows 16 zrb + .., columns 16 zj + r) and the stash
+#pragma unroll
+      for (int g = 0; g < 4; ++g) ZT[(16 * zrb + 4 * q + g) * W16_ZTP + 16 * zj + r] = dz[g];
+      const f4 zq = tp_quad(tb, dz, lane);
+      if (zrow0 < bs)
+        st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
+            (uint32_t)((zrow0 + trow) * 2 * Hm + 32 * mem + 16 * zj + tcol) * 4u, zq, false);
+    }
+    __syncthreads();  // the member's 32 x 32 dZ tile is in LDS
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      if (rowg + 16 * rb >= bs) continue;  // uniform
+      const float* ar = ZT + (16 * rb + r) * W16_ZTP + 8 * q;
+      bf8 z0, z1, z2;
+      split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), z0, z1, z2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f4* bp = W1X + ((4 * w + j) * 3) * 64 + lane;
+        const f4 v = mma_x6(hx[j][rb], z0, z1, z2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                            __builtin_bit_cast(bf8, bp[128]));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
+                                               hblk(4 * w + j, rb) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+      }
+    }
+    gs.publish();
+    PSTAMP(3);
+    // ---------------- P2: dh -> cell backward -> dG_t -> dx partials ----------------
+    float pg[4][4], pc[4], pcp[4], pdho[4];
+    {
+      const uint32_t eh = cellw ? (uint32_t)bs * H * 4u : 0u;  // the summing-only waves load nothing
+      const __amdgpu_buffer_rsrc_t rgs = make_rsrc(a.Gst + (size_t)o * 4 * H, eh * 4u),
+                                   rcs = make_rsrc(a.Cst + (size_t)o * H, GRU ? 0u : eh),
+                                   rcp = make_rsrc((GRU ? a.Hprev : a.Cprev) + (size_t)o * H, eh),
+                                   rdo = make_rsrc(a.DHO + (size_t)o * H, eh);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b = (uint32_t)(crow0 + 4 * q + g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pg[g][j] = bld(rgs, (b * 4 * H + j * H + unit) * 4u);
+        pc[g] = GRU ? 0.f : bld(rcs, (b * H + unit) * 4u);
+        pcp[g] = bld(rcp, (b * H + unit) * 4u);
+        pdho[g] = bld(rdo, (b * H + unit) * 4u);
+      }
+    }
+    gs.wait(3u * i + 2);
+    pin(pg[0]), pin(pg[1]), pin(pg[2]), pin(pg[3]), pin(pc), pin(pcp), pin(pdho);
+    PSTAMP(4);
+    // dh of the own 16 units, row block crb: half the producers per wave
+    f4 dhr = f4zero();
+    if (crow0 < bs)
+      sum_partials<M / 2>(pw, hblk(mem, crb) + (uint32_t)(8 * (w >> 1)) * 1024u + (uint32_t)lane * 16u, dhr,
+                          mem % (M / 2));
+    if (!cellw) DHX[crb * 64 + lane] = dhr;
+    __syncthreads();
+    if (cellw) dhr += DHX[crb * 64 + lane];
+    PSTAMP(7);
+    float dgh[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = crow0 + 4 * q + g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dgh[g][j] = 0.f;
+      if (!cellw || b >= bs) continue;
+      const bool fin = b >= succ_valid;
+      if constexpr (GRU) {
+        const float dh = dhr[g] + (fin ? 0.f : carry[g]) + pdho[g];
+        const float r_ = pg[g][0], z_ = pg[g][1], n_ = pg[g][2], ghn = pg[g][3];
+        const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
+        dgh[g][0] = dnp * ghn * r_ * (1.f - r_);
+        dgh[g][1] = dh * (pcp[g] - n_) * z_ * (1.f - z_);
+        dgh[g][2] = dnp;
+        dgh[g][3] = dnp * r_;
+        carry[g] = dh * z_;
+        if (t == 0) a.DC0[(long)b * H + unit] = dh * z_;
+      } else {
+        const float dh = dhr[g] + pdho[g];
+        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
+        const float tc = ftanh(pc[g]);
+        const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
+        dgh[g][0] = dc * g_ * i_ * (1.f - i_);
+        dgh[g][1] = dc * pcp[g] * f_ * (1.f - f_);
+        dgh[g][2] = dc * i_ * (1.f - g_ * g_);
+        dgh[g][3] = dh * tc * o_ * (1.f - o_);
+        carry[g] = dc * f_;
+        if (t == 0) a.DC0[(long)b * H + unit] = dc * f_;
+      }
+    }
+    if (cellw) {  // the dG tile: rows 16 crb + .., columns [slot][own unit] (rows >= bs hold 0)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) DT[(16 * crb + 4 * q + g) * W16_DTP + 16 * j + r] = dgh[g][j];
+    }
+    __syncthreads();
+    dgv = i + 1 < T;
+    // dx partials of this step's dG columns: 2 x NXS tiles dealt over the waves
+    if (NXS > 0 && i + 1 < T) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        if (rowg + 16 * rb >= bs) continue;  // uniform
+        bf8 av[2][3];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float* ar = DT + (16 * rb + r) * W16_DTP + 32 * c + 8 * q;
+          split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), av[c][0], av[c][1], av[c][2]);
+        }
+#pragma unroll
+        for (int jj = 0; jj < (NXS + 3) / 4; ++jj) {
+          const int k = 4 * jj + ((w + 2 * rb) & 3);  // tile of this wave (rotated by row block: 5,5,4,4 per wave)
+          if (k >= NXS) continue;
+          f4 v = f4zero();
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const f4* bp = DXI + ((k * 2 + c) * 3) * 64 + lane;
+            v = mma_x6(v, av[c][0], av[c][1], av[c][2], __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
+                       __builtin_bit_cast(bf8, bp[128]));
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
+                                                 xblk(k, rb) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+        }
+      }
+    }
+    gs.publish();
+    PSTAMP(5);
+    // stash for the weight-gradient GEMMs (plain 16-B stores after the publish):
+    // 32 rows x 4 slots x 4 quads of own units = 2 quads per thread
+    {
+      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.dG + (size_t)o * GH, (uint32_t)bs * GH * 4u);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int k = threadIdx.x + 256 * k2, row = k >> 4, slot = (k >> 2) & 3, qd = 4 * (k & 3);
+        if (rowg + row >= bs) continue;
+        const f4 v = *reinterpret_cast<const f4*>(DT + row * W16_DTP + 16 * slot + qd);
+        const uint32_t so = (uint32_t)((rowg + row) * GH + u0 + qd) * 4u;
+        if constexpr (GRU) {  // dGX = (dr, dz, dn), dGH = (dr, dz, dn r)
+          const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.dGH + (size_t)o * GH, (uint32_t)bs * GH * 4u);
+          if (slot < 3) st4(rg, so + (uint32_t)(slot * H) * 4u, v, false);
+          if (slot != 2) st4(rh, so + (uint32_t)((slot == 3 ? 2 : slot) * H) * 4u, v, false);
+        } else {
+          st4(rg, so + (uint32_t)(slot * H) * 4u, v, false);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 bool persist_enabled() {
@@ -2617,6 +2999,35 @@ static bool dec_bwd_folded() {
   const char* v = getenv("ABCD_DECBWD");
   return !(v && v[0] == 's');
 }
+// ABCD_DECBWD=w16: the 32-row / 16-member form (dec_bwd_w16)
+static bool dec_bwd_w16_on() {
+  const char* v = getenv("ABCD_DECBWD");
+  return v && v[0] == 'w';
+}
+template <int NXS, bool GRU>
+static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+  const int ng = cdiv(a.B, W16_ROWS), nchx = a.Fp / 16;
+  const size_t lds = (size_t)NXS * 2 * 3 * 64 * 16 + (size_t)16 * 3 * 64 * 16 + (size_t)2 * nchx * 64 * 16 +
+                     (size_t)W16_ROWS * (W16_DTP + W16_ZTP) * 4 + (size_t)2 * 64 * 16 + (size_t)4 * 2 * TP_FLOATS * 4;
+  const int grid = ng * W16_M;
+  if (a.B <= 0 || 2 * nchx > 4 * W16_M) return 0;
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_w16<NXS, GRU>, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(zero_sync(s, a.sync, ng));
+  PDecBwdArgs b = a;
+  b.nrt = ng;
+  b.flags = 1;
+  b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
+  {
+    TimedScope ts(s, TK_DEC_BWD);
+    dec_bwd_w16<NXS, GRU><<<grid, 256, lds, s>>>(b);
+  }
+  note_dispatch(TK_DEC_BWD, "dec_bwd_w16<%d,%s> grid %d", NXS, GRU ? "GRU" : "LSTM", grid);
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
 
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {
   *launched = false;
@@ -2626,6 +3037,11 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
           a.Fp / 16 <= a.H / 8))
       return 0;
     const int nxs = a.feedback ? a.Fp / 16 : 0;
+    if (dec_bwd_w16_on()) {
+      if (nxs == 9) return launch_dec_bwd_w16<9, true>(s, a, launched);
+      if (nxs == 5) return launch_dec_bwd_w16<5, true>(s, a, launched);
+      if (nxs == 0) return launch_dec_bwd_w16<0, true>(s, a, launched);
+    }
     if (dec_bwd_folded()) {
       if (nxs == 9) return launch_dec_bwd_fold<9, 16, true>(s, a, launched);
       if (nxs == 5) return launch_dec_bwd_fold<5, 16, true>(s, a, launched);
@@ -2641,6 +3057,11 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
   // split-K form: H = 256 (32 members), 2Hm/16 == members, Fp/16 <= members
   if (a.part && x6_enabled(a.H) && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8) {
     const int nxs = a.feedback ? a.Fp / 16 : 0;
+    if (dec_bwd_w16_on()) {
+      if (nxs == 9) return launch_dec_bwd_w16<9, false>(s, a, launched);
+      if (nxs == 5) return launch_dec_bwd_w16<5, false>(s, a, launched);
+      if (nxs == 0) return launch_dec_bwd_w16<0, false>(s, a, launched);
+    }
     if (dec_bwd_folded()) {
       if (nxs == 9) return launch_dec_bwd_fold<9, 16>(s, a, launched);
       if (nxs == 5) return launch_dec_bwd_fold<5, 16>(s, a, launched);

@@ -1317,7 +1317,7 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
   bool done = false;
   {
     PDecBwdArgs pa{};
-    pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS);
+    pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS); pa.B = B;
     pa.feedback = c->feedback;
     pa.off = w.off; pa.sync = w.sync;
     pa.WihT = w.WihTp; pa.WhhT = w.WhhT; pa.W2mT = w.W2mT; pa.W2lT = w.W2lT; pa.W1T = w.W1catT;

@@ -46,6 +46,9 @@ KERNELS = {
 
 if os.environ.get("ABCD_DECBWD", "").startswith("s"):  # the unfolded decoder BPTT (A/B runs)
     KERNELS = {r: k[:3] + (f"dec_bwd_sk<9,16,16,{r}>",) for r, k in KERNELS.items()}
+W16 = os.environ.get("ABCD_DECBWD", "").startswith("w")  # the 32-row / 16-member decoder BPTT (A/B runs)
+if W16:
+    KERNELS = {r: k[:3] + (f"dec_bwd_w16<9,{r}>",) for r, k in KERNELS.items()}
 
 # (bench config, batch, seed of the synthetic batch)
 CASES = [("c2", 512, 2024), ("c4", 512, 2025), ("c5", 128, 2026), ("c5gru", 128, 2027),
@@ -91,7 +94,8 @@ def test_full_shape_step_vs_oracle(name, B, seed):
     assert N.lib().abcd_device_status() == 0
     ran = N.dispatch()
     tiles = (B + 63) // 64
-    grids = {"enc_fwd": tiles * 2 * 16, "enc_bwd": tiles * 2 * 16, "dec_fwd": tiles * 32, "dec_bwd": tiles * 32}
+    grids = {"enc_fwd": tiles * 2 * 16, "enc_bwd": tiles * 2 * 16, "dec_fwd": tiles * 32,
+             "dec_bwd": (B + 31) // 32 * 16 if W16 else tiles * 32}
     for role, kern in zip(("enc_fwd", "enc_bwd", "dec_fwd", "dec_bwd"), KERNELS[cfg["rnn"]]):
         assert ran[role][0] == f"{kern} grid {grids[role]}", (role, ran[role])
         assert ran[role][1] == 1, (role, ran[role])

@@ -36,6 +36,10 @@ EXPECT = {
 if os.environ.get("ABCD_DECBWD", "").startswith("s"):  # the unfolded decoder BPTT (A/B runs)
     for _r in EXPECT:
         EXPECT[_r]["dec_bwd"] = f"dec_bwd_sk<9,16,16,{_r}>"
+W16 = os.environ.get("ABCD_DECBWD", "").startswith("w")  # the 32-row / 16-member decoder BPTT (A/B runs)
+if W16:
+    for _r in EXPECT:
+        EXPECT[_r]["dec_bwd"] = f"dec_bwd_w16<9,{_r}>"
 
 
 def _noise(inp):
@@ -61,7 +65,8 @@ def test_fused_step_prod_vs_reference(name):
     for role, kern in EXPECT[meta["rnn"]].items():
         assert ran[role][0].startswith(kern), (role, ran[role])
         assert ran[role][1] == 1, (role, ran[role])
-    assert ran["dec_bwd"][0].endswith("grid 64") and ran["dec_fwd"][0].endswith("grid 64")  # 2 row groups x 32 members
+    # 2 row groups x 32 members (dec_bwd_w16: 3 groups of 32 rows x 16 members)
+    assert ran["dec_bwd"][0].endswith("grid 48" if W16 else "grid 64") and ran["dec_fwd"][0].endswith("grid 64")
     if not meta.get("plain"):  # the fused sampler head, 5 tiles of 16 rows (the last one ragged: 72 = 4 x 16 + 8)
         assert "samp_head_fwd grid 5" in ran["samp_fwd"][0] and ran["samp_fwd"][1] == 1, ran["samp_fwd"]
         assert ran["samp_bwd"][0].startswith("samp_head_bwd grid 5") and ran["samp_bwd"][1] == 1, ran["samp_bwd"]
