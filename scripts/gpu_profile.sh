@@ -15,3 +15,5 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_f
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing > /dev/null 2> $OUT/pmc_write.err
 python scripts/pmc_traffic.py $OUT/pmc_fetch $OUT/pmc_write $OUT/traffic.json > /dev/null
 echo "pmc done"
+bash scripts/gpu_pmc_mfma.sh $OUT/mfma c2 > $OUT/mfma.log 2>&1 && cp $OUT/mfma/pmc_mfma.json $OUT/pmc_mfma.json
+echo "pmc mfma done"

@@ -2999,10 +2999,13 @@ static bool dec_bwd_folded() {
   const char* v = getenv("ABCD_DECBWD");
   return !(v && v[0] == 's');
 }
-// ABCD_DECBWD=w16: the 32-row / 16-member form (dec_bwd_w16)
+// dec_bwd_w16 by default (32-row groups of 16 members: half the split-K
+// exchange): same-box A/B at c2 against dec_bwd_fold, dec_bwd 3.08 / 3.06 ->
+// 2.55 / 2.55 ms per launch, step 9.99 / 9.99 -> 9.49 / 9.47 ms.
+// ABCD_DECBWD=f: dec_bwd_fold, =sk: dec_bwd_sk (A/B timing)
 static bool dec_bwd_w16_on() {
   const char* v = getenv("ABCD_DECBWD");
-  return v && v[0] == 'w';
+  return !(v && (v[0] == 'f' || v[0] == 's'));
 }
 template <int NXS, bool GRU>
 static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launched) {

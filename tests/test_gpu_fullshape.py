@@ -13,7 +13,7 @@ replayed Gumbel / N(0, 1) noise, against ``oracle.train_step`` on the same
 inputs (the torch-CPU restatement of ``learning.py:147-163`` pinned to the
 reference's fixtures in ``tests/golden``):
 
-* dispatch: the kernels and grids bench.py times (c2: ``dec_bwd_fold<9,16,LSTM>
+* dispatch: the kernels and grids bench.py times (c2: ``dec_bwd_w16<9,LSTM>
   grid 256``, 16 encoder groups = ``grid 256``);
 * em / off / kl / loss within 1e-4 relative (north star);
 * logits within 1e-4 of their max, argmax categories identical;
@@ -40,15 +40,16 @@ LOSS_TOL = 1e-4
 GRAD_TOL = 1e-3
 
 KERNELS = {
-    "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_sk<4,16>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_fold<9,16,LSTM>"),
-    "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_sk<3,16>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_fold<9,16,GRU>"),
+    "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_sk<4,16>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
+    "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_sk<3,16>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_w16<9,GRU>"),
 }
-
-if os.environ.get("ABCD_DECBWD", "").startswith("s"):  # the unfolded decoder BPTT (A/B runs)
+# A/B runs of the earlier decoder BPTT forms (64-row groups of 32 members)
+_DB = os.environ.get("ABCD_DECBWD", "")
+W16 = not _DB.startswith(("f", "s"))
+if _DB.startswith("s"):
     KERNELS = {r: k[:3] + (f"dec_bwd_sk<9,16,16,{r}>",) for r, k in KERNELS.items()}
-W16 = os.environ.get("ABCD_DECBWD", "").startswith("w")  # the 32-row / 16-member decoder BPTT (A/B runs)
-if W16:
-    KERNELS = {r: k[:3] + (f"dec_bwd_w16<9,{r}>",) for r, k in KERNELS.items()}
+elif _DB.startswith("f"):
+    KERNELS = {r: k[:3] + (f"dec_bwd_fold<9,16,{r}>",) for r, k in KERNELS.items()}
 
 # (bench config, batch, seed of the synthetic batch)
 CASES = [("c2", 512, 2024), ("c4", 512, 2025), ("c5", 128, 2026), ("c5gru", 128, 2027),

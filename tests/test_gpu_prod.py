@@ -29,17 +29,17 @@ GRAD_TOL = 1e-3
 # the kernels bench.py's configs dispatch at H = Hm = 256, F = 129 (Fp = 144)
 EXPECT = {
     "LSTM": {"enc_fwd": "enc_fwd_persist<4,16,8>", "enc_bwd": "enc_bwd_sk<4,16>",
-             "dec_fwd": "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd": "dec_bwd_fold<9,16,LSTM>"},
+             "dec_fwd": "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd": "dec_bwd_w16<9,LSTM>"},
     "GRU": {"enc_fwd": "enc_fwd_persist<3,16,8>", "enc_bwd": "enc_bwd_sk<3,16>",
-            "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_fold<9,16,GRU>"},
+            "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_w16<9,GRU>"},
 }
-if os.environ.get("ABCD_DECBWD", "").startswith("s"):  # the unfolded decoder BPTT (A/B runs)
-    for _r in EXPECT:
+_DB = os.environ.get("ABCD_DECBWD", "")  # A/B runs of the earlier decoder BPTT forms
+for _r in EXPECT:
+    if _DB.startswith("s"):
         EXPECT[_r]["dec_bwd"] = f"dec_bwd_sk<9,16,16,{_r}>"
-W16 = os.environ.get("ABCD_DECBWD", "").startswith("w")  # the 32-row / 16-member decoder BPTT (A/B runs)
-if W16:
-    for _r in EXPECT:
-        EXPECT[_r]["dec_bwd"] = f"dec_bwd_w16<9,{_r}>"
+    elif _DB.startswith("f"):
+        EXPECT[_r]["dec_bwd"] = f"dec_bwd_fold<9,16,{_r}>"
+W16 = not _DB.startswith(("f", "s"))  # the 32-row / 16-member decoder BPTT (default)
 
 
 def _noise(inp):
