@@ -92,7 +92,10 @@ def test_featurizer_matches_reference_toy_batch():
     log_and_normalize -> DataLoader pop-from-end -> pack_sequence;
     tests/golden/toy_step.npz, make_golden.py:run_toy_step) against
     DeviceFeaturizer on the same segments' raw samples: identical
-    batch_sizes and is_offset, log-amplitudes within 1e-4."""
+    batch_sizes and is_offset; log-amplitudes as close to the reference's as
+    the reference's own fp32 STFT is to the float64 truth (elementwise, + 1e-5:
+    near-empty bins amplify the fp32 rounding of |X| through the log), and no
+    further from that truth than the reference (or 1e-5)."""
     from modules import data_utils as du
     from golden_io import GOLDEN
     z = np.load(os.path.join(GOLDEN, "toy_step.npz"), allow_pickle=False)
@@ -108,5 +111,13 @@ def test_featurizer_matches_reference_toy_batch():
     torch.cuda.synchronize()
     assert torch.equal(bs, torch.from_numpy(z["batch_sizes"]))
     assert torch.equal(is_off.cpu(), torch.from_numpy(z["is_offset"]))
-    err = (data.cpu() - torch.from_numpy(z["data"])).abs().max().item()
-    assert err <= 1e-4, err
+    win = torch.hann_window(frame).double()
+    truth = torch.nn.utils.rnn.pack_sequence([
+        (torch.stft(torch.from_numpy(w).double(), frame, hop_length=hop, window=win, center=True,
+                    return_complex=True).abs().T + 2 ** (-15)).log() for w in waves]).data
+    ref = torch.from_numpy(z["data"]).double()
+    got = data.cpu().double()
+    gpu_err, ref_err = (got - truth).abs().max().item(), (ref - truth).abs().max().item()
+    assert gpu_err <= max(1e-5, ref_err), (gpu_err, ref_err)
+    slack = (ref - truth).abs() + 1e-5
+    assert bool(((got - ref).abs() <= slack).all()), float(((got - ref).abs() - slack).max())
