@@ -44,6 +44,7 @@ struct PBwdDir {
 struct PBwdArgs {
   PBwdDir d[2];
   int H, nd, T, nrt;
+  int B;             // batch (rows of the first step): the 32-row groups of enc_bwd_w8
   const int* off;
   unsigned* sync;
   unsigned long long* prof;

@@ -2512,6 +2512,223 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// enc_bwd_w8 (round 4): enc_bwd_sk with HALF the exchange, as dec_bwd_w16
+// does for the decoder.  A group is a 32-ROW tile of one direction with 8
+// members owning 32 units each (K = G x 32 gate columns: one 32-deep chunk
+// per gate, so a GRU member multiplies 3 chunks instead of 2 padded ones);
+// per step a member writes its partial of dh_rec for all 256 units of its 32
+// rows (32 KiB instead of 64) and a consumer sums 8 partials instead of 16.
+// The waves split the output columns: wave w forms the partials of units
+// 64w .. 64w + 63 (4 subtiles x both 16-row blocks x G chunks = 24 G MFMAs
+// per subtile pair, 192 per wave for the LSTM as in enc_bwd_sk) and keeps
+// the first two chunks of its quarter of the W_hh image in registers (96
+// VGPRs), the rest in LDS.  Cell backward: wave (rb, uh) runs rows 16 rb ..
+// of units 16 uh .. of the member's 32.  Reference: the BPTT of nn.LSTM /
+// nn.GRU, model.py:53,60-66.
+// ---------------------------------------------------------------------------
+constexpr int W8_ROWS = 32;   // rows per group
+constexpr int W8_M = 8;       // members per group (32 units each)
+constexpr int W8_DTP = 132;   // pitch (floats) of the member's 32 x 4*32 dG tile in LDS
+template <int G>
+__global__ __launch_bounds__(256) void enc_bwd_w8(PBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  constexpr int H = 256, GH = G * H, M = W8_M, NSUB = H / 16;
+  constexpr int NC = G;                     // 32-deep chunks = gates
+  constexpr int NCR = 2, NCL = NC - NCR;    // chunks of the image in registers / in LDS
+  const int T = a.T, ng = a.nd * a.nrt;     // a.nrt: 32-row tiles per direction (the launcher's count)
+  const Role role = assign_role(ng, M);
+  const int grp = role.grp, mem = role.mem;
+  const int dir = grp / a.nrt, rt = grp % a.nrt;
+  const PBwdDir& D = a.d[dir];
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int u0 = mem * 32;
+  const int rb = w & 1, uh = w >> 1;        // this wave's cell tile: rows 16 rb .., units u0 + 16 uh ..
+  const int unit = u0 + 16 * uh + r;
+  const int rowg = rt * W8_ROWS, row0 = rowg + 16 * rb;
+  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
+  // LDS: [wave][subtile j][chunk c - NCR][plane][64] | dG tile [32][132] | wave transposes
+  f4* BL = smem;
+  float* DT = reinterpret_cast<float*>(BL + 4 * 4 * (NCL > 0 ? NCL : 1) * 3 * 64);
+  float* tb = DT + W8_ROWS * W8_DTP + w * TP_FLOATS;
+  const int trow = lane >> 2, tcol = 4 * (lane & 3);
+  // image of output subtile s = 4w + j, chunk c (gate c), lane (rr = r, qq = q):
+  // rows k = 32c + 8q + 0..7 = W_hh rows c H + u0 + 8q + 0..7, column unit 16 s + r
+  bf8 Br[4][NCR][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float* src = D.WhhT + (long)(16 * (4 * w + j) + r) * GH + c * H + u0 + 8 * q;
+      bf8 h, m, l;
+      split8(*reinterpret_cast<const f4*>(src), *reinterpret_cast<const f4*>(src + 4), h, m, l);
+      if (c < NCR) {
+        Br[j][c][0] = h, Br[j][c][1] = m, Br[j][c][2] = l;
+      } else {
+        f4* d = BL + (((w * 4 + j) * NCL + (c - NCR)) * 3) * 64 + lane;
+        d[0] = __builtin_bit_cast(f4, h);
+        d[64] = __builtin_bit_cast(f4, m);
+        d[128] = __builtin_bit_cast(f4, l);
+      }
+    }
+  __syncthreads();
+  const size_t slot_f = (size_t)ng * NSUB * 2 * M * 256;  // floats per parity slot
+  // 1-KiB block of (group, consumer subtile s, row block b2, producer)
+  auto pblk = [&](int s, int b2) { return (uint32_t)((((size_t)grp * NSUB + s) * 2 + b2) * M) * 1024u; };
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+  const int* off = a.off;
+  for (int i = 0; i < T; ++i) {
+    const int t = D.rev ? i : T - 1 - i;
+    const int o = off[t], bs = off[t + 1] - o;
+    int succ_valid, prev_valid;
+    if (!D.rev) {
+      succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
+      prev_valid = t == 0 ? 0 : bs;
+    } else {
+      succ_valid = t >= 1 ? bs : 0;
+      prev_valid = t == T - 1 ? 0 : off[t + 2] - off[t + 1];
+    }
+    PSTAMP(0);
+    // cell operands: branch-free loads before the wait, pinned after it (bld)
+    float pg[4][4], pc[4], pcp[4], pdh[4], pdl[4], pdc[4];
+    {
+      const uint32_t eh = (uint32_t)bs * H * 4u;
+      const __amdgpu_buffer_rsrc_t rgs = make_rsrc(D.Gst + (size_t)o * 4 * H, eh * 4u),
+                                   rcs = make_rsrc(D.Cst + (size_t)o * H, G == 4 ? eh : 0u),
+                                   rcp = make_rsrc((G == 4 ? D.Cprev : D.Hprev) + (size_t)o * H,
+                                                   (uint32_t)prev_valid * H * 4u),
+                                   rdx = make_rsrc(D.DHX ? D.DHX + (size_t)o * D.lddhx : D.Gst,
+                                                   D.DHX ? (uint32_t)bs * D.lddhx * 4u : 0u),
+                                   rdl = make_rsrc(D.dlast ? D.dlast : D.Gst, D.dlast ? (uint32_t)bs * D.ldl * 4u : 0u);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
+        const bool fin = (int)b >= succ_valid;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pg[g][j] = bld(rgs, (b * 4 * H + j * H + unit) * 4u);
+        pc[g] = G == 4 ? bld(rcs, (b * H + unit) * 4u) : 0.f;
+        pcp[g] = bld(rcp, (b * H + unit) * 4u);
+        pdh[g] = bld(rdx, (b * D.lddhx + unit) * 4u);
+        // the last step's gradient enters rows that have no successor (rows >= bs read 0)
+        pdl[g] = bld(rdl, fin ? (b * D.ldl + D.hcol + unit) * 4u : 0x80000000u);
+        pdc[g] = (G == 4 && D.ccol >= 0) ? bld(rdl, fin ? (b * D.ldl + D.ccol + unit) * 4u : 0x80000000u) : 0.f;
+      }
+    }
+    f4 dhr = f4zero();
+    if (i > 0) group_wait(cnt, (unsigned)(M * i));
+    pin(pg[0]), pin(pg[1]), pin(pg[2]), pin(pg[3]), pin(pc), pin(pcp), pin(pdh), pin(pdl), pin(pdc);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) pdh[g] += pdl[g];
+    if (i > 0 && row0 < succ_valid) {
+      const __amdgpu_buffer_rsrc_t pr = make_rsrc(a.part + (size_t)(i & 1) * slot_f, (uint32_t)(slot_f * 4));
+      sum_partials<M>(pr, pblk(2 * mem + uh, rb) + (uint32_t)lane * 16u, dhr, mem);
+    }
+    PSTAMP(1);
+    // cell backward -> dG (LSTM: dGX == dGH; GRU: dGH = [dr, dz, dn*r], dGX gate 2 = dn)
+    float dgh[4][4], dgx[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int b = row0 + 4 * q + g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dgh[g][j] = dgx[g][j] = 0.f;
+      if (b >= bs) continue;
+      const bool fin = b >= succ_valid;
+      float dh = (fin ? 0.f : dhr[g]) + pdh[g];
+      if (G == 4) {
+        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
+        const float tc = ftanh(pc[g]);
+        const float dc = (fin ? pdc[g] : carry[g]) + dh * o_ * (1.f - tc * tc);
+        dgx[g][0] = dc * g_ * i_ * (1.f - i_);
+        dgx[g][1] = dc * pcp[g] * f_ * (1.f - f_);
+        dgx[g][2] = dc * i_ * (1.f - g_ * g_);
+        dgx[g][3] = dh * tc * o_ * (1.f - o_);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dgh[g][j] = dgx[g][j];
+        carry[g] = dc * f_;
+      } else {
+        if (!fin) dh += carry[g];
+        const float r_ = pg[g][0], z_ = pg[g][1], n_ = pg[g][2], ghn = pg[g][3];
+        const float hp = pcp[g];
+        const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
+        const float dzp = dh * (hp - n_) * z_ * (1.f - z_);
+        const float drp = dnp * ghn * r_ * (1.f - r_);
+        dgx[g][0] = drp; dgx[g][1] = dzp; dgx[g][2] = dnp;
+        dgh[g][0] = drp; dgh[g][1] = dzp; dgh[g][2] = dnp * r_;
+        carry[g] = dh * z_;
+      }
+    }
+    PSTAMP(2);
+    // the member's dG tile: rows 16 rb + .., columns [gate][32 own units] (rows >= bs hold 0)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int j = 0; j < G; ++j) DT[(16 * rb + 4 * q + g) * W8_DTP + 32 * j + 16 * uh + r] = dgh[g][j];
+    // partials for the next step from this step's own dG columns
+    if (i + 1 < T) {
+      __syncthreads();  // every wave's dG rows are in the member's tile
+      const __amdgpu_buffer_rsrc_t pw = make_rsrc(a.part + (size_t)((i + 1) & 1) * slot_f, (uint32_t)(slot_f * 4));
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2) {
+        if (rowg + 16 * b2 >= bs) break;  // uniform: row blocks past the step's batch
+        bf8 av[NC][3];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const float* ar = DT + (16 * b2 + r) * W8_DTP + 32 * c + 8 * q;
+          split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), av[c][0], av[c][1], av[c][2]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f4 acc = f4zero();
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            if (c < NCR) {
+              acc = mma_x6(acc, av[c][0], av[c][1], av[c][2], Br[j][c < NCR ? c : 0][0], Br[j][c < NCR ? c : 0][1],
+                           Br[j][c < NCR ? c : 0][2]);
+            } else {
+              const f4* bp = BL + (((w * 4 + j) * NCL + (c - NCR)) * 3) * 64 + lane;
+              acc = mma_x6(acc, av[c][0], av[c][1], av[c][2], __builtin_bit_cast(bf8, bp[0]),
+                           __builtin_bit_cast(bf8, bp[64]), __builtin_bit_cast(bf8, bp[128]));
+            }
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc), pw,
+                                                 pblk(4 * w + j, b2) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u,
+                                                 0, 16);
+        }
+      }
+    }
+    PSTAMP(3);
+    group_publish(cnt);
+    // stashes for the weight-gradient GEMMs after the launch (plain 16-B
+    // stores after the publish, read back from the dG tile: 32 rows x G gates
+    // x 8 quads of own units).  LSTM: dGX = dGH = dG.  GRU: the tile is dGH =
+    // (dr, dz, dn r); dGX = (dr, dz, dn) takes gate 2 from a transpose of dn.
+    {
+      const __amdgpu_buffer_rsrc_t rx = make_rsrc(D.dGX + (size_t)o * GH, (uint32_t)bs * GH * 4u);
+      const __amdgpu_buffer_rsrc_t rh = make_rsrc(D.dGH + (size_t)o * GH, (uint32_t)bs * GH * 4u);
+#pragma unroll
+      for (int k2 = 0; k2 < G; ++k2) {
+        const int k = threadIdx.x + 256 * k2, row = k / (8 * G), gate = (k >> 3) % G, qd = 4 * (k & 7);
+        if (rowg + row >= bs) continue;
+        const f4 v = *reinterpret_cast<const f4*>(DT + row * W8_DTP + 32 * gate + qd);
+        const uint32_t so = (uint32_t)((rowg + row) * GH + gate * H + u0 + qd) * 4u;
+        if (G == 3) {
+          st4(rh, so, v, false);
+          if (gate < 2) st4(rx, so, v, false);
+        } else {
+          st4(rx, so, v, false);
+        }
+      }
+      if (G == 3) {
+        const float dn[4] = {dgx[0][2], dgx[1][2], dgx[2][2], dgx[3][2]};
+        const f4 nq = tp_quad(tb, dn, lane);
+        if (row0 < bs) st4(rx, (uint32_t)((row0 + trow) * GH + 2 * H + u0 + 16 * uh + tcol) * 4u, nq, false);
+      }
+    }
+    PSTAMP(4);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 bool persist_enabled() {
@@ -2821,9 +3038,42 @@ static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
 }
 
 
+// ABCD_ENCBWD=w8: the 32-row / 8-member form (enc_bwd_w8)
+static bool enc_bwd_w8_on() {
+  const char* v = getenv("ABCD_ENCBWD");
+  return v && v[0] == 'w';
+}
+template <int G>
+static int launch_bwd_w8(hipStream_t s, const PBwdArgs& a, bool* launched) {
+  const int nrt = cdiv(a.B, W8_ROWS);
+  const int grid = a.nd * nrt * W8_M;
+  constexpr int NCL = G - 2;
+  const size_t lds = (size_t)4 * 4 * NCL * 3 * 64 * 16 + (size_t)W8_ROWS * W8_DTP * 4 + (size_t)4 * TP_FLOATS * 4;
+  if (a.B <= 0) return 0;
+  bool ok = false;
+  ABCD_TRY((hipError_t)fits_resident(enc_bwd_w8<G>, grid, lds, &ok));
+  if (!ok) return 0;
+  ABCD_TRY(zero_sync(s, a.sync, a.nd * nrt));
+  PBwdArgs b = a;
+  b.nrt = nrt;
+  b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
+  {
+    TimedScope ts(s, TK_ENC_BWD);
+    enc_bwd_w8<G><<<grid, 256, lds, s>>>(b);
+  }
+  note_dispatch(TK_ENC_BWD, "enc_bwd_w8<%d> grid %d", G, grid);
+  ABCD_CHECK_LAUNCH();
+  *launched = true;
+  return 0;
+}
+
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled()) return 0;
+  if (a.H == 256 && a.part && enc_bwd_w8_on()) {
+    const int rc = G == 4 ? launch_bwd_w8<4>(s, a, launched) : launch_bwd_w8<3>(s, a, launched);
+    if (rc || *launched) return rc;
+  }
   if (x6_enabled(a.H) && a.part) {
     if (G == 4) {
       if (a.H == 64) return launch_bwd_sk<4, 4>(s, a, launched);

@@ -532,6 +532,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
     {
       PBwdArgs pa{};
       pa.H = H; pa.nd = D; pa.T = T; pa.nrt = cdiv(x->B, PERSIST_ROWS); pa.off = w.off; pa.sync = w.sync;
+      pa.B = x->B;
       pa.part = w.part;
       for (int d = 0; d < D; ++d) {
         PBwdDir& b = pa.d[d];

@@ -258,7 +258,15 @@ class _OpStatus:
         self.where = where
 
     def sync(self, where):
-        self._read(True)
+        """Blocking check: raises PersistTimeout if any persistent launch
+        timed out since the last check; always reads AND clears the device's
+        status words (abcd_device_status), so a reported timeout is not
+        reported again by the next check."""
+        try:
+            self._read(True)
+        except PersistTimeout:
+            lib().abcd_device_status()
+            raise
         raise_on_status(lib().abcd_device_status(), where)
 
 

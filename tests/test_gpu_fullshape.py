@@ -50,6 +50,9 @@ if _DB.startswith("s"):
     KERNELS = {r: k[:3] + (f"dec_bwd_sk<9,16,16,{r}>",) for r, k in KERNELS.items()}
 elif _DB.startswith("f"):
     KERNELS = {r: k[:3] + (f"dec_bwd_fold<9,16,{r}>",) for r, k in KERNELS.items()}
+W8 = os.environ.get("ABCD_ENCBWD", "").startswith("w")  # the 32-row / 8-member encoder BPTT
+if W8:
+    KERNELS = {r: (k[0], f"enc_bwd_w8<{4 if r == 'LSTM' else 3}>") + k[2:] for r, k in KERNELS.items()}
 
 # (bench config, batch, seed of the synthetic batch)
 CASES = [("c2", 512, 2024), ("c4", 512, 2025), ("c5", 128, 2026), ("c5gru", 128, 2027),
@@ -95,7 +98,8 @@ def test_full_shape_step_vs_oracle(name, B, seed):
     assert N.lib().abcd_device_status() == 0
     ran = N.dispatch()
     tiles = (B + 63) // 64
-    grids = {"enc_fwd": tiles * 2 * 16, "enc_bwd": tiles * 2 * 16, "dec_fwd": tiles * 32,
+    grids = {"enc_fwd": tiles * 2 * 16, "enc_bwd": (B + 31) // 32 * 2 * 8 if W8 else tiles * 2 * 16,
+             "dec_fwd": tiles * 32,
              "dec_bwd": (B + 31) // 32 * 16 if W16 else tiles * 32}
     for role, kern in zip(("enc_fwd", "enc_bwd", "dec_fwd", "dec_bwd"), KERNELS[cfg["rnn"]]):
         assert ran[role][0] == f"{kern} grid {grids[role]}", (role, ran[role])

@@ -40,6 +40,9 @@ for _r in EXPECT:
     elif _DB.startswith("f"):
         EXPECT[_r]["dec_bwd"] = f"dec_bwd_fold<9,16,{_r}>"
 W16 = not _DB.startswith(("f", "s"))  # the 32-row / 16-member decoder BPTT (default)
+if os.environ.get("ABCD_ENCBWD", "").startswith("w"):  # the 32-row / 8-member encoder BPTT
+    for _r in EXPECT:
+        EXPECT[_r]["enc_bwd"] = f"enc_bwd_w8<{4 if _r == 'LSTM' else 3}>"
 
 
 def _noise(inp):
