@@ -114,8 +114,8 @@ def main():
                 print(f"   full-batch: cell-mma={med(7, 0):.0f} cell-epi+pub={med(1, 7):.0f} "
                       f"mlp-mma={med(6, 2):.0f} mlp-epi+pub={med(3, 6):.0f} step={med(5, 0):.0f}")
             else:
-                print(f"   full-batch: P0pub-to-dhr-done={med(6, 1):.0f} P1-wait-after-dhr={med(2, 6):.0f} "
-                      f"P2-gather-mma={med(7, 4):.0f} P2-cell+splitk+pub={med(5, 7):.0f}")
+                print(f"   full-batch: P0pub-to-HX-done={med(6, 1):.0f} P1-wait-after-HX={med(2, 6):.0f} "
+                      f"P2-dh-sum={med(7, 4):.0f} P2-cell+dx-partials+pub={med(5, 7):.0f}")
     # event timing of the persistent kernels
     lib.abcd_timing_reset()
     lib.abcd_timing_enable(1)

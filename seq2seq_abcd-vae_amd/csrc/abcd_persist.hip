@@ -3038,10 +3038,13 @@ static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
 }
 
 
-// ABCD_ENCBWD=w8: the 32-row / 8-member form (enc_bwd_w8)
+// enc_bwd_w8 by default (32-row groups of 8 members: half the split-K
+// exchange): same-box A/B at c2 against enc_bwd_sk, enc_bwd 1.90 / 1.89 ->
+// 1.60 / 1.59 ms per launch, step 9.51 / 9.53 -> 9.26 / 9.23 ms; c5gru 5.10 /
+// 5.21 -> 3.98 / 4.02 ms.  ABCD_ENCBWD=sk: enc_bwd_sk (A/B timing)
 static bool enc_bwd_w8_on() {
   const char* v = getenv("ABCD_ENCBWD");
-  return v && v[0] == 'w';
+  return !(v && v[0] == 's');
 }
 template <int G>
 static int launch_bwd_w8(hipStream_t s, const PBwdArgs& a, bool* launched) {

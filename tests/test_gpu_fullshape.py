@@ -40,8 +40,8 @@ LOSS_TOL = 1e-4
 GRAD_TOL = 1e-3
 
 KERNELS = {
-    "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_sk<4,16>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
-    "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_sk<3,16>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_w16<9,GRU>"),
+    "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_w8<4>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
+    "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_w8<3>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_w16<9,GRU>"),
 }
 # A/B runs of the earlier decoder BPTT forms (64-row groups of 32 members)
 _DB = os.environ.get("ABCD_DECBWD", "")
@@ -50,9 +50,9 @@ if _DB.startswith("s"):
     KERNELS = {r: k[:3] + (f"dec_bwd_sk<9,16,16,{r}>",) for r, k in KERNELS.items()}
 elif _DB.startswith("f"):
     KERNELS = {r: k[:3] + (f"dec_bwd_fold<9,16,{r}>",) for r, k in KERNELS.items()}
-W8 = os.environ.get("ABCD_ENCBWD", "").startswith("w")  # the 32-row / 8-member encoder BPTT
-if W8:
-    KERNELS = {r: (k[0], f"enc_bwd_w8<{4 if r == 'LSTM' else 3}>") + k[2:] for r, k in KERNELS.items()}
+W8 = not os.environ.get("ABCD_ENCBWD", "").startswith("s")  # the 32-row / 8-member encoder BPTT (default)
+if not W8:
+    KERNELS = {r: (k[0], f"enc_bwd_sk<{4 if r == 'LSTM' else 3},16>") + k[2:] for r, k in KERNELS.items()}
 
 # (bench config, batch, seed of the synthetic batch)
 CASES = [("c2", 512, 2024), ("c4", 512, 2025), ("c5", 128, 2026), ("c5gru", 128, 2027),
