@@ -114,8 +114,12 @@ def main():
                 print(f"   full-batch: cell-mma={med(7, 0):.0f} cell-epi+pub={med(1, 7):.0f} "
                       f"mlp-mma={med(6, 2):.0f} mlp-epi+pub={med(3, 6):.0f} step={med(5, 0):.0f}")
             else:
-                print(f"   full-batch: P0pub-to-HX-done={med(6, 1):.0f} P1-wait-after-HX={med(2, 6):.0f} "
-                      f"P2-dh-sum={med(7, 4):.0f} P2-cell+dx-partials+pub={med(5, 7):.0f}")
+                if os.environ.get("ABCD_STAMP_DIAG"):  # a library built with -DABCD_STAMP_DIAG (dec_bwd_w16)
+                    print(f"   full-batch P1: dZ-mma={med(6, 2):.0f} barrier+fold+stores={med(7, 6):.0f} "
+                          f"publish={med(3, 7):.0f}")
+                else:
+                    print(f"   full-batch: P0pub-to-HX-done={med(6, 1):.0f} P1-wait-after-HX={med(2, 6):.0f} "
+                          f"P2-dh-sum={med(7, 4):.0f} P2-cell+dx-partials+pub={med(5, 7):.0f}")
     # event timing of the persistent kernels
     lib.abcd_timing_reset()
     lib.abcd_timing_enable(1)

@@ -54,6 +54,9 @@ W8 = not os.environ.get("ABCD_ENCBWD", "").startswith("s")  # the 32-row / 8-mem
 if not W8:
     KERNELS = {r: (k[0], f"enc_bwd_sk<{4 if r == 'LSTM' else 3},16>") + k[2:] for r, k in KERNELS.items()}
 
+if os.environ.get("ABCD_NTLD") == "1":  # the nt-load gather forms (A/B runs)
+    KERNELS = {r: (k[0][:-1] + ",NT>", k[1], k[2][:-1] + ",NT>", k[3][:-1] + ",NT>") for r, k in KERNELS.items()}
+
 # (bench config, batch, seed of the synthetic batch)
 CASES = [("c2", 512, 2024), ("c4", 512, 2025), ("c5", 128, 2026), ("c5gru", 128, 2027),
          # the batch bench.py times at c5 / c5gru: 8 row groups, T_max = 512
