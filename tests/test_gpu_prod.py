@@ -40,10 +40,6 @@ for _r in EXPECT:
     elif _DB.startswith("f"):
         EXPECT[_r]["dec_bwd"] = f"dec_bwd_fold<9,16,{_r}>"
 W16 = not _DB.startswith(("f", "s"))  # the 32-row / 16-member decoder BPTT (default)
-if os.environ.get("ABCD_NTLD") == "1":  # the nt-load gather forms (A/B runs)
-    for _r in EXPECT:
-        for _k in ("enc_fwd", "dec_fwd", "dec_bwd"):
-            EXPECT[_r][_k] = EXPECT[_r][_k][:-1] + ",NT>"
 if os.environ.get("ABCD_ENCBWD", "").startswith("s"):  # A/B runs of the 64-row / 16-member encoder BPTT
     for _r in EXPECT:
         EXPECT[_r]["enc_bwd"] = f"enc_bwd_sk<{4 if _r == 'LSTM' else 3},16>"
