@@ -48,9 +48,7 @@ __device__ unsigned g_spin_limit = 1u << 22;    // polls before a hand-off wait 
 // K-contiguous operand read through a buffer resource with `sc1` (bypasses
 // this CU's L1, so it sees other workgroups' write-through stores); rows at
 // or beyond the resource's extent read as zero (hardware range check).
-// AUX: the load's cache policy, 16 = sc1; NTA (2 = nt) for the gathers whose
-// producers are all on the reader's XCD (see ntld below)
-template <int AUX = 16>
+template <int AUX = 16>  // the loads' cache policy (16 = sc1)
 struct BufKCt {
   __amdgpu_buffer_rsrc_t rs;
   uint32_t ld_bytes;
@@ -66,17 +64,6 @@ struct BufKCt {
   }
 };
 using BufKC = BufKCt<16>;
-// ABCD_NTLD=1 (experiment): hand-off gathers read with `nt` loads instead of
-// `sc1` when every producer of the data is on the reader's XCD (the groups
-// of group_role at ngroups % 8 == 0, HW_REG_XCC_ID-verified: scripts/xcc_map.py).
-// The producers store write-through (`sc1`: the store is acknowledged at the
-// memory side and drops the line from the XCD's L2), so the first reader
-// misses L2 and the group's other members may hit the line it brought in.
-constexpr int NTA = 2;
-static bool ntld_on(int ngroups) {
-  const char* v = getenv("ABCD_NTLD");
-  return v && v[0] == '1' && ngroups % 8 == 0;
-}
 // Two K segments back to back (e.g. [x | h] of a recurrent cell): chunks
 // [0, n0) come from segment 0, [n0, ntot) from segment 1; chunks >= ntot read
 // zero without touching memory (offset past the descriptor's extent).
@@ -283,7 +270,7 @@ DEV Role assign_role(int ngroups, int nmem) {
 // encoder forward: one launch per layer, both directions
 // ---------------------------------------------------------------------------
 // X6 > 0: split-fp32 recurrent MMA with X6 = H / 32 chunks (abcd_x6.h).
-template <int G, int PD, int X6, bool NT = false>
+template <int G, int PD, int X6>
 __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, nut = H / 16, nch = H / 16, T = a.T;
@@ -338,8 +325,8 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
     f4 acc[2][G];
     acc2_zero(acc);
     if (row0 < bs && prev_valid > 0) {
-      const BufKCt<NT ? NTA : 16> A{make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u),
-                                    (uint32_t)H * 4u};
+      const BufKC A{make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u),
+                    (uint32_t)H * 4u};
       if (X6) {
         wave_mma_x6<G, (X6 > 0 ? X6 : 1), 4>(acc[0], A, row0 + r, smem, X6, lane, q);
       } else {
@@ -1081,7 +1068,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 // the next step's Hprev rows) -- as two more tiles beside the mlp tile, and
 // carried in registers; step t+1's cell then waits only for x_{t+1} and runs
 // the NCC - 8 input chunks (H = 256: 8 recurrent chunks).
-template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, bool NT = false>
+template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
@@ -1149,7 +1136,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       // [x_t | h_{t-1}] in one ring (x is zero at t = 0: empty descriptor)
       const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.Xin + (size_t)o * Fp, t > 0 ? (uint32_t)bs * Fp * 4u : 0u);
       const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.Hprev + (size_t)o * H, (uint32_t)bs * H * 4u);
-      const BufKC2xt<NT ? NTA : 16> A{rx, rh, (uint32_t)Fp * 4u, (uint32_t)H * 4u, nx32, Fp};
+      const BufKC2x A{rx, rh, (uint32_t)Fp * 4u, (uint32_t)H * 4u, nx32, Fp};
       if (HPRE && i > 0) {
         acc[0] = acch[0];
         acc[1] = acch[1];
@@ -1219,7 +1206,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     if (has1) {
       f4 a1[1] = {f4zero()};
       if (row0 < bs) {
-        const BufKCt<NT ? NTA : 16> Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
+        const BufKC Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
         if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
@@ -1262,7 +1249,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     if (has2) {
       f4 ae[1] = {f4zero()};
       if (erow0 < bs) {
-        const BufKCt<NT ? NTA : 16> Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
+        const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
                        (uint32_t)2 * Hm * 4u};
         wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
                                 mem % NM32);
@@ -2184,7 +2171,7 @@ constexpr int W16_ROWS = 32;    // rows per group
 constexpr int W16_M = 16;       // members per group (16 units each)
 constexpr int W16_DTP = 68;     // pitch (floats) of the group's 32 x 64 dG tile in LDS
 constexpr int W16_ZTP = 36;     // pitch of the 32 x 32 dZ tile
-template <int NXS, bool GRU = false, bool NT = false>
+template <int NXS, bool GRU = false>
 __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   constexpr int H = 256, NHS = 16, GH = (GRU ? 3 : 4) * H, M = W16_M;
@@ -2377,8 +2364,7 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
       f4 acc[2][1];
       acc2_zero(acc);
       if (zrow0 < bs) {
-        const BufKCt<NT ? NTA : 16> A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u),
-                                      (uint32_t)Fp * 4u};
+        const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
         mma16<1>(acc, A, zrow0 + r, B1 + zj * nchx * 64, nchx, lane, q);
       }
       acc2_fold(acc);
@@ -2984,29 +2970,24 @@ static int ring_depth(int nch) { return nch % 16 == 0 ? 16 : (nch % 4 == 0 ? 4 :
 // x6 (split-fp32 on the bf16 matrix cores) for the compiled chunk counts
 static bool x6_enabled(int K) { return K == 64 || K == 128 || K == 256; }
 
-template <int G, int PD, int X6, bool NT = false>
-static int launch_fwd_k(hipStream_t s, const PFwdArgs& a, bool* launched) {
+template <int G, int PD, int X6>
+static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * (a.H / 16);
   const size_t lds = (size_t)G * 16 * a.H * (X6 ? 6 : 4) + (size_t)4 * TP_FLOATS * 4;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD, X6, NT>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(enc_fwd_persist<G, PD, X6>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PFwdArgs b = a;
   b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_ENC_FWD);
-    enc_fwd_persist<G, PD, X6, NT><<<grid, 256, lds, s>>>(b);
+    enc_fwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_ENC_FWD, "enc_fwd_persist<%d,%d,%d%s> grid %d", G, PD, X6, NT ? ",NT" : "", grid);
+  note_dispatch(TK_ENC_FWD, "enc_fwd_persist<%d,%d,%d> grid %d", G, PD, X6, grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
-}
-template <int G, int PD, int X6>
-static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
-  if (X6 && ntld_on(a.nd * a.nrt)) return launch_fwd_k<G, PD, X6, true>(s, a, launched);
-  return launch_fwd_k<G, PD, X6>(s, a, launched);
 }
 template <int G, int PD, int X6>
 static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
@@ -3166,13 +3147,13 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, bool NT = false>
+template <int NCC, int NH32, int NM32, bool GRU, bool HPRE>
 static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
   const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, NT>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
@@ -3180,10 +3161,9 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, NT><<<grid, 256, lds, s>>>(b);
+    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM",
-                NT ? ",NT" : "", grid);
+  note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -3192,7 +3172,6 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
 
 template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
-  if (ntld_on(a.nrt)) return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, true>(s, a, launched);
   return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true>(s, a, launched);
 }
 
@@ -3295,15 +3274,15 @@ static bool dec_bwd_w16_on() {
   const char* v = getenv("ABCD_DECBWD");
   return !(v && (v[0] == 'f' || v[0] == 's'));
 }
-template <int NXS, bool GRU, bool NT = false>
-static int launch_dec_bwd_w16_k(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+template <int NXS, bool GRU>
+static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   const int ng = cdiv(a.B, W16_ROWS), nchx = a.Fp / 16;
   const size_t lds = (size_t)NXS * 2 * 3 * 64 * 16 + (size_t)16 * 3 * 64 * 16 + (size_t)2 * nchx * 64 * 16 +
                      (size_t)W16_ROWS * (W16_DTP + W16_ZTP) * 4 + (size_t)2 * 64 * 16 + (size_t)4 * 2 * TP_FLOATS * 4;
   const int grid = ng * W16_M;
   if (a.B <= 0 || 2 * nchx > 4 * W16_M) return 0;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_w16<NXS, GRU, NT>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_w16<NXS, GRU>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, ng));
   PDecBwdArgs b = a;
@@ -3312,18 +3291,14 @@ static int launch_dec_bwd_w16_k(hipStream_t s, const PDecBwdArgs& a, bool* launc
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_w16<NXS, GRU, NT><<<grid, 256, lds, s>>>(b);
+    dec_bwd_w16<NXS, GRU><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_DEC_BWD, "dec_bwd_w16<%d,%s%s> grid %d", NXS, GRU ? "GRU" : "LSTM", NT ? ",NT" : "", grid);
+  note_dispatch(TK_DEC_BWD, "dec_bwd_w16<%d,%s> grid %d", NXS, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
 }
-template <int NXS, bool GRU>
-static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
-  if (ntld_on(cdiv(a.B, W16_ROWS))) return launch_dec_bwd_w16_k<NXS, GRU, true>(s, a, launched);
-  return launch_dec_bwd_w16_k<NXS, GRU>(s, a, launched);
-}
+
 
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {
   *launched = false;

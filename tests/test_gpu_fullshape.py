@@ -54,11 +54,6 @@ W8 = not os.environ.get("ABCD_ENCBWD", "").startswith("s")  # the 32-row / 8-mem
 if not W8:
     KERNELS = {r: (k[0], f"enc_bwd_sk<{4 if r == 'LSTM' else 3},16>") + k[2:] for r, k in KERNELS.items()}
 
-NTLD = os.environ.get("ABCD_NTLD") == "1"  # the nt-load gather forms (A/B runs): XCD-local groups only
-
-
-def _nt(kern, groups):
-    return kern[:-1] + ",NT>" if NTLD and groups % 8 == 0 else kern
 
 # (bench config, batch, seed of the synthetic batch)
 CASES = [("c2", 512, 2024), ("c4", 512, 2025), ("c5", 128, 2026), ("c5gru", 128, 2027),
@@ -107,9 +102,7 @@ def test_full_shape_step_vs_oracle(name, B, seed):
     grids = {"enc_fwd": tiles * 2 * 16, "enc_bwd": (B + 31) // 32 * 2 * 8 if W8 else tiles * 2 * 16,
              "dec_fwd": tiles * 32,
              "dec_bwd": (B + 31) // 32 * 16 if W16 else tiles * 32}
-    kerns = list(KERNELS[cfg["rnn"]])
-    kerns[0], kerns[2], kerns[3] = _nt(kerns[0], 2 * tiles), _nt(kerns[2], tiles), _nt(kerns[3], (B + 31) // 32)
-    for role, kern in zip(("enc_fwd", "enc_bwd", "dec_fwd", "dec_bwd"), kerns):
+    for role, kern in zip(("enc_fwd", "enc_bwd", "dec_fwd", "dec_bwd"), KERNELS[cfg["rnn"]]):
         assert ran[role][0] == f"{kern} grid {grids[role]}", (role, ran[role])
         assert ran[role][1] == 1, (role, ran[role])
     # the encoder's weight gradients: one gemm_wg2 launch for both directions (LSTM), split GEMMs (GRU)
