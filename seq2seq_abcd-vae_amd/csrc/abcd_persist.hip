@@ -2171,12 +2171,18 @@ constexpr int W16_ROWS = 32;    // rows per group
 constexpr int W16_M = 16;       // members per group (16 units each)
 constexpr int W16_DTP = 68;     // pitch (floats) of the group's 32 x 64 dG tile in LDS
 constexpr int W16_ZTP = 36;     // pitch of the 32 x 32 dZ tile
-template <int NXS, bool GRU = false>
+// ZX: the P1 dZ product on waves 0 / 1 only (row block w, both of the
+// member's dZ column tiles, x6 over K = Fp in ceil(Fp / 32) chunks): each
+// row block's dMU / dLV rows are loaded once per member instead of twice;
+// otherwise one (row block, tile) per wave in fp32 MFMA (mma16)
+template <int NXS, bool GRU = false, bool ZX = true>
 __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   constexpr int H = 256, NHS = 16, GH = (GRU ? 3 : 4) * H, M = W16_M;
   const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
   const int nchx = Fp / 16, nFt = Fp / 16;
+  constexpr int NCZ = (NXS > 0 ? NXS : 9) / 2 + 1;  // ZX: x6 chunks of K = Fp (Fp = 16 NXS with feedback)
+  const int ncz = (Fp + 31) / 32;
   const int ng = a.nrt;  // 32-row groups (the launcher's count)
   const Role role = assign_role(ng, M);
   const int grp = role.grp, mem = role.mem;
@@ -2192,7 +2198,7 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
   f4* DXI = smem;
   f4* W1X = DXI + NXS * 2 * 3 * 64;
   f4* B1 = W1X + NHS * 3 * 64;
-  float* DT = reinterpret_cast<float*>(B1 + 2 * nchx * 64);
+  float* DT = reinterpret_cast<float*>(B1 + (ZX ? 2 * ncz * 3 * 64 : 2 * nchx * 64));
   float* ZT = DT + W16_ROWS * W16_DTP;
   f4* DHX = reinterpret_cast<f4*>(ZT + W16_ROWS * W16_ZTP);
   float* tb = reinterpret_cast<float*>(DHX + 2 * 64) + w * 2 * TP_FLOATS;
@@ -2230,8 +2236,12 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
   }
   // P1 dZ column tiles 2 mem, 2 mem + 1 (mu tiles for mem < Hm / 32, else lv)
   const bool ismu = 2 * mem < Hm / 16;
-  stage_b_frag(B1, ismu ? a.W2mT : a.W2lT, Fp, 2, nchx,
-               [&](int j) { return 16 * (2 * mem + j) - (ismu ? 0 : Hm); });
+  if (ZX)
+    stage_x6(B1, ismu ? a.W2mT : a.W2lT, Fp, Fp, 2, ncz, 0, ncz,
+             [&](int j, int rr) { return 16 * (2 * mem + j) - (ismu ? 0 : Hm) + rr; });
+  else
+    stage_b_frag(B1, ismu ? a.W2mT : a.W2lT, Fp, 2, nchx,
+                 [&](int j) { return 16 * (2 * mem + j) - (ismu ? 0 : Hm); });
   // this wave's quarter of the W_hh image (units 64w .. 64w + 63), resident in registers
   bf8 Bh[4][2][3];
 #pragma unroll
@@ -2350,17 +2360,43 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
     PSTAMP(6);
 #endif
     // ---------------- P1: dZ tile -> this member's dh partials ----------------
-    float zpre[4];
+    float zpre[2][4];  // ZX: the activations of both tiles of row block w (waves 0 / 1)
     {
-      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (ZX && w >= 2) ? 0u : (uint32_t)bs * 2 * Hm * 4u);
+      const int zr0 = ZX ? rowg + 16 * w : zrow0;
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        zpre[g] = bld(rz, ((uint32_t)(zrow0 + 4 * q + g) * 2 * Hm + 32 * mem + 16 * zj + r) * 4u);
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          zpre[jj][g] = (ZX || jj == 0) ? bld(rz, ((uint32_t)(zr0 + 4 * q + g) * 2 * Hm + 32 * mem + 16 * (ZX ? jj : zj) + r) * 4u)
+                                        : 0.f;
     }
     gs.wait(3u * i + 1);
-    pin(zpre);
+    pin(zpre[0]), pin(zpre[1]);
     PSTAMP(2);
-    {
+    if (ZX) {
+      if (w < 2) {
+        const int zr0 = rowg + 16 * w;
+        f4 acc[2] = {f4zero(), f4zero()};
+        if (zr0 < bs) {
+          const __amdgpu_buffer_rsrc_t ra = make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u);
+          const BufKC2x A{ra, ra, (uint32_t)Fp * 4u, (uint32_t)Fp * 4u, ncz, Fp};  // k >= Fp reads 0
+          wave_mma_x6<2, NCZ, 4>(acc, A, zr0 + r, B1, ncz, lane, q);
+        }
+        const __amdgpu_buffer_rsrc_t rzs = make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          float dz[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) dz[g] = acc[jj][g] * (1.f - zpre[jj][g] * zpre[jj][g]);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) ZT[(16 * w + 4 * q + g) * W16_ZTP + 16 * jj + r] = dz[g];
+          const f4 zq = tp_quad(tb, dz, lane);
+          if (zr0 < bs) st4(rzs, (uint32_t)((zr0 + trow) * 2 * Hm + 32 * mem + 16 * jj + tcol) * 4u, zq, false);
+        }
+      }
+    } else {
+      float (&zp)[4] = zpre[0];
       f4 acc[2][1];
       acc2_zero(acc);
       if (zrow0 < bs) {
@@ -2370,7 +2406,7 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
       acc2_fold(acc);
       float dz[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) dz[g] = acc[0][0][g] * (1.f - zpre[g] * zpre[g]);
+      for (int g = 0; g < 4; ++g) dz[g] = acc[0][0][g] * (1.f - zp[g] * zp[g]);
       // the dZ tile for the fold (rows 16 zrb + .., columns 16 zj + r) and the stash
 #pragma unroll
       for (int g = 0; g < 4; ++g) ZT[(16 * zrb + 4 * q + g) * W16_ZTP + 16 * zj + r] = dz[g];
@@ -3274,15 +3310,17 @@ static bool dec_bwd_w16_on() {
   const char* v = getenv("ABCD_DECBWD");
   return !(v && (v[0] == 'f' || v[0] == 's'));
 }
-template <int NXS, bool GRU>
-static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
-  const int ng = cdiv(a.B, W16_ROWS), nchx = a.Fp / 16;
-  const size_t lds = (size_t)NXS * 2 * 3 * 64 * 16 + (size_t)16 * 3 * 64 * 16 + (size_t)2 * nchx * 64 * 16 +
+template <int NXS, bool GRU, bool ZX>
+static int launch_dec_bwd_w16_k(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+  const int ng = cdiv(a.B, W16_ROWS), nchx = a.Fp / 16, ncz = (a.Fp + 31) / 32;
+  const size_t b1 = ZX ? (size_t)2 * ncz * 3 * 64 * 16 : (size_t)2 * nchx * 64 * 16;
+  const size_t lds = (size_t)NXS * 2 * 3 * 64 * 16 + (size_t)16 * 3 * 64 * 16 + b1 +
                      (size_t)W16_ROWS * (W16_DTP + W16_ZTP) * 4 + (size_t)2 * 64 * 16 + (size_t)4 * 2 * TP_FLOATS * 4;
   const int grid = ng * W16_M;
   if (a.B <= 0 || 2 * nchx > 4 * W16_M) return 0;
+  if (ZX && ncz != (NXS > 0 ? NXS : 9) / 2 + 1) return 0;  // the kernel's compile-time chunk count
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_w16<NXS, GRU>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_w16<NXS, GRU, ZX>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, ng));
   PDecBwdArgs b = a;
@@ -3291,12 +3329,21 @@ static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launche
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_w16<NXS, GRU><<<grid, 256, lds, s>>>(b);
+    dec_bwd_w16<NXS, GRU, ZX><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_DEC_BWD, "dec_bwd_w16<%d,%s> grid %d", NXS, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
+}
+// ABCD_W16Z=0: the P1 dZ tiles on all four waves in fp32 MFMA (A/B timing)
+template <int NXS, bool GRU>
+static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+  const char* v = getenv("ABCD_W16Z");
+  if (v && v[0] == '0') return launch_dec_bwd_w16_k<NXS, GRU, false>(s, a, launched);
+  const int rc = launch_dec_bwd_w16_k<NXS, GRU, true>(s, a, launched);
+  if (rc || *launched) return rc;
+  return launch_dec_bwd_w16_k<NXS, GRU, false>(s, a, launched);
 }
 
 
