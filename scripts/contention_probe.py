@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-launch time of the four persistent kernels at c2 widths with EVERY
 sequence of length T (so every row group is full for all T steps), for
-B = 64 .. 512 (1 .. 8 row groups active at once).  If a step's latency were
+B = 32 .. 512 (the forward kernels run 64-row groups, 1 .. 8 active at once;
+dec_bwd_w16 / enc_bwd_w8 run 32-row groups, 1 .. 16).  If a step's latency were
 intrinsic to a group, the launch time would not depend on B; growth with B is
 chip-wide contention (the hand-off traffic of the groups sharing the
 MALL / HBM)."""
@@ -19,7 +20,7 @@ from modules import _native as N, noise  # noqa: E402
 
 def main():
     T = int(os.environ.get("PROBE_T", "200"))
-    for B in (64, 128, 256, 512):
+    for B in (32, 64, 128, 256, 512):
         cfg = dict(bench.CONFIGS["c2"], B=B, tmin=T, tmax=T)
         step = bench.build(cfg, "cuda")
         batch = bench.make_batch(cfg, 0, "cuda")
@@ -42,7 +43,7 @@ def main():
             lib.abcd_timing_read_kernel(kid, res)
             ms, n = res[0], res[1]
             out.append(f"{name} {ms / max(n, 1) * 1e3:8.1f} us ({ms / max(n, 1) * 1e3 / T:6.2f} us/step)")
-        print(f"B={B:4d} groups={B // 64}: " + "  ".join(out), flush=True)
+        print(f"B={B:4d} fwd groups={max(B // 64, 1)} bwd groups={B // 32}: " + "  ".join(out), flush=True)
         del step
 
 

@@ -1068,11 +1068,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 // the next step's Hprev rows) -- as two more tiles beside the mlp tile, and
 // carried in registers; step t+1's cell then waits only for x_{t+1} and runs
 // the NCC - 8 input chunks (H = 256: 8 recurrent chunks).
-// PL (experiment, ABCD_PLLD=1): the mlp and emit gathers (Hs / Aact rows:
-// 1-KiB / 2-KiB rows, so a 128-B line never spans two steps' rows, each row
-// written once per launch by a write-through store of a same-XCD member) read
-// with plain loads, so the group's 32 readers of a line may share it in L2
-template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, bool PL = false>
+template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
@@ -1210,7 +1206,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     if (has1) {
       f4 a1[1] = {f4zero()};
       if (row0 < bs) {
-        const BufKCt<PL ? 0 : 16> Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
+        const BufKC Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
         if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
@@ -1253,7 +1249,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     if (has2) {
       f4 ae[1] = {f4zero()};
       if (erow0 < bs) {
-        const BufKCt<PL ? 0 : 16> Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
+        const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
                        (uint32_t)2 * Hm * 4u};
         wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
                                 mem % NM32);
@@ -3187,13 +3183,13 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, bool PL = false>
+template <int NCC, int NH32, int NM32, bool GRU, bool HPRE>
 static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
   const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, PL>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
@@ -3201,7 +3197,7 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, PL><<<grid, 256, lds, s>>>(b);
+    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
@@ -3212,8 +3208,6 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
 
 template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
-  const char* v = getenv("ABCD_PLLD");
-  if (v && v[0] == '1' && a.nrt % 8 == 0) return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, true>(s, a, launched);
   return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true>(s, a, launched);
 }
 
