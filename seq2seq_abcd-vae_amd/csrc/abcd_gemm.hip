@@ -1287,14 +1287,243 @@ __global__ __launch_bounds__(256) void wg2_reduce_kernel(const float* slab, int 
   }
 }
 
+// ---------------------------------------------------------------------------
+// gemm_wg3: gemm_wg2's product with every operand split ONCE, in the staging
+// pass, and no VALU in the MFMA loop.  gemm_wg2 (above) keeps fp32 in LDS and
+// each wave splits the fragments it reads -- the A rows and the B columns
+// twice per workgroup, ~800 VALU per 32-deep chunk per wave against 312 MFMAs
+// whose issue gaps hide ~620 -- so its MFMA pipe idles about half the time
+// (PMC r07).  Here each thread splits the f4s it loaded into three bf16
+// planes stored [plane][k][col] with a k-row pitch that is an odd multiple of
+// 32 B, and the MFMA loop reads its operands with ds_read_b64_tr_b16 (4
+// k-rows x 16 columns per 16-lane group, delivered column-major).  The
+// 16-lane group g of a fragment reads k-rows 4g .. 4g + 3 and 16 + 4g ..
+// 16 + 4g + 3 (one permutation of k for both operands, so the sum is
+// unchanged), which puts the 8 rows of a 32-lane half on 8 distinct 32-B
+// bank slots: conflict-free.
+//   Tile 128 gate rows x one HALF of the NT = N1 + N2 columns (13 blocks of
+// 16; the two halves of a row tile are adjacent workgroups on one XCD, so
+// the second read of the dG tile is an L2 hit), 4 waves as 4 x 1 (32 rows x
+// 13 blocks, 104 accumulator registers).  Two stages of planes (2 x 66 KiB):
+// the next chunk's loads are issued before the MFMAs, split and stored into
+// the other stage between them, one barrier per chunk.
+// ---------------------------------------------------------------------------
 template <int N1, int N2>
+struct Wg3 {
+  static constexpr int NT = N1 + N2, NB = (NT + 15) / 16, NBH = (NB + 1) / 2, NH = 16 * NBH;  // cols per half
+  static constexpr int BM = 128, BK = 32, QH = NH / 4;  // f4 quads per k-row of a half
+  static constexpr int odd32(int bytes) { return (((bytes + 31) / 32) | 1) * 32; }
+  static constexpr int RA = odd32(BM * 2), RB = odd32(NH * 2);  // k-row pitch (bytes)
+  static constexpr int PA = BK * RA, PB = BK * RB;               // plane bytes
+  static constexpr int OB = 3 * PA, STG = 3 * (PA + PB);         // B planes' base, stage bytes
+  static constexpr int AV = BK * BM / 4 / 256, BVT = BK * QH, BV = (BVT + 255) / 256, NV = AV + BV;
+  static constexpr int SP = NH + 4;  // epilogue staging pitch (floats)
+  static constexpr int DUMMY = 2 * STG;                       // 64 lanes x 8 B of discarded stores
+  static constexpr size_t LDS = 2 * (size_t)STG + 512;
+  static_assert(N1 % 4 == 0 && N2 % 4 == 0 && (BK * BM / 4) % 256 == 0, "f4 staging");
+  static_assert(STG % 16 == 0 && LDS <= 160 * 1024 && (size_t)4 * 16 * SP * 4 <= LDS, "LDS");
+};
+
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+
+// 4 fp32 -> the three bf16 planes' 8-byte pieces (split8's decomposition)
+DEV void split4(const f4& x, u2v& h, u2v& m, u2v& l) {
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float a = x[2 * e], b = x[2 * e + 1];
+    const uint32_t hp = cvt_pk(a, b);
+    const float ra = a - lo_f(hp), rb = b - hi_f(hp);
+    const uint32_t mp = cvt_pk(ra, rb);
+    h[e] = hp;
+    m[e] = mp;
+    l[e] = cvt_pk(ra - lo_f(mp), rb - hi_f(mp));
+  }
+}
+
+template <int N1, int N2>
+__global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
+  using G = Wg3<N1, N2>;
+  constexpr int NT = G::NT, NBH = G::NBH, NH = G::NH, BM = G::BM, BK = G::BK;
+  constexpr int RA = G::RA, RB = G::RB, PA = G::PA, PB = G::PB, OB = G::OB, STG = G::STG;
+  constexpr int AV = G::AV, BV = G::BV, NV = G::NV;
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  char* const lds = reinterpret_cast<char*>(wsm);
+  const dim3 bid = xcd_tile(true);  // both halves of the row tiles of one (direction, K range) on one XCD
+  const int dz = bid.z, d = dz / a.Z, z = dz % a.Z;
+  const int half = bid.x & 1, m0 = (bid.x >> 1) * BM, M = a.M, n0 = half * NH;
+  const int kb = z * a.kps, ke = min(a.K, kb + a.kps);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.A[d], (uint32_t)((size_t)ke * a.lda * 4));
+  const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.B1[d], (uint32_t)((size_t)ke * a.ldb1 * 4));
+  const __amdgpu_buffer_rsrc_t r2 = make_rsrc(a.B2[d], (uint32_t)((size_t)ke * a.ldb2 * 4));
+  constexpr uint32_t OOB = 0x80000000u;
+  // this thread's f4s of a chunk: v < AV the dG rows; then the half's
+  // columns, per v from ONE source (a uniform buffer resource -- a per-lane
+  // choice would become a waterfall loop): half 0 = X's N1 columns (VX f4s
+  // per thread) then Hprev's first NH - N1, half 1 = Hprev's rest (zero pad
+  // beyond NT, never stored).  A global element offset at k0 = 0 (-1: read
+  // nothing) and a byte offset in plane 0 of a stage (-1: no store).
+  constexpr int QX = N1 / 4, QH0 = (NH - N1) / 4, QH1 = (NT - NH) / 4;
+  constexpr int VX = (BK * QX + 255) / 256;
+  static_assert(N1 <= NH && VX + (BK * QH0 + 255) / 256 <= BV && (BK * QH1 + 255) / 256 <= BV, "half layout");
+  int gof[NV], lof[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    if (v < AV) {
+      const int x = tid + 256 * v, k = x / (BM / 4), m = m0 + 4 * (x % (BM / 4));
+      gof[v] = m < M ? k * (int)a.lda + m : -1;
+      lof[v] = k * RA + 8 * (x % (BM / 4));
+      continue;
+    }
+    const int u = v - AV;
+    int k, c, n;  // k-row, local column, column in the source
+    bool in;
+    if (half == 0 && u < VX) {
+      const int x = tid + 256 * u;
+      in = x < BK * QX, k = x / QX, c = 4 * (x % QX), n = c;
+    } else if (half == 0) {
+      const int x = tid + 256 * (u - VX);
+      in = x < BK * QH0, k = x / QH0, c = N1 + 4 * (x % QH0), n = c - N1;
+    } else {
+      const int x = tid + 256 * u;
+      in = x < BK * QH1, k = x / QH1, c = 4 * (x % QH1), n = NH - N1 + c;
+    }
+    const long ld = (half == 0 && u < VX) ? a.ldb1 : a.ldb2;
+    gof[v] = in ? k * (int)ld + n : -1;
+    lof[v] = in ? OB + k * RB + 2 * c : -1;
+  }
+  auto ld4 = [](const __amdgpu_buffer_rsrc_t& rs, uint32_t o) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+  };
+  auto gload = [&](int k0, f4 (&raw)[NV]) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const bool x1 = v >= AV && half == 0 && v - AV < VX;  // uniform
+      const long ld = v < AV ? a.lda : x1 ? a.ldb1 : a.ldb2;
+      const uint32_t o = gof[v] < 0 ? OOB : (uint32_t)(((long)k0 * ld + gof[v]) * 4);
+      raw[v] = ld4(v < AV ? rA : x1 ? r1 : r2, o);
+    }
+  };
+  // split one f4 into the stage's three planes; branch-free (a branch would
+  // cut the MFMA loop into blocks the scheduler cannot interleave): an f4
+  // with no place stores to a per-lane dummy slot past the two stages
+  auto sstore = [&](int stage, int v, const f4& x) {
+    u2v h, m, l;
+    split4(x, h, m, l);
+    const bool ok = lof[v] >= 0;
+    char* base = lds + (ok ? stage * STG + lof[v] : G::DUMMY + 8 * lane);
+    const int pp = ok ? (v < AV ? PA : PB) : 0;
+    *reinterpret_cast<u2v*>(base) = h;
+    *reinterpret_cast<u2v*>(base + pp) = m;
+    *reinterpret_cast<u2v*>(base + 2 * pp) = l;
+  };
+  // lane's transposed-read offset: group q reads k-rows 4q + (r >> 2), columns 4 (r & 3) .. + 3
+  const int offA = (4 * q + (r >> 2)) * RA + 8 * (r & 3) + 2 * (32 * w);
+  const int offB = OB + (4 * q + (r >> 2)) * RB + 8 * (r & 3);
+  typedef __attribute__((address_space(3))) s4v lds_s4;
+  auto trf = [&](int off, int pitch) -> bf8 {  // k-rows at off and 16 further
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off + 16 * pitch));
+    return __builtin_bit_cast(bf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  f4 acc[2][NBH];
+  acc_zero(acc);
+  constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+  // the pad columns NT - n0 .. NH of both stages' B planes read as 0 (never stored)
+  for (int e = tid; n0 + NH > NT && e < 2 * 3 * BK * (n0 + NH - NT); e += 256) {
+    const int np = n0 + NH - NT, sp = e / (BK * np), x = e % (BK * np);
+    *reinterpret_cast<short*>(lds + (sp / 3) * STG + OB + (sp % 3) * PB + (x / np) * RB + 2 * (NT - n0 + x % np)) = 0;
+  }
+  {
+    f4 raw[NV];
+    gload(kb, raw);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) sstore(0, v, raw[v]);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    // branch-free: on the last chunk the loads read past the K range (0)
+    // and the stores fill the stage nobody reads again
+    f4 raw[NV];
+    gload(k0 + BK, raw);
+    const int sb = cur * STG;
+    bf8 ap[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) ap[i][p] = trf(sb + p * PA + offA + 2 * 16 * i, RA);
+    auto bload = [&](int j, bf8 (&bp)[3]) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bp[p] = trf(sb + p * PB + offB + 2 * 16 * j, RB);
+    };
+    bf8 bp[3];
+    bload(0, bp);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NBH; ++j) {
+      bf8 bq[3];
+      if (j + 1 < NBH) bload(j + 1, bq);
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][j] = mfma_bf(ap[i][TA[t]], bp[TB[t]], acc[i][j]);
+      // the next chunk's f4s split and stored into the other stage in the
+      // MFMA gaps of the later blocks (loaded before this chunk's first MFMA)
+      constexpr int J0 = NBH - NV;
+      if (j >= J0) sstore(cur ^ 1, j - J0, raw[j - J0]);
+      // order: the next block's 6 transposed reads first (12 MFMAs before
+      // their use), then each MFMA followed by two of the split's VALU, the
+      // plane stores last
+      if (j + 1 < NBH) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (j >= J0) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+      if (j >= J0) __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + 1 < NBH) bp[0] = bq[0], bp[1] = bq[1], bp[2] = bq[2];
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  // epilogue (gemm_wg2's): per 16-row block, a wave-private LDS transpose,
+  // then whole-row 16-B stores of the half's columns into this K range's slab [M][NT]
+  constexpr int SP = G::SP;
+  float* stg = wsm + w * 16 * SP;
+  float* const out = a.slab + (size_t)dz * M * NT;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < NBH; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < NBH; ++p) {  // 16 rows x 4 NBH quads = 64 NBH lanes' worth
+      const int e = lane + 64 * p, lr = e / (4 * NBH), c4 = e % (4 * NBH);
+      const int gcol = n0 + 4 * c4, grow = m0 + 32 * w + 16 * i + lr;
+      if (grow < M && gcol < NT)
+        *reinterpret_cast<f4*>(out + (size_t)grow * NT + gcol) = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int N1, int N2, bool W3>
 static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F, float* scratch,
                             size_t scratch_floats) {
-  using G = Wg2<N1, N2>;
+  using G = Wg2<N1, N2>;  // tile and slab geometry (gemm_wg3 shares it)
+  static_assert(Wg3<N1, N2>::BM == G::BM && Wg3<N1, N2>::NT == G::NT, "same tiles");
   const int mt = cdiv(M, G::BM);
   // one workgroup per CU: about 256 / (nd x mt) K ranges, the grid a multiple of 8
-  int Z = std::max(1, 256 / (nd * mt));
-  while ((nd * mt * Z) % 8) ++Z;
+  const int tw = W3 ? 2 * mt : mt;  // workgroups per (direction, K range)
+  int Z = std::max(1, 256 / (nd * tw));
+  while ((nd * tw * Z) % 8) ++Z;
   Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)nd * M * G::NT)));
   if (Z < 1) return -1;
   const int kps = ((cdiv(K, Z) + 31) / 32) * 32;
@@ -1307,12 +1536,16 @@ static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int
   }
   a.lda = M; a.ldb1 = N1; a.ldb2 = N2; a.M = M; a.K = K; a.kps = kps; a.Z = Z; a.slab = scratch;
   static bool attr = false;
+  const void* fn = W3 ? (const void*)gemm_wg3_kernel<N1, N2> : (const void*)gemm_wg2_kernel<N1, N2>;
+  const size_t lds = W3 ? Wg3<N1, N2>::LDS : G::LDS;
   if (!attr) {
-    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg2_kernel<N1, N2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)G::LDS));
+    ABCD_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  gemm_wg2_kernel<N1, N2><<<dim3(mt, 1, nd * Z), 256, G::LDS, s>>>(a);
+  if (W3)  // the two column halves of a row tile in adjacent x
+    gemm_wg3_kernel<N1, N2><<<dim3(2 * mt, 1, nd * Z), 256, lds, s>>>(a);
+  else
+    gemm_wg2_kernel<N1, N2><<<dim3(mt, 1, nd * Z), 256, lds, s>>>(a);
   ABCD_CHECK_LAUNCH();
   const long nq = (long)nd * M * G::NT / 4;
   wg2_reduce_kernel<<<(int)std::min<long>(2048, cdiv(nq, 256)), 256, 0, s>>>(scratch, nd, Z, M, G::NT, N1, F,
@@ -1332,8 +1565,16 @@ int wgrad_lstm_l0(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F,
   for (int d = 0; d < nd; ++d)
     if (((uintptr_t)dirs[d].dG | (uintptr_t)dirs[d].X | (uintptr_t)dirs[d].Hprev) & 15) return -1;
   if (M % 4) return -1;
-  if (Fp == 144 && H == 256) return wgrad_wg2_launch<144, 256>(s, nd, dirs, M, K, F, scratch, scratch_floats);
+  if (Fp == 144 && H == 256)
+    return wg3_on() ? wgrad_wg2_launch<144, 256, true>(s, nd, dirs, M, K, F, scratch, scratch_floats)
+                    : wgrad_wg2_launch<144, 256, false>(s, nd, dirs, M, K, F, scratch, scratch_floats);
   return -1;
+}
+
+// ABCD_WG3=0 selects gemm_wg2 (fragments split by every wave in the MFMA loop)
+bool wg3_on() {
+  const char* v = getenv("ABCD_WG3");
+  return !(v && v[0] == '0');
 }
 
 template <int MR, int NR, bool AKC, bool BKC>

@@ -109,6 +109,7 @@ struct WgOut {
   float* b_hh[2];
   float* w_hh[2];
 };
+bool wg3_on();  // gemm_wg3 (default) or gemm_wg2 for the layer-0 LSTM weight gradients
 int wgrad_lstm_l0(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F, int Fp, int H, float* scratch,
                   size_t scratch_floats);
 

@@ -30,13 +30,16 @@ def test_gemm_nt_vs_torch(M, N, K):
     assert err <= 1e-5 * K ** 0.5 * 4 + 1e-5, err
 
 
+@pytest.mark.parametrize("wg", ["3", "2"])
 @pytest.mark.parametrize("nd,F,H,K", [(2, 129, 256, 65583), (1, 129, 256, 3001), (2, 130, 256, 777), (2, 33, 48, 500),
-                                       (1, 20, 24, 64)])
-def test_lstm_wgrad_vs_torch(nd, F, H, K):
+                                       (1, 20, 24, 64), (2, 129, 256, 31), (1, 143, 256, 100003)])
+def test_lstm_wgrad_vs_torch(nd, F, H, K, wg, monkeypatch):
     """abcd_lstm_wgrad (the LSTM layer's w_ih, b_ih, b_hh, w_hh gradients from
-    the gate gradients, model.py:53,60-66): gemm_wg2 at F <= 143, H = 256
-    (the c2 shape first, both directions), the split-GEMM route elsewhere --
-    against float64 torch."""
+    the gate gradients, model.py:53,60-66): gemm_wg3 (default) or gemm_wg2
+    (ABCD_WG3=0) at F <= 143, H = 256 (the c2 shape first, both directions;
+    a K below one chunk; the widest F with a K range that is not a multiple
+    of 32), the split-GEMM route elsewhere -- against float64 torch."""
+    monkeypatch.setenv("ABCD_WG3", "1" if wg == "3" else "0")
     import ctypes
     from modules import _native as Nn
     g = torch.Generator(device="cuda").manual_seed(nd * 7 + F + H + K)
@@ -56,7 +59,7 @@ def test_lstm_wgrad_vs_torch(nd, F, H, K):
                                       Nn.ptr(ws), ws.numel(), Nn.stream()), "lstm wgrad")
     torch.cuda.synchronize()
     route = Nn.dispatch()["enc_wgrad"][0]
-    assert route == (f"gemm_wg2<144,{H}> x{nd}" if (H == 256 and F <= 143 and (F + 16) // 16 * 16 == 144)
+    assert route == (f"gemm_wg{wg}<144,{H}> x{nd}" if (H == 256 and F <= 143 and (F + 16) // 16 * 16 == 144)
                      else "gemm split (x6s/x6t)"), route
     rel = lambda a, b: ((a.double() - b).abs().max() / b.abs().max()).item()
     for d in range(nd):

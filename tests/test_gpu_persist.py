@@ -116,20 +116,22 @@ def _with_env(key, val, fn):
             os.environ[key] = old
 
 
+@pytest.mark.parametrize("wg", ["3", "2"])
 @pytest.mark.parametrize("B,Tmax", [(70, 30), (512, 200)])
-def test_encoder_wgrad_wg2(B, Tmax):
-    """The layer-0 bi-LSTM weight gradients through gemm_wg2 (one launch for
-    both directions: [dW_ih | db | dW_hh] = dG^T [X | 1 | Hprev], F = 129,
-    H = 256) against the split GEMM route (ABCD_WG2=0) and, at the small
-    batch, against torch.nn.LSTM in float64 (model.py:53,60-66)."""
+def test_encoder_wgrad_wg2(B, Tmax, wg):
+    """The layer-0 bi-LSTM weight gradients through gemm_wg3 (default) and
+    gemm_wg2 (ABCD_WG3=0) -- one launch for both directions: [dW_ih | db |
+    dW_hh] = dG^T [X | 1 | Hprev], F = 129, H = 256 -- against the split GEMM
+    route (ABCD_WG2=0) and, at the small batch, against torch.nn.LSTM in
+    float64 (model.py:53,60-66)."""
     from modules import _native as Nn
     F, H = 129, 256
     enc = _enc(F, H, "LSTM", 1, True, seed=5)
     packed = _batch(B, Tmax, F, seed=9)
     dout = torch.randn(B, enc.hidden_size_total, device="cuda")
     Nn.lib().abcd_dispatch_reset()
-    out_n, g_n = _run(enc, packed, dout, persist=True)
-    assert Nn.dispatch()["enc_wgrad"] == ("gemm_wg2<144,256> x2", 1)
+    out_n, g_n = _with_env("ABCD_WG3", "1" if wg == "3" else "0", lambda: _run(enc, packed, dout, persist=True))
+    assert Nn.dispatch()["enc_wgrad"] == (f"gemm_wg{wg}<144,256> x2", 1)
     out_o, g_o = _with_env("ABCD_WG2", "0", lambda: _run(enc, packed, dout, persist=True))
     assert Nn.dispatch()["enc_wgrad"] == ("gemm split (x6s/x6t)", 2)
     assert torch.equal(out_n, out_o)
