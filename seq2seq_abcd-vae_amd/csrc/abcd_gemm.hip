@@ -1396,14 +1396,24 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
   auto ld4 = [](const __amdgpu_buffer_rsrc_t& rs, uint32_t o) {
     return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
   };
+  // byte offsets at k0 = 0, OOB (2^31: stays past every buffer's 2^31-byte
+  // bound after adding k0 rows) for nothing to read; the row pitch of each
+  // v's source in bytes (uniform)
+  uint32_t gob[NV];
+  uint32_t rowb[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const bool x1 = v >= AV && half == 0 && v - AV < VX;
+    rowb[v] = 4u * (uint32_t)(v < AV ? a.lda : x1 ? a.ldb1 : a.ldb2);
+    gob[v] = gof[v] < 0 ? OOB : 4u * (uint32_t)gof[v];
+  }
+  auto gload1 = [&](int k0, int v) -> f4 {
+    const bool x1 = v >= AV && half == 0 && v - AV < VX;  // uniform
+    return ld4(v < AV ? rA : x1 ? r1 : r2, gob[v] + (uint32_t)k0 * rowb[v]);
+  };
   auto gload = [&](int k0, f4 (&raw)[NV]) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const bool x1 = v >= AV && half == 0 && v - AV < VX;  // uniform
-      const long ld = v < AV ? a.lda : x1 ? a.ldb1 : a.ldb2;
-      const uint32_t o = gof[v] < 0 ? OOB : (uint32_t)(((long)k0 * ld + gof[v]) * 4);
-      raw[v] = ld4(v < AV ? rA : x1 ? r1 : r2, o);
-    }
+    for (int v = 0; v < NV; ++v) raw[v] = gload1(k0, v);
   };
   // split one f4 into the stage's three planes; branch-free (a branch would
   // cut the MFMA loop into blocks the scheduler cannot interleave): an f4
@@ -1435,19 +1445,18 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
     const int np = n0 + NH - NT, sp = e / (BK * np), x = e % (BK * np);
     *reinterpret_cast<short*>(lds + (sp / 3) * STG + OB + (sp % 3) * PB + (x / np) * RB + 2 * (NT - n0 + x % np)) = 0;
   }
-  {
-    f4 raw[NV];
-    gload(kb, raw);
+  // raw holds chunk c + 1 while chunk c multiplies; each f4 is reloaded with
+  // chunk c + 2 right after its split, so every load has a whole chunk of
+  // MFMAs to land (loads past the K range read 0; on the last chunks the
+  // splits fill the stage nobody reads again: branch-free)
+  f4 raw[NV];
+  gload(kb, raw);
 #pragma unroll
-    for (int v = 0; v < NV; ++v) sstore(0, v, raw[v]);
-  }
+  for (int v = 0; v < NV; ++v) sstore(0, v, raw[v]);
+  gload(kb + BK, raw);
   __syncthreads();
   int cur = 0;
   for (int k0 = kb; k0 < ke; k0 += BK) {
-    // branch-free: on the last chunk the loads read past the K range (0)
-    // and the stores fill the stage nobody reads again
-    f4 raw[NV];
-    gload(k0 + BK, raw);
     const int sb = cur * STG;
     bf8 ap[2][3];
 #pragma unroll
@@ -1472,7 +1481,10 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
       // the next chunk's f4s split and stored into the other stage in the
       // MFMA gaps of the later blocks (loaded before this chunk's first MFMA)
       constexpr int J0 = NBH - NV;
-      if (j >= J0) sstore(cur ^ 1, j - J0, raw[j - J0]);
+      if (j >= J0) {
+        sstore(cur ^ 1, j - J0, raw[j - J0]);
+        raw[j - J0] = gload1(k0 + 2 * BK, j - J0);
+      }
       // order: the next block's 6 transposed reads first (12 MFMAs before
       // their use), then each MFMA followed by two of the split's VALU, the
       // plane stores last
@@ -1482,7 +1494,10 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if (j >= J0) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
       }
-      if (j >= J0) __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+      if (j >= J0) {
+        __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       if (j + 1 < NBH) bp[0] = bq[0], bp[1] = bq[1], bp[2] = bq[2];
     }
