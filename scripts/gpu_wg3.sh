@@ -1,4 +1,4 @@
-# GPU box: gemm_wg3 (pre-split planes, transposed LDS reads) parity and same-box A/B against gemm_wg2
+# GPU box: gemm_wg3 (pre-split planes, transposed LDS reads, 8 waves) parity and same-box A/B against gemm_wg2
 set -e
 OUT=gpurun_out/wg3
 mkdir -p $OUT
@@ -9,5 +9,7 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_fullshape.py -x -q --timeou
 tail -1 $OUT/pytest_full.log
 bash scripts/ab_env.sh ABCD_WG3 "0 1" > $OUT/ab.log 2>&1; cat $OUT/ab.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/prof.err
-grep -h "gemm_wg" $OUT/prof/*/run_kernel_stats.csv $OUT/prof/run_kernel_stats.csv 2>/dev/null | cut -c1-200 || true
+python scripts/step_timeline.py $(find $OUT/prof -name "run_kernel_trace.csv" | head -1) > $OUT/timeline.txt
+grep -h "gemm_wg" $OUT/prof/run_kernel_stats.csv | cut -c1-200 || true
+tail -30 $OUT/timeline.txt | cut -c1-110
 echo wg3 done

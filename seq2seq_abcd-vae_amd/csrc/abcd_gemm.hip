@@ -1308,20 +1308,25 @@ __global__ __launch_bounds__(256) void wg2_reduce_kernel(const float* slab, int 
 // the next chunk's loads are issued before the MFMAs, split and stored into
 // the other stage between them, one barrier per chunk.
 // ---------------------------------------------------------------------------
-template <int N1, int N2>
+template <int N1, int N2, int W = 4>
 struct Wg3 {
   static constexpr int NT = N1 + N2, NB = (NT + 15) / 16, NBH = (NB + 1) / 2, NH = 16 * NBH;  // cols per half
-  static constexpr int BM = 128, BK = 32, QH = NH / 4;  // f4 quads per k-row of a half
+  static constexpr int BM = 128, BK = 32, T = 64 * W, RW = BM / W, MI = RW / 16;  // rows / 16-row blocks per wave
   static constexpr int odd32(int bytes) { return (((bytes + 31) / 32) | 1) * 32; }
   static constexpr int RA = odd32(BM * 2), RB = odd32(NH * 2);  // k-row pitch (bytes)
   static constexpr int PA = BK * RA, PB = BK * RB;               // plane bytes
   static constexpr int OB = 3 * PA, STG = 3 * (PA + PB);         // B planes' base, stage bytes
-  static constexpr int AV = BK * BM / 4 / 256, BVT = BK * QH, BV = (BVT + 255) / 256, NV = AV + BV;
+  // f4s per thread: the dG rows, then the half's columns (half 0: X's, then
+  // Hprev's first NH - N1; half 1: Hprev's rest), each v from one source
+  static constexpr int QX = N1 / 4, QH0 = (NH - N1) / 4, QH1 = (NT - NH) / 4;
+  static constexpr int VX = (BK * QX + T - 1) / T, V0 = VX + (BK * QH0 + T - 1) / T, V1 = (BK * QH1 + T - 1) / T;
+  static constexpr int AV = BK * BM / 4 / T, BV = V0 > V1 ? V0 : V1, NV = AV + BV;
   static constexpr int SP = NH + 4;  // epilogue staging pitch (floats)
   static constexpr int DUMMY = 2 * STG;                       // 64 lanes x 8 B of discarded stores
   static constexpr size_t LDS = 2 * (size_t)STG + 512;
-  static_assert(N1 % 4 == 0 && N2 % 4 == 0 && (BK * BM / 4) % 256 == 0, "f4 staging");
-  static_assert(STG % 16 == 0 && LDS <= 160 * 1024 && (size_t)4 * 16 * SP * 4 <= LDS, "LDS");
+  static_assert(N1 % 4 == 0 && N2 % 4 == 0 && (BK * BM / 4) % T == 0 && RW % 16 == 0 && N1 <= NH, "staging");
+  static_assert(STG % 16 == 0 && LDS <= 160 * 1024 && (size_t)W * 16 * SP * 4 <= LDS, "LDS");
+  static_assert(NV <= NBH, "one f4 split per MFMA block");
 };
 
 typedef short s4v __attribute__((ext_vector_type(4)));
@@ -1341,12 +1346,14 @@ DEV void split4(const f4& x, u2v& h, u2v& m, u2v& l) {
   }
 }
 
-template <int N1, int N2>
-__global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
-  using G = Wg3<N1, N2>;
-  constexpr int NT = G::NT, NBH = G::NBH, NH = G::NH, BM = G::BM, BK = G::BK;
+// DIAG (timing probes only, wrong results; ABCD_WG3DIAG): 1 = no splits or
+// plane stores in the loop, 2 = no MFMAs, 3 = the loads alone, 4 = no loads
+template <int N1, int N2, int W, int DIAG = 0>
+__global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
+  using G = Wg3<N1, N2, W>;
+  constexpr int NT = G::NT, NBH = G::NBH, NH = G::NH, BM = G::BM, BK = G::BK, T = G::T, RW = G::RW, MI = G::MI;
   constexpr int RA = G::RA, RB = G::RB, PA = G::PA, PB = G::PB, OB = G::OB, STG = G::STG;
-  constexpr int AV = G::AV, BV = G::BV, NV = G::NV;
+  constexpr int AV = G::AV, NV = G::NV, QX = G::QX, QH0 = G::QH0, QH1 = G::QH1, VX = G::VX;
   extern __shared__ __attribute__((aligned(16))) float wsm[];
   char* const lds = reinterpret_cast<char*>(wsm);
   const dim3 bid = xcd_tile(true);  // both halves of the row tiles of one (direction, K range) on one XCD
@@ -1364,14 +1371,11 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
   // per thread) then Hprev's first NH - N1, half 1 = Hprev's rest (zero pad
   // beyond NT, never stored).  A global element offset at k0 = 0 (-1: read
   // nothing) and a byte offset in plane 0 of a stage (-1: no store).
-  constexpr int QX = N1 / 4, QH0 = (NH - N1) / 4, QH1 = (NT - NH) / 4;
-  constexpr int VX = (BK * QX + 255) / 256;
-  static_assert(N1 <= NH && VX + (BK * QH0 + 255) / 256 <= BV && (BK * QH1 + 255) / 256 <= BV, "half layout");
   int gof[NV], lof[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     if (v < AV) {
-      const int x = tid + 256 * v, k = x / (BM / 4), m = m0 + 4 * (x % (BM / 4));
+      const int x = tid + T * v, k = x / (BM / 4), m = m0 + 4 * (x % (BM / 4));
       gof[v] = m < M ? k * (int)a.lda + m : -1;
       lof[v] = k * RA + 8 * (x % (BM / 4));
       continue;
@@ -1380,13 +1384,13 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
     int k, c, n;  // k-row, local column, column in the source
     bool in;
     if (half == 0 && u < VX) {
-      const int x = tid + 256 * u;
+      const int x = tid + T * u;
       in = x < BK * QX, k = x / QX, c = 4 * (x % QX), n = c;
     } else if (half == 0) {
-      const int x = tid + 256 * (u - VX);
+      const int x = tid + T * (u - VX);
       in = x < BK * QH0, k = x / QH0, c = N1 + 4 * (x % QH0), n = c - N1;
     } else {
-      const int x = tid + 256 * u;
+      const int x = tid + T * u;
       in = x < BK * QH1, k = x / QH1, c = 4 * (x % QH1), n = NH - N1 + c;
     }
     const long ld = (half == 0 && u < VX) ? a.ldb1 : a.ldb2;
@@ -1429,7 +1433,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
     *reinterpret_cast<u2v*>(base + 2 * pp) = l;
   };
   // lane's transposed-read offset: group q reads k-rows 4q + (r >> 2), columns 4 (r & 3) .. + 3
-  const int offA = (4 * q + (r >> 2)) * RA + 8 * (r & 3) + 2 * (32 * w);
+  const int offA = (4 * q + (r >> 2)) * RA + 8 * (r & 3) + 2 * (RW * w);
   const int offB = OB + (4 * q + (r >> 2)) * RB + 8 * (r & 3);
   typedef __attribute__((address_space(3))) s4v lds_s4;
   auto trf = [&](int off, int pitch) -> bf8 {  // k-rows at off and 16 further
@@ -1437,11 +1441,11 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
     const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off + 16 * pitch));
     return __builtin_bit_cast(bf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
-  f4 acc[2][NBH];
+  f4 acc[MI][NBH];
   acc_zero(acc);
   constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
   // the pad columns NT - n0 .. NH of both stages' B planes read as 0 (never stored)
-  for (int e = tid; n0 + NH > NT && e < 2 * 3 * BK * (n0 + NH - NT); e += 256) {
+  for (int e = tid; n0 + NH > NT && e < 2 * 3 * BK * (n0 + NH - NT); e += T) {
     const int np = n0 + NH - NT, sp = e / (BK * np), x = e % (BK * np);
     *reinterpret_cast<short*>(lds + (sp / 3) * STG + OB + (sp % 3) * PB + (x / np) * RB + 2 * (NT - n0 + x % np)) = 0;
   }
@@ -1449,23 +1453,22 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
   // chunk c + 2 right after its split, so every load has a whole chunk of
   // MFMAs to land (loads past the K range read 0; on the last chunks the
   // splits fill the stage nobody reads again: branch-free)
-  f4 raw[NV];
-  gload(kb, raw);
-#pragma unroll
-  for (int v = 0; v < NV; ++v) sstore(0, v, raw[v]);
-  gload(kb + BK, raw);
-  __syncthreads();
-  int cur = 0;
-  for (int k0 = kb; k0 < ke; k0 += BK) {
+  // two register sets of raw f4s, each a chunk ahead of the other: while
+  // chunk c multiplies, one set (chunk c + 1) is split into the other stage
+  // and each f4 reloaded with chunk c + 3 right after its split, so every load
+  // has two chunks of MFMAs to land (loads past the K range read 0; chunks
+  // past it multiply zeros; all branch-free).  The loop runs chunk pairs so
+  // the sets swap roles without register moves.
+  auto chunk = [&](int k0, int cur, f4 (&rw)[NV]) {
     const int sb = cur * STG;
-    bf8 ap[2][3];
+    bf8 ap[MI][3];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) ap[i][p] = trf(sb + p * PA + offA + 2 * 16 * i, RA);
+      for (int p = 0; p < 3; ++p) ap[i][p] = DIAG == 3 ? bf8{} : trf(sb + p * PA + offA + 2 * 16 * i, RA);
     auto bload = [&](int j, bf8 (&bp)[3]) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bp[p] = trf(sb + p * PB + offB + 2 * 16 * j, RB);
+      for (int p = 0; p < 3; ++p) bp[p] = DIAG == 3 ? bf8{} : trf(sb + p * PB + offB + 2 * 16 * j, RB);
     };
     bf8 bp[3];
     bload(0, bp);
@@ -1477,20 +1480,24 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
 #pragma unroll
       for (int t = 0; t < 6; ++t)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][j] = mfma_bf(ap[i][TA[t]], bp[TB[t]], acc[i][j]);
+        for (int i = 0; i < MI; ++i)
+          if (DIAG == 3) {
+          } else if (DIAG != 2) acc[i][j] = mfma_bf(ap[i][TA[t]], bp[TB[t]], acc[i][j]);
+          else acc[i][j][0] += (float)ap[i][TA[t]][0] * (float)bp[TB[t]][1];
       // the next chunk's f4s split and stored into the other stage in the
-      // MFMA gaps of the later blocks (loaded before this chunk's first MFMA)
+      // MFMA gaps of the later blocks
       constexpr int J0 = NBH - NV;
       if (j >= J0) {
-        sstore(cur ^ 1, j - J0, raw[j - J0]);
-        raw[j - J0] = gload1(k0 + 2 * BK, j - J0);
+        if (DIAG != 1 && DIAG != 3) sstore(cur ^ 1, j - J0, rw[j - J0]);
+        else acc[0][j][1] += rw[j - J0][0];
+        if (DIAG != 4) rw[j - J0] = gload1(k0 + 3 * BK, j - J0);
       }
       // order: the next block's 6 transposed reads first (12 MFMAs before
       // their use), then each MFMA followed by two of the split's VALU, the
-      // plane stores last
+      // plane stores and the reload last
       if (j + 1 < NBH) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
-      for (int k = 0; k < 12; ++k) {
+      for (int k = 0; k < 6 * MI; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if (j >= J0) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
       }
@@ -1502,7 +1509,17 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
       if (j + 1 < NBH) bp[0] = bq[0], bp[1] = bq[1], bp[2] = bq[2];
     }
     __syncthreads();
-    cur ^= 1;
+  };
+  f4 rawA[NV], rawB[NV];
+  gload(kb, rawA);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) sstore(0, v, rawA[v]);
+  gload(kb + BK, rawA);
+  gload(kb + 2 * BK, rawB);
+  __syncthreads();
+  for (int k0 = kb; k0 < ke; k0 += 2 * BK) {
+    chunk(k0, 0, rawA);
+    chunk(k0 + BK, 1, rawB);
   }
   // epilogue (gemm_wg2's): per 16-row block, a wave-private LDS transpose,
   // then whole-row 16-B stores of the half's columns into this K range's slab [M][NT]
@@ -1510,7 +1527,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
   float* stg = wsm + w * 16 * SP;
   float* const out = a.slab + (size_t)dz * M * NT;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < MI; ++i) {
 #pragma unroll
     for (int j = 0; j < NBH; ++j)
 #pragma unroll
@@ -1520,7 +1537,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
 #pragma unroll
     for (int p = 0; p < NBH; ++p) {  // 16 rows x 4 NBH quads = 64 NBH lanes' worth
       const int e = lane + 64 * p, lr = e / (4 * NBH), c4 = e % (4 * NBH);
-      const int gcol = n0 + 4 * c4, grow = m0 + 32 * w + 16 * i + lr;
+      const int gcol = n0 + 4 * c4, grow = m0 + RW * w + 16 * i + lr;
       if (grow < M && gcol < NT)
         *reinterpret_cast<f4*>(out + (size_t)grow * NT + gcol) = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
     }
@@ -1529,11 +1546,35 @@ __global__ __launch_bounds__(256, 1) void gemm_wg3_kernel(WgArgs a) {
   }
 }
 
+template <int N1, int N2, int W, int DIAG>
+static int wg3_go1(hipStream_t s, const WgArgs& a, dim3 grid) {
+  constexpr size_t lds = Wg3<N1, N2, W>::LDS;
+  static bool attr = false;
+  if (!attr) {
+    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg3_kernel<N1, N2, W, DIAG>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  gemm_wg3_kernel<N1, N2, W, DIAG><<<grid, 64 * W, lds, s>>>(a);
+  return 0;
+}
+
+template <int N1, int N2, int W>
+static int wg3_go(hipStream_t s, const WgArgs& a, dim3 grid, int diag) {
+  switch (diag) {
+    case 1: return wg3_go1<N1, N2, W, 1>(s, a, grid);
+    case 2: return wg3_go1<N1, N2, W, 2>(s, a, grid);
+    case 3: return wg3_go1<N1, N2, W, 3>(s, a, grid);
+    case 4: return wg3_go1<N1, N2, W, 4>(s, a, grid);
+    default: return wg3_go1<N1, N2, W, 0>(s, a, grid);
+  }
+}
+
 template <int N1, int N2, bool W3>
 static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F, float* scratch,
                             size_t scratch_floats) {
   using G = Wg2<N1, N2>;  // tile and slab geometry (gemm_wg3 shares it)
-  static_assert(Wg3<N1, N2>::BM == G::BM && Wg3<N1, N2>::NT == G::NT, "same tiles");
+  static_assert(Wg3<N1, N2>::BM == G::BM && Wg3<N1, N2>::NT == G::NT, "same slab geometry");
   const int mt = cdiv(M, G::BM);
   // one workgroup per CU: about 256 / (nd x mt) K ranges, the grid a multiple of 8
   const int tw = W3 ? 2 * mt : mt;  // workgroups per (direction, K range)
@@ -1541,7 +1582,8 @@ static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int
   while ((nd * tw * Z) % 8) ++Z;
   Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)nd * M * G::NT)));
   if (Z < 1) return -1;
-  const int kps = ((cdiv(K, Z) + 31) / 32) * 32;
+  // gemm_wg3 runs chunk pairs: K ranges of whole pairs
+  const int kq = W3 ? 64 : 32, kps = ((cdiv(K, Z) + kq - 1) / kq) * kq;
   Z = cdiv(K, kps);
   WgArgs a{};
   WgOut o{};
@@ -1550,17 +1592,23 @@ static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int
     o.w_ih[d] = dirs[d].w_ih; o.b_ih[d] = dirs[d].b_ih; o.b_hh[d] = dirs[d].b_hh; o.w_hh[d] = dirs[d].w_hh;
   }
   a.lda = M; a.ldb1 = N1; a.ldb2 = N2; a.M = M; a.K = K; a.kps = kps; a.Z = Z; a.slab = scratch;
-  static bool attr = false;
-  const void* fn = W3 ? (const void*)gemm_wg3_kernel<N1, N2> : (const void*)gemm_wg2_kernel<N1, N2>;
-  const size_t lds = W3 ? Wg3<N1, N2>::LDS : G::LDS;
-  if (!attr) {
-    ABCD_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
+  if (!W3) {
+    static bool attr = false;
+    if (!attr) {
+      ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg2_kernel<N1, N2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)G::LDS));
+      attr = true;
+    }
+    gemm_wg2_kernel<N1, N2><<<dim3(mt, 1, nd * Z), 256, G::LDS, s>>>(a);
+  } else {
+    // the two column halves of a row tile in adjacent x; ABCD_WG3W = 4 or 8
+    // waves; ABCD_WG3DIAG: the timing probes (wrong results)
+    const char* dg = getenv("ABCD_WG3DIAG");
+    const char* wv = getenv("ABCD_WG3W");
+    const int diag = dg ? atoi(dg) : 0, waves = wv && wv[0] == '4' ? 4 : 8;
+    ABCD_TRY((hipError_t)(waves == 8 ? wg3_go<N1, N2, 8>(s, a, dim3(2 * mt, 1, nd * Z), diag)
+                                     : wg3_go<N1, N2, 4>(s, a, dim3(2 * mt, 1, nd * Z), diag)));
   }
-  if (W3)  // the two column halves of a row tile in adjacent x
-    gemm_wg3_kernel<N1, N2><<<dim3(2 * mt, 1, nd * Z), 256, lds, s>>>(a);
-  else
-    gemm_wg2_kernel<N1, N2><<<dim3(mt, 1, nd * Z), 256, lds, s>>>(a);
   ABCD_CHECK_LAUNCH();
   const long nq = (long)nd * M * G::NT / 4;
   wg2_reduce_kernel<<<(int)std::min<long>(2048, cdiv(nq, 256)), 256, 0, s>>>(scratch, nd, Z, M, G::NT, N1, F,
