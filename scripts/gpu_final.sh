@@ -12,4 +12,5 @@ tail -1 gpurun_out/$TAG/smoke.log
 bash scripts/gpu_profile.sh $TAG
 bash scripts/gpu_timeline.sh ${TAG}tl
 timeout -k 10 240 python -u scripts/persist_stamps.py > gpurun_out/$TAG/persist_phase_stamps.log 2>&1
+timeout -k 10 300 python -u scripts/contention_probe.py > gpurun_out/$TAG/contention_probe.log 2>&1
 echo final done
