@@ -1308,10 +1308,13 @@ __global__ __launch_bounds__(256) void wg2_reduce_kernel(const float* slab, int 
 // the next chunk's loads are issued before the MFMAs, split and stored into
 // the other stage between them, one barrier per chunk.
 // ---------------------------------------------------------------------------
-template <int N1, int N2, int W = 4>
+template <int N1, int N2, int W = 4, int WN = 1>
 struct Wg3 {
   static constexpr int NT = N1 + N2, NB = (NT + 15) / 16, NBH = (NB + 1) / 2, NH = 16 * NBH;  // cols per half
-  static constexpr int BM = 128, BK = 32, T = 64 * W, RW = BM / W, MI = RW / 16;  // rows / 16-row blocks per wave
+  // W waves as (W / WN) row groups x WN column groups: RW rows (MI 16-row
+  // blocks) x NB0 column blocks per wave (the last column group NBL)
+  static constexpr int BM = 128, BK = 32, T = 64 * W, WM = W / WN, RW = BM / WM, MI = RW / 16;
+  static constexpr int NB0 = (NBH + WN - 1) / WN, NBL = NBH - (WN - 1) * NB0;
   static constexpr int odd32(int bytes) { return (((bytes + 31) / 32) | 1) * 32; }
   static constexpr int RA = odd32(BM * 2), RB = odd32(NH * 2);  // k-row pitch (bytes)
   static constexpr int PA = BK * RA, PB = BK * RB;               // plane bytes
@@ -1321,12 +1324,12 @@ struct Wg3 {
   static constexpr int QX = N1 / 4, QH0 = (NH - N1) / 4, QH1 = (NT - NH) / 4;
   static constexpr int VX = (BK * QX + T - 1) / T, V0 = VX + (BK * QH0 + T - 1) / T, V1 = (BK * QH1 + T - 1) / T;
   static constexpr int AV = BK * BM / 4 / T, BV = V0 > V1 ? V0 : V1, NV = AV + BV;
-  static constexpr int SP = NH + 4;  // epilogue staging pitch (floats)
+  static constexpr int SP = 16 * NB0 + 4;  // epilogue staging pitch (floats)
   static constexpr int DUMMY = 2 * STG;                       // 64 lanes x 8 B of discarded stores
   static constexpr size_t LDS = 2 * (size_t)STG + 512;
   static_assert(N1 % 4 == 0 && N2 % 4 == 0 && (BK * BM / 4) % T == 0 && RW % 16 == 0 && N1 <= NH, "staging");
   static_assert(STG % 16 == 0 && LDS <= 160 * 1024 && (size_t)W * 16 * SP * 4 <= LDS, "LDS");
-  static_assert(NV <= NBH, "one f4 split per MFMA block");
+  static_assert(NV <= NBL && W % WN == 0, "one f4 split per MFMA block");
 };
 
 typedef short s4v __attribute__((ext_vector_type(4)));
@@ -1347,11 +1350,13 @@ DEV void split4(const f4& x, u2v& h, u2v& m, u2v& l) {
 }
 
 // DIAG (timing probes only, wrong results; ABCD_WG3DIAG): 1 = no splits or
-// plane stores in the loop, 2 = no MFMAs, 3 = the loads alone, 4 = no loads
-template <int N1, int N2, int W, int DIAG = 0>
+// plane stores in the loop, 2 = no MFMAs (3 = the loads alone, 4 = no loads:
+// not instantiated)
+template <int N1, int N2, int W, int WN, int DIAG = 0>
 __global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
-  using G = Wg3<N1, N2, W>;
-  constexpr int NT = G::NT, NBH = G::NBH, NH = G::NH, BM = G::BM, BK = G::BK, T = G::T, RW = G::RW, MI = G::MI;
+  using G = Wg3<N1, N2, W, WN>;
+  constexpr int NT = G::NT, NH = G::NH, BM = G::BM, BK = G::BK, T = G::T, RW = G::RW, MI = G::MI;
+  constexpr int NB0 = G::NB0, NBL = G::NBL, WM = G::WM;
   constexpr int RA = G::RA, RB = G::RB, PA = G::PA, PB = G::PB, OB = G::OB, STG = G::STG;
   constexpr int AV = G::AV, NV = G::NV, QX = G::QX, QH0 = G::QH0, QH1 = G::QH1, VX = G::VX;
   extern __shared__ __attribute__((aligned(16))) float wsm[];
@@ -1433,15 +1438,19 @@ __global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
     *reinterpret_cast<u2v*>(base + 2 * pp) = l;
   };
   // lane's transposed-read offset: group q reads k-rows 4q + (r >> 2), columns 4 (r & 3) .. + 3
-  const int offA = (4 * q + (r >> 2)) * RA + 8 * (r & 3) + 2 * (RW * w);
-  const int offB = OB + (4 * q + (r >> 2)) * RB + 8 * (r & 3);
+  // waves w and w + 4 share a SIMD: one of each column group (wave-uniform:
+  // the column-block guard below must be a scalar branch)
+  const int wu = __builtin_amdgcn_readfirstlane(w), wm = wu % WM, wn = wu / WM;
+  const int nb = wn == WN - 1 ? NBL : NB0;  // this wave's column blocks (wave-uniform)
+  const int offA = (4 * q + (r >> 2)) * RA + 8 * (r & 3) + 2 * (RW * wm);
+  const int offB = OB + (4 * q + (r >> 2)) * RB + 8 * (r & 3) + 2 * 16 * NB0 * wn;
   typedef __attribute__((address_space(3))) s4v lds_s4;
   auto trf = [&](int off, int pitch) -> bf8 {  // k-rows at off and 16 further
     const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off));
     const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off + 16 * pitch));
     return __builtin_bit_cast(bf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
-  f4 acc[MI][NBH];
+  f4 acc[MI][NB0];
   acc_zero(acc);
   constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
   // the pad columns NT - n0 .. NH of both stages' B planes read as 0 (never stored)
@@ -1474,20 +1483,23 @@ __global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
     bload(0, bp);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < NBH; ++j) {
+    for (int j = 0; j < NB0; ++j) {
       bf8 bq[3];
-      if (j + 1 < NBH) bload(j + 1, bq);
+      if (j + 1 < NB0) bload(j + 1, bq);  // (past nb: in-range LDS, never multiplied)
+      if (NB0 == NBL || j < nb) {
 #pragma unroll
-      for (int t = 0; t < 6; ++t)
+        for (int t = 0; t < 6; ++t)
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
-          if (DIAG == 3) {
-          } else if (DIAG != 2) acc[i][j] = mfma_bf(ap[i][TA[t]], bp[TB[t]], acc[i][j]);
-          else acc[i][j][0] += (float)ap[i][TA[t]][0] * (float)bp[TB[t]][1];
+          for (int i = 0; i < MI; ++i)
+            if (DIAG == 3) {
+            } else if (DIAG != 2) acc[i][j] = mfma_bf(ap[i][TA[t]], bp[TB[t]], acc[i][j]);
+            else acc[i][j][0] += (float)ap[i][TA[t]][0] * (float)bp[TB[t]][1];
+      }
       // the next chunk's f4s split and stored into the other stage in the
-      // MFMA gaps of the later blocks
-      constexpr int J0 = NBH - NV;
-      if (j >= J0) {
+      // MFMA gaps of the later blocks (blocks every wave has)
+      constexpr int J0 = NBL - NV;
+      const bool sj = j >= J0 && j - J0 < NV;  // (compile time: block j splits f4 j - J0)
+      if (sj) {
         if (DIAG != 1 && DIAG != 3) sstore(cur ^ 1, j - J0, rw[j - J0]);
         else acc[0][j][1] += rw[j - J0][0];
         if (DIAG != 4) rw[j - J0] = gload1(k0 + 3 * BK, j - J0);
@@ -1495,18 +1507,18 @@ __global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
       // order: the next block's 6 transposed reads first (12 MFMAs before
       // their use), then each MFMA followed by two of the split's VALU, the
       // plane stores and the reload last
-      if (j + 1 < NBH) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+      if (j + 1 < NB0) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
       for (int k = 0; k < 6 * MI; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (j >= J0) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        if (sj) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
       }
-      if (j >= J0) {
+      if (sj) {
         __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (j + 1 < NBH) bp[0] = bq[0], bp[1] = bq[1], bp[2] = bq[2];
+      if (j + 1 < NB0) bp[0] = bq[0], bp[1] = bq[1], bp[2] = bq[2];
     }
     __syncthreads();
   };
@@ -1529,16 +1541,16 @@ __global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
 #pragma unroll
-    for (int j = 0; j < NBH; ++j)
+    for (int j = 0; j < NB0; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int p = 0; p < NBH; ++p) {  // 16 rows x 4 NBH quads = 64 NBH lanes' worth
-      const int e = lane + 64 * p, lr = e / (4 * NBH), c4 = e % (4 * NBH);
-      const int gcol = n0 + 4 * c4, grow = m0 + RW * w + 16 * i + lr;
-      if (grow < M && gcol < NT)
+    for (int p = 0; p < NB0; ++p) {  // 16 rows x 4 NB0 quads = 64 NB0 lanes' worth
+      const int e = lane + 64 * p, lr = e / (4 * NB0), c4 = e % (4 * NB0);
+      const int lcol = 16 * NB0 * wn + 4 * c4, gcol = n0 + lcol, grow = m0 + RW * wm + 16 * i + lr;
+      if (grow < M && lcol < NH && gcol < NT)
         *reinterpret_cast<f4*>(out + (size_t)grow * NT + gcol) = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1546,27 +1558,25 @@ __global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
   }
 }
 
-template <int N1, int N2, int W, int DIAG>
+template <int N1, int N2, int W, int WN, int DIAG>
 static int wg3_go1(hipStream_t s, const WgArgs& a, dim3 grid) {
-  constexpr size_t lds = Wg3<N1, N2, W>::LDS;
+  constexpr size_t lds = Wg3<N1, N2, W, WN>::LDS;
   static bool attr = false;
   if (!attr) {
-    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg3_kernel<N1, N2, W, DIAG>,
+    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg3_kernel<N1, N2, W, WN, DIAG>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  gemm_wg3_kernel<N1, N2, W, DIAG><<<grid, 64 * W, lds, s>>>(a);
+  gemm_wg3_kernel<N1, N2, W, WN, DIAG><<<grid, 64 * W, lds, s>>>(a);
   return 0;
 }
 
-template <int N1, int N2, int W>
+template <int N1, int N2, int W, int WN>
 static int wg3_go(hipStream_t s, const WgArgs& a, dim3 grid, int diag) {
   switch (diag) {
-    case 1: return wg3_go1<N1, N2, W, 1>(s, a, grid);
-    case 2: return wg3_go1<N1, N2, W, 2>(s, a, grid);
-    case 3: return wg3_go1<N1, N2, W, 3>(s, a, grid);
-    case 4: return wg3_go1<N1, N2, W, 4>(s, a, grid);
-    default: return wg3_go1<N1, N2, W, 0>(s, a, grid);
+    case 1: return wg3_go1<N1, N2, W, WN, 1>(s, a, grid);
+    case 2: return wg3_go1<N1, N2, W, WN, 2>(s, a, grid);
+    default: return wg3_go1<N1, N2, W, WN, 0>(s, a, grid);
   }
 }
 
@@ -1605,9 +1615,14 @@ static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int
     // waves; ABCD_WG3DIAG: the timing probes (wrong results)
     const char* dg = getenv("ABCD_WG3DIAG");
     const char* wv = getenv("ABCD_WG3W");
-    const int diag = dg ? atoi(dg) : 0, waves = wv && wv[0] == '4' ? 4 : 8;
-    ABCD_TRY((hipError_t)(waves == 8 ? wg3_go<N1, N2, 8>(s, a, dim3(2 * mt, 1, nd * Z), diag)
-                                     : wg3_go<N1, N2, 4>(s, a, dim3(2 * mt, 1, nd * Z), diag)));
+    const int diag = dg ? atoi(dg) : 0;
+    const dim3 gr(2 * mt, 1, nd * Z);
+    // ABCD_WG3W: 8x1 (8 waves of 16 rows x 13 column blocks), 4x2 (the default:
+    // 8 waves of 32 rows x 7 / 6 blocks, half the transposed B reads), 4 (4 x 1)
+    const int form = !wv ? 1 : wv[0] == '8' ? 0 : wv[0] == '4' && wv[1] == 0 ? 2 : 1;
+    ABCD_TRY((hipError_t)(form == 0   ? wg3_go<N1, N2, 8, 1>(s, a, gr, diag)
+                          : form == 1 ? wg3_go<N1, N2, 8, 2>(s, a, gr, diag)
+                                      : wg3_go<N1, N2, 4, 1>(s, a, gr, diag)));
   }
   ABCD_CHECK_LAUNCH();
   const long nq = (long)nd * M * G::NT / 4;
