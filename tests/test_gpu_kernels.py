@@ -30,7 +30,7 @@ def test_gemm_nt_vs_torch(M, N, K):
     assert err <= 1e-5 * K ** 0.5 * 4 + 1e-5, err
 
 
-@pytest.mark.parametrize("wg", ["3", "2"])
+@pytest.mark.parametrize("wg", ["3", "2", "3w8"])
 @pytest.mark.parametrize("nd,F,H,K", [(2, 129, 256, 65583), (1, 129, 256, 3001), (2, 130, 256, 777), (2, 33, 48, 500),
                                        (1, 20, 24, 64), (2, 129, 256, 31), (1, 143, 256, 100003)])
 def test_lstm_wgrad_vs_torch(nd, F, H, K, wg, monkeypatch):
@@ -39,7 +39,11 @@ def test_lstm_wgrad_vs_torch(nd, F, H, K, wg, monkeypatch):
     (ABCD_WG3=0) at F <= 143, H = 256 (the c2 shape first, both directions;
     a K below one chunk; the widest F with a K range that is not a multiple
     of 32), the split-GEMM route elsewhere -- against float64 torch."""
-    monkeypatch.setenv("ABCD_WG3", "1" if wg == "3" else "0")
+    # "3": gemm_wg3 in its default 4 x 2 wave form; "3w8": its 8 x 1 form
+    monkeypatch.setenv("ABCD_WG3", "0" if wg == "2" else "1")
+    if wg == "3w8":
+        monkeypatch.setenv("ABCD_WG3W", "8")
+    wg = wg[0]
     import ctypes
     from modules import _native as Nn
     g = torch.Generator(device="cuda").manual_seed(nd * 7 + F + H + K)
