@@ -19,7 +19,7 @@ import sys
 from collections import defaultdict
 
 # role -> the persistent kernels that implement it (bench.py reports by role)
-ROLES = {"enc_fwd": ("enc_fwd_persist", "enc_fwd_w8"), "enc_bwd": ("enc_bwd_persist", "enc_bwd_sk", "enc_bwd_w8"),
+ROLES = {"enc_fwd": ("enc_fwd_persist",), "enc_bwd": ("enc_bwd_persist", "enc_bwd_sk", "enc_bwd_w8"),
          "dec_fwd": ("dec_fwd_persist", "dec_fwd_x6"), "dec_bwd": ("dec_bwd_persist", "dec_bwd_sk", "dec_bwd_fold", "dec_bwd_w16")}
 KERNELS = tuple(ROLES)
 

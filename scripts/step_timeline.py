@@ -6,7 +6,7 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "enc_fwd_persist" in r["Kernel_Name"] or "enc_fwd_w8" in r["Kernel_Name"]]
+idx = [i for i, r in enumerate(rows) if "enc_fwd_persist" in r["Kernel_Name"]]
 s, e = idx[-3], idx[-2]
 t0 = int(rows[s]["Start_Timestamp"])
 for r in rows[s - 3:e]:

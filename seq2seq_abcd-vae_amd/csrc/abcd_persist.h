@@ -27,7 +27,6 @@ struct PFwdDir {
 struct PFwdArgs {
   PFwdDir d[2];
   int H, nd, T, nrt;
-  int B;             // rows of the first step (enc_fwd_w8 counts its 32-row groups from it)
   const int* off;    // device: off[0..T]
   unsigned* sync;    // one 128-B counter line per group, zeroed before the launch
   unsigned long long* prof;  // diagnostics: per-step s_memtime stamps, or null

@@ -406,214 +406,6 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// enc_fwd_w8 (round 4): the LSTM encoder forward in 32-row groups of 8
-// members (32 units each), as enc_bwd_w8 does for the BPTT.  A member of
-// enc_fwd_persist (64 rows x 16 units) gathers all 64 h rows of its group
-// every step and each wave splits its own 16 rows (64 KiB per member, 1 MiB
-// per group and step over 16 members); here a member gathers its 32 rows ONCE
-// (32 KiB: 8 sc1 f4 loads per thread), splits them into x6 fragment planes in
-// LDS and all 4 waves read them: half the gather volume chip-wide, a quarter
-// of the splits.  Wave w owns units u0 + 8w .. +7 for both 16-row blocks;
-// its two 16-column tiles are [i | f] and [g | o] of those 8 units (the cell
-// pairs lanes r and r ^ 8 by a shuffle, as dec_fwd_x6); the first NCR chunks
-// of its W_hh image stay in registers, the rest in LDS.  H = 256 only.
-// Reference: nn.LSTM's recurrence, model.py:53,60-66.
-// ---------------------------------------------------------------------------
-constexpr int F8_ROWS = 32, F8_M = 8, F8_TPP = 12;  // rows, members per group, transpose pitch (floats)
-// lanes r < 8 hold v[rb][g] for row 16 rb + 4q + g, column r of a wave's
-// 32 x 8 tile; returns lane l's row quad: row l >> 1, columns 4 (l & 1) .. + 3
-DEV f4 tp8(float* tb, const float (&v)[2][4], int lane) {
-  const int r = lane & 15, q = lane >> 4;
-  __builtin_amdgcn_wave_barrier();  // the previous quad reads of this buffer are issued
-  if (r < 8) {
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) tb[(16 * rb + 4 * q + g) * F8_TPP + r] = v[rb][g];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  return *reinterpret_cast<const f4*>(tb + (lane >> 1) * F8_TPP + 4 * (lane & 1));
-}
-template <int NCR>
-__global__ __launch_bounds__(256) void enc_fwd_w8(PFwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) f4 smem[];
-  constexpr int H = 256, M = F8_M, NC = H / 32, NCL = NC - NCR;
-  const int T = a.T, ng = a.nd * a.nrt;  // a.nrt: 32-row tiles per direction (the launcher's count)
-  const Role role = assign_role(ng, M);
-  const int grp = role.grp, mem = role.mem;
-  const int dir = grp / a.nrt, rt = grp % a.nrt;
-  const PFwdDir& D = a.d[dir];
-  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int uo = mem * 32 + 8 * w;  // the wave's 8 units
-  const bool lo = r < 8;
-  const int unit = uo + (r & 7);
-  const int rowg = rt * F8_ROWS;
-  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
-  // LDS: W_hh image chunks NCR.. [wave][tile][NCL][3][64] | h planes [2 rb][NC][3][64] | wave transposes
-  f4* BL = smem;
-  f4* AP = BL + 4 * 2 * (NCL > 0 ? NCL : 1) * 3 * 64;
-  float* tb = reinterpret_cast<float*>(AP + 2 * NC * 3 * 64) + w * F8_ROWS * F8_TPP;
-  // image of tile p, chunk c, lane (r, q): column r = gate 2p + (r >> 3) of unit uo + (r & 7), k = 32c + 8q + 0..7
-  bf8 Br[2][NCR][3];
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const float* src = D.Whh + (long)((2 * p + (r >> 3)) * H + unit) * H + 32 * c + 8 * q;
-      bf8 h, m, l;
-      split8(*reinterpret_cast<const f4*>(src), *reinterpret_cast<const f4*>(src + 4), h, m, l);
-      if (c < NCR) {
-        Br[p][c < NCR ? c : 0][0] = h, Br[p][c < NCR ? c : 0][1] = m, Br[p][c < NCR ? c : 0][2] = l;
-      } else {
-        f4* d = BL + (((w * 2 + p) * NCL + (c - NCR)) * 3) * 64 + lane;
-        d[0] = __builtin_bit_cast(f4, h);
-        d[64] = __builtin_bit_cast(f4, m);
-        d[128] = __builtin_bit_cast(f4, l);
-      }
-    }
-  __syncthreads();
-  float st[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // c of the lane's cells
-  const int* off = a.off;
-  for (int i = 0; i < T; ++i) {
-    const int t = D.rev ? T - 1 - i : i;
-    const int o = off[t], bs = off[t + 1] - o;
-    int prev_valid, next_off, next_bs;
-    if (D.rev) {
-      prev_valid = t == T - 1 ? 0 : off[t + 2] - off[t + 1];
-      next_off = t >= 1 ? off[t - 1] : 0;
-      next_bs = t >= 1 ? bs : 0;
-    } else {
-      prev_valid = t == 0 ? 0 : bs;
-      next_off = off[t + 1];
-      next_bs = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
-    }
-    PSTAMP(0);
-    // input projection of this lane's accumulator elements (gate 2p + (r >> 3)
-    // of its unit), loaded before the wait
-    float gxp[2][2][4];
-    {
-      const __amdgpu_buffer_rsrc_t rgx = make_rsrc(D.GX + (size_t)o * D.ldgx, (uint32_t)bs * D.ldgx * 4u);
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            gxp[rb][p][g] = bld(rgx, ((uint32_t)(rowg + 16 * rb + 4 * q + g) * D.ldgx + (2 * p + (r >> 3)) * H + unit) * 4u);
-    }
-    if (i > 0) group_wait(cnt, (unsigned)(M * i));
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb) pin(gxp[rb][0]), pin(gxp[rb][1]);
-    PSTAMP(1);
-    f4 acc[2][2];
-    acc2_zero(acc);
-    if (rowg < prev_valid) {  // (uniform) the group's h rows, gathered once and split into planes
-      const __amdgpu_buffer_rsrc_t rh = make_rsrc(D.Hprev + (size_t)o * H, (uint32_t)prev_valid * H * 4u);
-      f4 xl[4], xh[4];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int it = threadIdx.x + 256 * v, rb = it >> 9, c = (it >> 6) & 7, ln = it & 63;
-        const uint32_t ob = (uint32_t)((rowg + 16 * rb + (ln & 15)) * H + 32 * c + 8 * (ln >> 4)) * 4u;
-        xl[v] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rh, ob, 0, 16));
-        xh[v] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rh, ob + 16u, 0, 16));
-      }
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int it = threadIdx.x + 256 * v, rb = it >> 9, c = (it >> 6) & 7, ln = it & 63;
-        bf8 h, m, l;
-        split8(xl[v], xh[v], h, m, l);
-        f4* d = AP + ((rb * NC + c) * 3) * 64 + ln;
-        d[0] = __builtin_bit_cast(f4, h);
-        d[64] = __builtin_bit_cast(f4, m);
-        d[128] = __builtin_bit_cast(f4, l);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        bf8 av[2][3];
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl) av[rb][pl] = __builtin_bit_cast(bf8, AP[((rb * NC + c) * 3 + pl) * 64 + lane]);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          bf8 bv[3];
-          if (c < NCR) {
-            bv[0] = Br[p][c < NCR ? c : 0][0], bv[1] = Br[p][c < NCR ? c : 0][1], bv[2] = Br[p][c < NCR ? c : 0][2];
-          } else {
-            const f4* bp = BL + (((w * 2 + p) * NCL + (c - NCR)) * 3) * 64 + lane;
-            bv[0] = __builtin_bit_cast(bf8, bp[0]), bv[1] = __builtin_bit_cast(bf8, bp[64]);
-            bv[2] = __builtin_bit_cast(bf8, bp[128]);
-          }
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb)
-            acc[rb][p] = mma_x6(acc[rb][p], av[rb][0], av[rb][1], av[rb][2], bv[0], bv[1], bv[2]);
-        }
-      }
-    }
-    PSTAMP(2);
-    // cell: lanes r and r ^ 8 hold [i | f] (tile 0) and [g | o] (tile 1) of unit uo + (r & 7)
-    float hv[2][4], cv[2][4], gv[4][2][4];
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float v0 = acc[rb][0][g] + gxp[rb][0][g], v1 = acc[rb][1][g] + gxp[rb][1][g];
-        const float w0 = __shfl_xor(v0, 8, 64), w1 = __shfl_xor(v1, 8, 64);
-        const float i_ = fsigmoid(lo ? v0 : w0), f_ = fsigmoid(lo ? w0 : v0);
-        const float g_ = ftanh(lo ? v1 : w1), o_ = fsigmoid(lo ? w1 : v1);
-        const bool haspred = rowg + 16 * rb + 4 * q + g < prev_valid;
-        cv[rb][g] = f_ * (haspred ? st[rb][g] : 0.f) + i_ * g_;
-        hv[rb][g] = o_ * ftanh(cv[rb][g]);
-        st[rb][g] = cv[rb][g];
-        gv[0][rb][g] = i_, gv[1][rb][g] = f_, gv[2][rb][g] = g_, gv[3][rb][g] = o_;
-      }
-    // h -> the next step's operand rows (write-through, one 16-B store per lane)
-    const uint32_t qh = (uint32_t)((rowg + (lane >> 1)) * H + uo + 4 * (lane & 1)) * 4u;
-    {
-      const f4 hq = tp8(tb, hv, lane);
-      if (rowg < next_bs) st4(make_rsrc(D.Hprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qh, hq, true);
-    }
-    PSTAMP(3);
-    group_publish(cnt);
-    // stashes for the backward pass and the outputs (plain 16-B stores)
-    if (rowg < bs) {
-      const __amdgpu_buffer_rsrc_t rg = make_rsrc(D.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
-      const uint32_t go = (uint32_t)((rowg + (lane >> 1)) * 4 * H + uo + 4 * (lane & 1)) * 4u;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st4(rg, go + (uint32_t)(j * H) * 4u, tp8(tb, gv[j], lane), false);
-      const f4 cq = tp8(tb, cv, lane);
-      st4(make_rsrc(D.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qh, cq, false);
-      if (D.Y)
-        st4(make_rsrc(D.Y + (size_t)o * D.ldy, (uint32_t)bs * D.ldy * 4u),
-            (uint32_t)((rowg + (lane >> 1)) * D.ldy + uo + 4 * (lane & 1)) * 4u, tp8(tb, hv, lane), false);
-      if (rowg < next_bs) st4(make_rsrc(D.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qh, cq, false);
-    }
-    if (lo) {  // rows without a predecessor / whose sequence ends here (rare)
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int b = rowg + 16 * rb + 4 * q + g;
-          if (b >= bs) continue;
-          const long rr = o + b;
-          if (b >= prev_valid) {
-            D.Cprev[rr * H + unit] = 0.f;
-            D.Hprev[rr * H + unit] = 0.f;
-          }
-          if (b >= next_bs && D.out) {
-            D.out[(long)b * D.ldo + D.hcol + unit] = hv[rb][g];
-            D.out[(long)b * D.ldo + D.ccol + unit] = cv[rb][g];
-          }
-        }
-    }
-    PSTAMP(4);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // encoder backward (BPTT): one launch per layer, both directions
 // ---------------------------------------------------------------------------
 // X6 > 0: split-fp32 recurrent MMA over X6 = G * H / 32 chunks (abcd_x6.h)
@@ -3253,34 +3045,6 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   return 0;
 }
 
-// enc_fwd_w8 for the LSTM at H = 256 by default; ABCD_ENCFWD=p: enc_fwd_persist (A/B timing)
-static bool enc_fwd_w8_on() {
-  const char* v = getenv("ABCD_ENCFWD");
-  return !(v && v[0] == 'p');
-}
-static int launch_fwd_w8(hipStream_t s, const PFwdArgs& a, bool* launched) {
-  constexpr int NCR = 4;
-  if (a.B <= 0) return 0;
-  const int nrt = cdiv(a.B, F8_ROWS);
-  const int grid = a.nd * nrt * F8_M;
-  const size_t lds = (size_t)4 * 2 * (8 - NCR) * 3 * 64 * 16 + (size_t)2 * 8 * 3 * 64 * 16 + (size_t)4 * F8_ROWS * F8_TPP * 4;
-  bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(enc_fwd_w8<NCR>, grid, lds, &ok));
-  if (!ok) return 0;
-  ABCD_TRY(zero_sync(s, a.sync, a.nd * nrt));
-  PFwdArgs b = a;
-  b.nrt = nrt;
-  b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
-  {
-    TimedScope ts(s, TK_ENC_FWD);
-    enc_fwd_w8<NCR><<<grid, 256, lds, s>>>(b);
-  }
-  note_dispatch(TK_ENC_FWD, "enc_fwd_w8<%d> grid %d", NCR, grid);
-  ABCD_CHECK_LAUNCH();
-  *launched = true;
-  return 0;
-}
-
 template <int G>
 static int launch_fwd_x6(hipStream_t s, const PFwdArgs& a, bool* launched) {
   if (a.H == 64) return launch_fwd<G, 16, 2>(s, a, launched);
@@ -3291,10 +3055,6 @@ static int launch_fwd_x6(hipStream_t s, const PFwdArgs& a, bool* launched) {
 int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled()) return 0;
-  if (G == 4 && a.H == 256 && enc_fwd_w8_on()) {
-    ABCD_TRY((hipError_t)launch_fwd_w8(s, a, launched));
-    if (*launched) return 0;
-  }
   if (x6_enabled(a.H)) return G == 4 ? launch_fwd_x6<4>(s, a, launched) : launch_fwd_x6<3>(s, a, launched);
   const int pd = ring_depth(a.H / 16);
   if (G == 4) {

@@ -426,7 +426,6 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
     {
       PFwdArgs pa{};
       pa.H = H; pa.nd = D; pa.T = T; pa.nrt = cdiv(x->B, PERSIST_ROWS); pa.off = w.off; pa.sync = w.sync;
-      pa.B = x->B;
       for (int d = 0; d < D; ++d) {
         const abcd_rnn_w& W = p->w[l][d];
         PFwdDir& f = pa.d[d];

@@ -40,7 +40,7 @@ LOSS_TOL = 1e-4
 GRAD_TOL = 1e-3
 
 KERNELS = {
-    "LSTM": ("enc_fwd_w8<4>", "enc_bwd_w8<4>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
+    "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_w8<4>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
     "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_w8<3>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_w16<9,GRU>"),
 }
 # A/B runs of the earlier decoder BPTT forms (64-row groups of 32 members)
@@ -50,9 +50,6 @@ if _DB.startswith("s"):
     KERNELS = {r: k[:3] + (f"dec_bwd_sk<9,16,16,{r}>",) for r, k in KERNELS.items()}
 elif _DB.startswith("f"):
     KERNELS = {r: k[:3] + (f"dec_bwd_fold<9,16,{r}>",) for r, k in KERNELS.items()}
-F8 = not os.environ.get("ABCD_ENCFWD", "").startswith("p")  # the 32-row / 8-member LSTM encoder forward (default)
-if not F8:
-    KERNELS["LSTM"] = ("enc_fwd_persist<4,16,8>",) + KERNELS["LSTM"][1:]
 W8 = not os.environ.get("ABCD_ENCBWD", "").startswith("s")  # the 32-row / 8-member encoder BPTT (default)
 if not W8:
     KERNELS = {r: (k[0], f"enc_bwd_sk<{4 if r == 'LSTM' else 3},16>") + k[2:] for r, k in KERNELS.items()}
@@ -102,7 +99,7 @@ def test_full_shape_step_vs_oracle(name, B, seed):
     assert N.lib().abcd_device_status() == 0
     ran = N.dispatch()
     tiles = (B + 63) // 64
-    grids = {"enc_fwd": (B + 31) // 32 * 2 * 8 if (F8 and cfg["rnn"] == "LSTM") else tiles * 2 * 16, "enc_bwd": (B + 31) // 32 * 2 * 8 if W8 else tiles * 2 * 16,
+    grids = {"enc_fwd": tiles * 2 * 16, "enc_bwd": (B + 31) // 32 * 2 * 8 if W8 else tiles * 2 * 16,
              "dec_fwd": tiles * 32,
              "dec_bwd": (B + 31) // 32 * 16 if W16 else tiles * 32}
     for role, kern in zip(("enc_fwd", "enc_bwd", "dec_fwd", "dec_bwd"), KERNELS[cfg["rnn"]]):

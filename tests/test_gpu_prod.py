@@ -28,7 +28,7 @@ GRAD_TOL = 1e-3
 
 # the kernels bench.py's configs dispatch at H = Hm = 256, F = 129 (Fp = 144)
 EXPECT = {
-    "LSTM": {"enc_fwd": "enc_fwd_w8<4>", "enc_bwd": "enc_bwd_w8<4>",
+    "LSTM": {"enc_fwd": "enc_fwd_persist<4,16,8>", "enc_bwd": "enc_bwd_w8<4>",
              "dec_fwd": "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd": "dec_bwd_w16<9,LSTM>"},
     "GRU": {"enc_fwd": "enc_fwd_persist<3,16,8>", "enc_bwd": "enc_bwd_w8<3>",
             "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_w16<9,GRU>"},
@@ -40,8 +40,6 @@ for _r in EXPECT:
     elif _DB.startswith("f"):
         EXPECT[_r]["dec_bwd"] = f"dec_bwd_fold<9,16,{_r}>"
 W16 = not _DB.startswith(("f", "s"))  # the 32-row / 16-member decoder BPTT (default)
-if os.environ.get("ABCD_ENCFWD", "").startswith("p"):  # A/B runs of the 64-row / 16-member encoder forward
-    EXPECT["LSTM"]["enc_fwd"] = "enc_fwd_persist<4,16,8>"
 if os.environ.get("ABCD_ENCBWD", "").startswith("s"):  # A/B runs of the 64-row / 16-member encoder BPTT
     for _r in EXPECT:
         EXPECT[_r]["enc_bwd"] = f"enc_bwd_sk<{4 if _r == 'LSTM' else 3},16>"
