@@ -14,8 +14,6 @@ synchronises with the host; loss terms and diagnostics stay on the device in
 """
 import itertools
 
-import os
-
 import torch
 
 from . import _native as N
@@ -227,8 +225,7 @@ class FusedStep:
         d_h = torch.empty(B, self.E, device=dev)
         N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
                                                float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
-                                               self.samp_g, N.ptr(ws_s), ws_s.numel(), st,
-                                               N.c_void_p(side.cuda_stream) if _SAMP_SIDE else None),
+                                               self.samp_g, N.ptr(ws_s), ws_s.numel(), st, None),
                 "sampler backward")  # one stream: its parameter GEMMs beside enc_bwd only slow the BPTT (DESIGN s3)
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
                                                  self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
@@ -316,10 +313,6 @@ def check_status(records, where="training step"):
     bad = r.nonzero()
     if bad.numel():
         N.raise_on_status(float(r[bad[0, 0]]), f"{where} {int(bad[0, 0]) + 1}")
-
-
-# ABCD_SAMPSIDE=1 (A/B timing): the sampler's parameter-gradient GEMMs on the side stream
-_SAMP_SIDE = os.environ.get("ABCD_SAMPSIDE") == "1"
 
 
 class StatusWatch:
