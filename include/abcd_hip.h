@@ -377,6 +377,15 @@ int abcd_timing_read_kernel(int kid, double* out);
 const char* abcd_dispatch_name(int kid);
 long abcd_dispatch_count(int kid);
 void abcd_dispatch_reset(void);
+/* diagnostics (scripts/, not part of the reference's interface):
+ * abcd_debug_persist_prof -- the persistent kernels of the roles in `mask`
+ * (1 enc fwd, 2 enc bwd, 4 dec fwd, 8 dec bwd) stamp s_memrealtime at their
+ * phase boundaries into dev_buf (blocks x T x 8 u64; null: off);
+ * abcd_debug_xcc_map -- launches `blocks` one-per-CU workgroups that record
+ * their XCC id into dev_out[block] (the placement the persistent kernels'
+ * group roles rely on).  Returns 0 / a HIP error. */
+void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask);
+int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream);
 /* 0 if no persistent recurrent kernel has timed out waiting for its group
  * since the last call (a timeout means the grid was not co-resident; the
  * results of that launch are invalid).  Reads and clears the device word;
