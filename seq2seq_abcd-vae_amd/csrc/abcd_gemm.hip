@@ -1558,6 +1558,207 @@ __global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
   }
 }
 
+// gemm_wg3b: gemm_wg3 with 256-row tiles (half the B-operand bytes per MFMA:
+// the wg3 loop is bound by its operand traffic).  Two A stages (52 KiB each)
+// but ONE B stage (39 KiB): the next chunk's B columns are split and stored
+// between two barriers at the end of each chunk; the A rows as in wg3, inside
+// the MFMA gaps.  8 waves as 4 row groups (64 rows) x 2 column groups (7 / 6
+// blocks).  (ABCD_WG3W=b, an experiment.)
+template <int N1, int N2>
+struct Wg3b {
+  static constexpr int NT = N1 + N2, NB = (NT + 15) / 16, NBH = (NB + 1) / 2, NH = 16 * NBH;
+  static constexpr int BM = 256, BK = 32, T = 512, WM = 4, RW = BM / WM, MI = RW / 16;
+  static constexpr int NB0 = (NBH + 1) / 2, NBL = NBH - NB0;
+  static constexpr int odd32(int bytes) { return (((bytes + 31) / 32) | 1) * 32; }
+  static constexpr int RA = odd32(BM * 2), RB = odd32(NH * 2);
+  static constexpr int PA = BK * RA, PB = BK * RB, SA = 3 * PA, OB = 2 * SA, DUMMY = OB + 3 * PB;
+  static constexpr int QX = N1 / 4, QH0 = (NH - N1) / 4, QH1 = (NT - NH) / 4;
+  static constexpr int VX = (BK * QX + T - 1) / T, V0 = VX + (BK * QH0 + T - 1) / T, V1 = (BK * QH1 + T - 1) / T;
+  static constexpr int AV = BK * BM / 4 / T, BV = V0 > V1 ? V0 : V1;
+  static constexpr int SP = 16 * NB0 + 4;
+  static constexpr size_t LDS = (size_t)DUMMY + 512;
+  static_assert(LDS <= 160 * 1024 && (size_t)8 * 16 * SP * 4 <= LDS && AV + 1 <= NBL, "wg3b layout");
+};
+
+template <int N1, int N2>
+__global__ __launch_bounds__(512, 1) void gemm_wg3b_kernel(WgArgs a) {
+  using G = Wg3b<N1, N2>;
+  constexpr int NT = G::NT, NH = G::NH, BM = G::BM, BK = G::BK, T = G::T, RW = G::RW, MI = G::MI, WM = G::WM;
+  constexpr int NB0 = G::NB0, NBL = G::NBL, RA = G::RA, RB = G::RB, PA = G::PA, PB = G::PB, SA = G::SA, OB = G::OB;
+  constexpr int AV = G::AV, BV = G::BV, QX = G::QX, QH0 = G::QH0, QH1 = G::QH1, VX = G::VX;
+  constexpr uint32_t OOB = 0x80000000u;
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  char* const lds = reinterpret_cast<char*>(wsm);
+  const dim3 bid = xcd_tile(true);
+  const int dz = bid.z, d = dz / a.Z, z = dz % a.Z;
+  const int half = bid.x & 1, m0 = (bid.x >> 1) * BM, M = a.M, n0 = half * NH;
+  const int kb = z * a.kps, ke = min(a.K, kb + a.kps);
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  const int wu = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wu % WM, wn = wu / WM;
+  const int nb = wn ? NBL : NB0;
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.A[d], (uint32_t)((size_t)ke * a.lda * 4));
+  const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.B1[d], (uint32_t)((size_t)ke * a.ldb1 * 4));
+  const __amdgpu_buffer_rsrc_t r2 = make_rsrc(a.B2[d], (uint32_t)((size_t)ke * a.ldb2 * 4));
+  auto ld4 = [](const __amdgpu_buffer_rsrc_t& rs, uint32_t o) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+  };
+  // A f4s: byte offset at k0 = 0 (OOB past M) and in plane 0 of an A stage
+  uint32_t goa[AV];
+  int loa[AV];
+#pragma unroll
+  for (int v = 0; v < AV; ++v) {
+    const int x = tid + T * v, k = x / (BM / 4), m = m0 + 4 * (x % (BM / 4));
+    goa[v] = m < M ? 4u * (uint32_t)(k * (int)a.lda + m) : OOB;
+    loa[v] = k * RA + 8 * (x % (BM / 4));
+  }
+  // B f4s (per v one uniform source, as gemm_wg3)
+  uint32_t gobv[BV], rowbv[BV];
+  int lob[BV];
+#pragma unroll
+  for (int u = 0; u < BV; ++u) {
+    int k, c, n;
+    bool in;
+    if (half == 0 && u < VX) {
+      const int x = tid + T * u;
+      in = x < BK * QX, k = x / QX, c = 4 * (x % QX), n = c;
+    } else if (half == 0) {
+      const int x = tid + T * (u - VX);
+      in = x < BK * QH0, k = x / QH0, c = N1 + 4 * (x % QH0), n = c - N1;
+    } else {
+      const int x = tid + T * u;
+      in = x < BK * QH1, k = x / QH1, c = 4 * (x % QH1), n = NH - N1 + c;
+    }
+    const bool x1 = half == 0 && u < VX;
+    const int ld = (int)(x1 ? a.ldb1 : a.ldb2);
+    rowbv[u] = 4u * (uint32_t)ld;
+    gobv[u] = in ? 4u * (uint32_t)(k * ld + n) : OOB;
+    lob[u] = in ? OB + k * RB + 2 * c : -1;
+  }
+  auto glA = [&](int k0, int v) { return ld4(rA, goa[v] + (uint32_t)k0 * 4u * (uint32_t)a.lda); };
+  auto glB = [&](int k0, int u) {
+    const bool x1 = half == 0 && u < VX;
+    return ld4(x1 ? r1 : r2, gobv[u] + (uint32_t)k0 * rowbv[u]);
+  };
+  auto stA = [&](int stage, int v, const f4& x) {
+    u2v h, m, l;
+    split4(x, h, m, l);
+    char* base = lds + stage * SA + loa[v];
+    *reinterpret_cast<u2v*>(base) = h;
+    *reinterpret_cast<u2v*>(base + PA) = m;
+    *reinterpret_cast<u2v*>(base + 2 * PA) = l;
+  };
+  auto stB = [&](int u, const f4& x) {
+    u2v h, m, l;
+    split4(x, h, m, l);
+    const bool ok = lob[u] >= 0;
+    char* base = lds + (ok ? lob[u] : G::DUMMY + 8 * lane);
+    const int pp = ok ? PB : 0;
+    *reinterpret_cast<u2v*>(base) = h;
+    *reinterpret_cast<u2v*>(base + pp) = m;
+    *reinterpret_cast<u2v*>(base + 2 * pp) = l;
+  };
+  const int offA = (4 * q + (r >> 2)) * RA + 8 * (r & 3) + 2 * (RW * wm);
+  const int offB = OB + (4 * q + (r >> 2)) * RB + 8 * (r & 3) + 2 * 16 * NB0 * wn;
+  typedef __attribute__((address_space(3))) s4v lds_s4;
+  auto trf = [&](int off, int pitch) -> bf8 {
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off + 16 * pitch));
+    return __builtin_bit_cast(bf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  f4 acc[MI][NB0];
+  acc_zero(acc);
+  constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
+  // the pad columns NT - n0 .. NH of the B planes read as 0 (never stored)
+  for (int e = tid; n0 + NH > NT && e < 3 * BK * (n0 + NH - NT); e += T) {
+    const int np = n0 + NH - NT, p = e / (BK * np), x = e % (BK * np);
+    *reinterpret_cast<short*>(lds + OB + p * PB + (x / np) * RB + 2 * (NT - n0 + x % np)) = 0;
+  }
+  f4 ra[AV], rb[BV];
+#pragma unroll
+  for (int v = 0; v < AV; ++v) stA(0, v, glA(kb, v));
+#pragma unroll
+  for (int u = 0; u < BV; ++u) stB(u, glB(kb, u));
+#pragma unroll
+  for (int v = 0; v < AV; ++v) ra[v] = glA(kb + BK, v);
+#pragma unroll
+  for (int u = 0; u < BV; ++u) rb[u] = glB(kb + BK, u);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const int sa = cur * SA;
+    bf8 ap[MI][3];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) ap[i][p] = trf(sa + p * PA + offA + 2 * 16 * i, RA);
+    auto bload = [&](int j, bf8 (&bp)[3]) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bp[p] = trf(p * PB + offB + 2 * 16 * j, RB);
+    };
+    bf8 bp[3];
+    bload(0, bp);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NB0; ++j) {
+      bf8 bq[3];
+      if (j + 1 < NB0) bload(j + 1, bq);
+      if (j < nb) {
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+          for (int i = 0; i < MI; ++i) acc[i][j] = mfma_bf(ap[i][TA[t]], bp[TB[t]], acc[i][j]);
+      }
+      constexpr int J0 = 1;  // A f4 j - J0 split into the other A stage in block j
+      const bool sj = j >= J0 && j - J0 < AV;
+      if (sj) {
+        stA(cur ^ 1, j - J0, ra[j - J0]);
+        ra[j - J0] = glA(k0 + 2 * BK, j - J0);
+      }
+      if (j + 1 < NB0) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+      for (int k = 0; k < 6 * MI; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (sj) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      }
+      if (sj) {
+        __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + 1 < NB0) bp[0] = bq[0], bp[1] = bq[1], bp[2] = bq[2];
+    }
+    __syncthreads();  // every wave is done with the B stage
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      stB(u, rb[u]);
+      rb[u] = glB(k0 + 2 * BK, u);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  constexpr int SP = G::SP;
+  float* stg = wsm + wu * 16 * SP;
+  float* const out = a.slab + (size_t)dz * M * NT;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int j = 0; j < NB0; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < NB0; ++p) {
+      const int e = lane + 64 * p, lr = e / (4 * NB0), c4 = e % (4 * NB0);
+      const int lcol = 16 * NB0 * wn + 4 * c4, gcol = n0 + lcol, grow = m0 + RW * wm + 16 * i + lr;
+      if (grow < M && lcol < NH && gcol < NT)
+        *reinterpret_cast<f4*>(out + (size_t)grow * NT + gcol) = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <int N1, int N2, int W, int WN, int DIAG>
 static int wg3_go1(hipStream_t s, const WgArgs& a, dim3 grid) {
   constexpr size_t lds = Wg3<N1, N2, W, WN>::LDS;
@@ -1587,7 +1788,10 @@ static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int
   static_assert(Wg3<N1, N2>::BM == G::BM && Wg3<N1, N2>::NT == G::NT, "same slab geometry");
   const int mt = cdiv(M, G::BM);
   // one workgroup per CU: about 256 / (nd x mt) K ranges, the grid a multiple of 8
-  const int tw = W3 ? 2 * mt : mt;  // workgroups per (direction, K range)
+  const char* wv0 = getenv("ABCD_WG3W");
+  const bool w3b = W3 && wv0 && wv0[0] == 'b';  // gemm_wg3b: 256-row tiles
+  const int mtb = w3b ? cdiv(M, 256) : mt;
+  const int tw = W3 ? 2 * mtb : mt;  // workgroups per (direction, K range)
   int Z = std::max(1, 256 / (nd * tw));
   while ((nd * tw * Z) % 8) ++Z;
   Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)nd * M * G::NT)));
@@ -1613,6 +1817,20 @@ static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int
   } else {
     // the two column halves of a row tile in adjacent x; ABCD_WG3W = 4 or 8
     // waves; ABCD_WG3DIAG: the timing probes (wrong results)
+    if (w3b) {
+      static bool attr_b = false;
+      if (!attr_b) {
+        ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg3b_kernel<N1, N2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)Wg3b<N1, N2>::LDS));
+        attr_b = true;
+      }
+      gemm_wg3b_kernel<N1, N2><<<dim3(2 * mtb, 1, nd * Z), 512, Wg3b<N1, N2>::LDS, s>>>(a);
+      ABCD_CHECK_LAUNCH();
+      const long nqb = (long)nd * M * G::NT / 4;
+      wg2_reduce_kernel<<<(int)std::min<long>(2048, cdiv(nqb, 256)), 256, 0, s>>>(scratch, nd, Z, M, G::NT, N1, F, N2, o);
+      ABCD_CHECK_LAUNCH();
+      return 0;
+    }
     const char* dg = getenv("ABCD_WG3DIAG");
     const char* wv = getenv("ABCD_WG3W");
     const int diag = dg ? atoi(dg) : 0;
