@@ -1563,7 +1563,8 @@ __global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
 // but ONE B stage (39 KiB): the next chunk's B columns are split and stored
 // between two barriers at the end of each chunk; the A rows as in wg3, inside
 // the MFMA gaps.  8 waves as 4 row groups (64 rows) x 2 column groups (7 / 6
-// blocks).  (ABCD_WG3W=b, an experiment.)
+// blocks).  Same-box A/B at c2 against the 4 x 2 gemm_wg3: 507 vs ~579 us
+// per launch, step 8.97 / 8.94 -> 8.85 / 8.86 ms.  The default.
 template <int N1, int N2>
 struct Wg3b {
   static constexpr int NT = N1 + N2, NB = (NT + 15) / 16, NBH = (NB + 1) / 2, NH = 16 * NBH;
@@ -1788,8 +1789,10 @@ static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int
   static_assert(Wg3<N1, N2>::BM == G::BM && Wg3<N1, N2>::NT == G::NT, "same slab geometry");
   const int mt = cdiv(M, G::BM);
   // one workgroup per CU: about 256 / (nd x mt) K ranges, the grid a multiple of 8
+  // gemm_wg3b (256-row tiles) by default; ABCD_WG3W = 2 / 8 / 4: gemm_wg3's
+  // 4 x 2, 8 x 1 or 4-wave forms (128-row tiles)
   const char* wv0 = getenv("ABCD_WG3W");
-  const bool w3b = W3 && wv0 && wv0[0] == 'b';  // gemm_wg3b: 256-row tiles
+  const bool w3b = W3 && !(wv0 && (wv0[0] == '2' || wv0[0] == '8' || wv0[0] == '4'));
   const int mtb = w3b ? cdiv(M, 256) : mt;
   const int tw = W3 ? 2 * mtb : mt;  // workgroups per (direction, K range)
   int Z = std::max(1, 256 / (nd * tw));

@@ -30,7 +30,7 @@ def test_gemm_nt_vs_torch(M, N, K):
     assert err <= 1e-5 * K ** 0.5 * 4 + 1e-5, err
 
 
-@pytest.mark.parametrize("wg", ["3", "2", "3w8"])
+@pytest.mark.parametrize("wg", ["3", "2", "3w8", "3w2"])
 @pytest.mark.parametrize("nd,F,H,K", [(2, 129, 256, 65583), (1, 129, 256, 3001), (2, 130, 256, 777), (2, 33, 48, 500),
                                        (1, 20, 24, 64), (2, 129, 256, 31), (1, 143, 256, 100003)])
 def test_lstm_wgrad_vs_torch(nd, F, H, K, wg, monkeypatch):
@@ -39,10 +39,10 @@ def test_lstm_wgrad_vs_torch(nd, F, H, K, wg, monkeypatch):
     (ABCD_WG3=0) at F <= 143, H = 256 (the c2 shape first, both directions;
     a K below one chunk; the widest F with a K range that is not a multiple
     of 32), the split-GEMM route elsewhere -- against float64 torch."""
-    # "3": gemm_wg3 in its default 4 x 2 wave form; "3w8": its 8 x 1 form
+    # "3": the default (gemm_wg3b, 256-row tiles); "3w2" / "3w8": gemm_wg3's 4 x 2 / 8 x 1 forms
     monkeypatch.setenv("ABCD_WG3", "0" if wg == "2" else "1")
-    if wg == "3w8":
-        monkeypatch.setenv("ABCD_WG3W", "8")
+    if wg in ("3w8", "3w2"):
+        monkeypatch.setenv("ABCD_WG3W", wg[2])
     wg = wg[0]
     import ctypes
     from modules import _native as Nn
