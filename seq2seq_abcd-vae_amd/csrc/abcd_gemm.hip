@@ -1875,6 +1875,13 @@ bool wg3_on() {
   const char* v = getenv("ABCD_WG3");
   return !(v && v[0] == '0');
 }
+// the dispatch record's name of the form wgrad_lstm_l0 runs (printf format, Fp, H, nd)
+const char* wg_dispatch_fmt() {
+  if (!wg3_on()) return "gemm_wg2<%d,%d> x%d";
+  const char* wv = getenv("ABCD_WG3W");
+  const bool w3b = !(wv && (wv[0] == '2' || wv[0] == '8' || wv[0] == '4'));
+  return w3b ? "gemm_wg3b<%d,%d> x%d" : "gemm_wg3<%d,%d> x%d";
+}
 
 template <int MR, int NR, bool AKC, bool BKC>
 static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,

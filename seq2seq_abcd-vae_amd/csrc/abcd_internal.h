@@ -110,6 +110,7 @@ struct WgOut {
   float* w_hh[2];
 };
 bool wg3_on();  // gemm_wg3 (default) or gemm_wg2 for the layer-0 LSTM weight gradients
+const char* wg_dispatch_fmt();  // "gemm_wg3b<%d,%d> x%d" etc.: the form wgrad_lstm_l0 runs
 int wgrad_lstm_l0(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F, int Fp, int H, float* scratch,
                   size_t scratch_floats);
 

@@ -645,7 +645,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
         if (wg2 > 0) return wg2;
       }
     }
-    if (l == 0) note_dispatch(TK_ENC_WGRAD, wg2 == 0 ? (wg3_on() ? "gemm_wg3<%d,%d> x%d" : "gemm_wg2<%d,%d> x%d")
+    if (l == 0) note_dispatch(TK_ENC_WGRAD, wg2 == 0 ? wg_dispatch_fmt()
                                                    : "gemm split (x6s/x6t)", Fp, H, D);
     if (wg2 == 0) {
     } else if (D == 2 && l == 0 && wgrad_stream && wgrad_stream != stream) {
@@ -1053,7 +1053,7 @@ extern "C" int abcd_lstm_wgrad(int nd, int F, int H, int K, const float* const* 
   for (int d = 0; d < nd; ++d) dirs[d] = WgDir{dG[d], Xp, Hprev[d], w_ih[d], b_ih[d], b_hh ? b_hh[d] : nullptr, w_hh[d]};
   const int r = wgrad_lstm_l0(s, nd, dirs, M, K, F, Fp, H, scratch, scf);
   if (r == 0) {
-    note_dispatch(TK_ENC_WGRAD, wg3_on() ? "gemm_wg3<%d,%d> x%d" : "gemm_wg2<%d,%d> x%d", Fp, H, nd);
+    note_dispatch(TK_ENC_WGRAD, wg_dispatch_fmt(), Fp, H, nd);
     return 0;
   }
   if (r > 0) return r;

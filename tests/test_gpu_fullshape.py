@@ -105,8 +105,8 @@ def test_full_shape_step_vs_oracle(name, B, seed):
     for role, kern in zip(("enc_fwd", "enc_bwd", "dec_fwd", "dec_bwd"), KERNELS[cfg["rnn"]]):
         assert ran[role][0] == f"{kern} grid {grids[role]}", (role, ran[role])
         assert ran[role][1] == 1, (role, ran[role])
-    # the encoder's weight gradients: one gemm_wg3 launch for both directions (LSTM), split GEMMs (GRU)
-    wg = "gemm_wg3<144,256> x2" if cfg["rnn"] == "LSTM" else "gemm split (x6s/x6t)"
+    # the encoder's weight gradients: one gemm_wg3b launch for both directions (LSTM), split GEMMs (GRU)
+    wg = "gemm_wg3b<144,256> x2" if cfg["rnn"] == "LSTM" else "gemm split (x6s/x6t)"
     assert ran["enc_wgrad"] == (wg, 1), ran["enc_wgrad"]
 
     obatch = dict(data=batch["data"], batch_sizes=bsz, is_offset=batch["is_offset"], speakers=batch["speakers"])

@@ -43,7 +43,7 @@ def test_lstm_wgrad_vs_torch(nd, F, H, K, wg, monkeypatch):
     monkeypatch.setenv("ABCD_WG3", "0" if wg == "2" else "1")
     if wg in ("3w8", "3w2"):
         monkeypatch.setenv("ABCD_WG3W", wg[2])
-    wg = wg[0]
+    wg = {"3": "3b", "2": "2"}.get(wg, "3")
     import ctypes
     from modules import _native as Nn
     g = torch.Generator(device="cuda").manual_seed(nd * 7 + F + H + K)

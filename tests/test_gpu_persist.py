@@ -119,7 +119,7 @@ def _with_env(key, val, fn):
 @pytest.mark.parametrize("wg", ["3", "2"])
 @pytest.mark.parametrize("B,Tmax", [(70, 30), (512, 200)])
 def test_encoder_wgrad_wg2(B, Tmax, wg):
-    """The layer-0 bi-LSTM weight gradients through gemm_wg3 (default) and
+    """The layer-0 bi-LSTM weight gradients through gemm_wg3b (default) and
     gemm_wg2 (ABCD_WG3=0) -- one launch for both directions: [dW_ih | db |
     dW_hh] = dG^T [X | 1 | Hprev], F = 129, H = 256 -- against the split GEMM
     route (ABCD_WG2=0) and, at the small batch, against torch.nn.LSTM in
@@ -131,7 +131,7 @@ def test_encoder_wgrad_wg2(B, Tmax, wg):
     dout = torch.randn(B, enc.hidden_size_total, device="cuda")
     Nn.lib().abcd_dispatch_reset()
     out_n, g_n = _with_env("ABCD_WG3", "1" if wg == "3" else "0", lambda: _run(enc, packed, dout, persist=True))
-    assert Nn.dispatch()["enc_wgrad"] == (f"gemm_wg{wg}<144,256> x2", 1)
+    assert Nn.dispatch()["enc_wgrad"] == (f"gemm_wg{'3b' if wg == '3' else wg}<144,256> x2", 1)
     out_o, g_o = _with_env("ABCD_WG2", "0", lambda: _run(enc, packed, dout, persist=True))
     assert Nn.dispatch()["enc_wgrad"] == ("gemm split (x6s/x6t)", 2)
     assert torch.equal(out_n, out_o)
