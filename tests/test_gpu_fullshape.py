@@ -51,6 +51,9 @@ if _DB.startswith("s"):
 elif _DB.startswith("f"):
     KERNELS = {r: k[:3] + (f"dec_bwd_fold<9,16,{r}>",) for r, k in KERNELS.items()}
 W8 = not os.environ.get("ABCD_ENCBWD", "").startswith("s")  # the 32-row / 8-member encoder BPTT (default)
+# the encoder weight-gradient form (ABCD_WG3=0: gemm_wg2; ABCD_WG3W=2/8/4: gemm_wg3; default gemm_wg3b)
+WG_FORM = ("gemm_wg2" if os.environ.get("ABCD_WG3", "") == "0"
+           else "gemm_wg3" if os.environ.get("ABCD_WG3W", "")[:1] in ("2", "8", "4") else "gemm_wg3b")
 if not W8:
     KERNELS = {r: (k[0], f"enc_bwd_sk<{4 if r == 'LSTM' else 3},16>") + k[2:] for r, k in KERNELS.items()}
 
@@ -106,7 +109,7 @@ def test_full_shape_step_vs_oracle(name, B, seed):
         assert ran[role][0] == f"{kern} grid {grids[role]}", (role, ran[role])
         assert ran[role][1] == 1, (role, ran[role])
     # the encoder's weight gradients: one gemm_wg3b launch for both directions (LSTM), split GEMMs (GRU)
-    wg = "gemm_wg3b<144,256> x2" if cfg["rnn"] == "LSTM" else "gemm split (x6s/x6t)"
+    wg = f"{WG_FORM}<144,256> x2" if cfg["rnn"] == "LSTM" else "gemm split (x6s/x6t)"
     assert ran["enc_wgrad"] == (wg, 1), ran["enc_wgrad"]
 
     obatch = dict(data=batch["data"], batch_sizes=bsz, is_offset=batch["is_offset"], speakers=batch["speakers"])
