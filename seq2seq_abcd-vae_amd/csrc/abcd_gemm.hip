@@ -722,7 +722,8 @@ static int gemm_x6f_launch(hipStream_t s, int M, int N, int K, const float* A, l
 // B-plane LDS reads, the splits, the epilogue transposes and the MFMAs.
 // Tried and slower: a three-slot register ring (blocks two ahead, 391 us),
 // MR = 4 (scratch), BN = 64 at two workgroups per CU (294-311 us, more A
-// re-reads), MR = 1 (306-339 us).
+// re-reads), MR = 1 (306-339 us); MR = 3 (round 4: 48-row blocks, 196 AGPRs
+// as spill room): input projection 292 us either way, offset head 82 vs 71.
 // ---------------------------------------------------------------------------
 template <int NC, int BN, int MR, int OCC>
 __global__ __launch_bounds__(256, OCC) void gemm_x6r_kernel(const float* __restrict__ A, long lda,
