@@ -1068,12 +1068,7 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 // the next step's Hprev rows) -- as two more tiles beside the mlp tile, and
 // carried in registers; step t+1's cell then waits only for x_{t+1} and runs
 // the NCC - 8 input chunks (H = 256: 8 recurrent chunks).
-// EK (round 4): emit over ALL 32 members with K split in two: member (tile jq
-// < 8, 16-row quarter) runs mu on waves 0 / 1 and lv on waves 2 / 3, each
-// wave half of K = Hm (an 8-KiB gather instead of 16); the three partial tiles
-// meet in LDS and wave 0 samples.  A ninth column tile (Fp = 144: F = 129's
-// last column) is formed on wave 2 by VALU dot products, two rows per member.
-template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, bool EK = false>
+template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
@@ -1091,17 +1086,15 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
            a.sync + ((size_t)2 * a.nrt + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
            M, mem, a.flags, 0u};
   // emit roles: tile j2 of [mu | lv] columns, row half `half`; wave part 0 = mu, 1 = lv
-  // (EK: tile j2 = mem >> 2 < 8, rows 16 (mem & 3) .., K half kh = w & 1)
-  const int j2 = EK ? mem >> 2 : mem >> 1, half = mem & 1, part = w >> 1, kh = w & 1;
-  const int erow0 = EK ? rt * PERSIST_ROWS + 16 * (mem & 3) : rt * PERSIST_ROWS + 32 * half + 16 * (w & 1);
-  const bool has1 = mem < n1t, has2 = j2 < (EK ? (n2t < 8 ? n2t : 8) : n2t);
-  const int nxt = EK && n2t > 8 ? F - 128 : 0;  // EK: real columns of the ninth tile (VALU path)
+  const int j2 = mem >> 1, half = mem & 1, part = w >> 1;
+  const int erow0 = rt * PERSIST_ROWS + 32 * half + 16 * (w & 1);
+  const bool has1 = mem < n1t, has2 = j2 < n2t;
   // LDS images
   f4* BC = smem;                        // cell [x | h]: [2][NCC][3][64]
   f4* B1 = BC + 2 * NCC * 3 * 64;       // mlp tile: [NH32][3][64]
   f4* B2 = B1 + NH32 * 3 * 64;          // emit: mu tile, lv tile: [2][NM32][3][64]
-  float* LVX = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [2][16][16] (EK: [3][16][16])
-  float* tb = LVX + (EK ? 3 : 2) * 16 * 16 + w * TP_FLOATS;        // this wave's transpose tile
+  float* LVX = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [2][16][16]
+  float* tb = LVX + 2 * 16 * 16 + w * TP_FLOATS;                   // this wave's transpose tile
   if (nx32)
     stage_x6(BC, a.Wih, Fp, Fp, 2, nx32, 0, NCC,
              [&](int j, int rr) { return GRU ? dec_gru_row(H, u0, j, rr, true) : dec_cell_row(H, u0, j, rr); });
@@ -1116,7 +1109,6 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   const float b1v = has1 ? a.b1[16 * mem + r] : 0.f;
   const int col2 = 16 * j2 + r;
   const float b2v = has2 ? (part ? a.b2l[col2] : a.b2m[col2]) : 0.f;
-  const float b2lv = EK && has2 ? a.b2l[col2] : 0.f;  // EK: wave 0 finishes lv too
   const bool lo = r < 8;
   __syncthreads();
   float cst[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1236,115 +1228,6 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     gs.publish();
     PSTAMP(3);
     // ---------------- emit ----------------
-    if constexpr (EK) {
-      // wave 0's noise for its tile, drawn before the wait
-      float epre[4] = {0.f, 0.f, 0.f, 0.f}, mpre[4] = {1.f, 1.f, 1.f, 1.f};
-      if (has2 && w == 0 && col2 < F) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int b = erow0 + 4 * q + g;
-          if (b < bs) {
-            const long rr = o + b;
-            epre[g] = a.eps ? a.eps[rr * F + col2] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col2);
-            if (a.xmask && b < next_bs) mpre[g] = a.xmask[(long)(next_off + b) * F + col2];
-          }
-        }
-      }
-      // the ninth tile: wave 2 owns rows 2 mem, 2 mem + 1 of the group; lane l
-      // (row l >> 5, segment l & 31: Aact columns 16 seg .. + 15) -- its noise
-      // for the (at most 16) real columns, one per lane of each row half
-      const int xrow = rt * PERSIST_ROWS + 2 * mem + (lane >> 5), xseg = lane & 31;
-      float xe = 0.f, xm = 1.f;
-      if (nxt > 0 && w == 2 && (lane & 31) < nxt && xrow < bs) {
-        const int c = 128 + (lane & 31);
-        const long rr = o + xrow;
-        xe = a.eps ? a.eps[rr * F + c] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + c);
-        if (a.xmask && xrow < next_bs) xm = a.xmask[(long)(next_off + xrow) * F + c];
-      }
-      gs.wait(3u * i + 2, 3);
-      PSTAMP(4);
-      f4 xa[4];  // wave 2: its 16 Aact values of the ninth tile's rows (loaded behind the MMA)
-      if (nxt > 0 && w == 2) {
-        const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          xa[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rx, (uint32_t)(xrow * 2 * Hm + 16 * xseg + 4 * k) * 4u, 0, 16));
-      }
-      f4 ae[1] = {f4zero()};
-      if (has2 && erow0 < bs) {
-        const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm + kh * (Hm / 2),
-                                                    (uint32_t)(bs * 2 * Hm - part * Hm - kh * (Hm / 2)) * 4u);
-        const BufKC Aa{rk, (uint32_t)2 * Hm * 4u};
-        wave_mma_x6<1, NM32 / 2, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64 + kh * (NM32 / 2) * 3 * 64, NM32, lane,
-                                    q, mem % (NM32 / 2));
-      }
-      if (w > 0) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) LVX[((w - 1) * 16 + 4 * q + g) * 16 + r] = ae[0][g];
-      }
-      float xo[3] = {0.f, 0.f, 0.f};  // wave 2, ninth tile: mu, lv, x of (xrow, 128 + (lane & 31))
-      if (nxt > 0 && w == 2) {
-        // per real column c: the 16-lane segments (row, part) reduce their dot products
-        for (int c = 0; c < nxt; ++c) {
-          const float* wr = (xseg < 16 ? a.W2m : a.W2l) + (size_t)(128 + c) * Hm + 16 * (xseg & 15);
-          float d = 0.f;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const f4 wv = *reinterpret_cast<const f4*>(wr + 4 * k);
-            d += xa[k][0] * wv[0] + xa[k][1] * wv[1] + xa[k][2] * wv[2] + xa[k][3] * wv[3];
-          }
-#pragma unroll
-          for (int sh = 1; sh < 16; sh <<= 1) d += __shfl_xor(d, sh, 64);
-          // lanes 0 / 32 hold mu of rows 0 / 1, lanes 16 / 48 lv
-          const float lvv = __shfl(d, (lane & 32) + 16, 64);
-          const float muv = __shfl(d, lane & 32, 64);
-          if ((lane & 31) == c) {
-            xo[0] = muv + a.b2m[128 + c];
-            xo[1] = lvv + a.b2l[128 + c];
-          }
-        }
-        xo[2] = (lane & 31) < nxt ? xo[0] + __expf(0.5f * xo[1]) * xe : 0.f;
-        // the self-feedback input of the tile's 16 columns (the pad ones 0: the
-        // next cell multiplies all Fp columns)
-        if (a.feedback && (lane & 31) < 16 && xrow < next_bs)
-          st_sc1(a.Xin + (long)(next_off + xrow) * Fp + 128 + (lane & 31), xo[2] * xm);
-      }
-      __syncthreads();
-      const uint32_t eoff = (uint32_t)((erow0 + trow) * Fp + 16 * j2 + tcol) * 4u;
-      float mu[4] = {0.f, 0.f, 0.f, 0.f}, lv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (has2 && w == 0) {
-        float xv[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int e = (4 * q + g) * 16 + r;
-          mu[g] = col2 < F ? ae[0][g] + LVX[e] + b2v : 0.f;
-          lv[g] = col2 < F ? LVX[256 + e] + LVX[512 + e] + b2lv : 0.f;
-          const float x = col2 < F ? mu[g] + __expf(0.5f * lv[g]) * epre[g] : 0.f;
-          epre[g] = x;
-          xv[g] = x * mpre[g];
-        }
-        const f4 xq = tp_quad(tb, xv, lane);
-        if (a.feedback && erow0 < next_bs)
-          st4(make_rsrc(a.Xin + (size_t)next_off * Fp, (uint32_t)next_bs * Fp * 4u), eoff, xq, true);
-      }
-      gs.publish();
-      if (has2 && w == 0 && erow0 < bs) {
-        const uint32_t ext = (uint32_t)bs * Fp * 4u;
-        st4(make_rsrc(a.MU + (size_t)o * Fp, ext), eoff, tp_quad(tb, mu, lane), false);
-        st4(make_rsrc(a.LV + (size_t)o * Fp, ext), eoff, tp_quad(tb, lv, lane), false);
-        st4(make_rsrc(a.OUT + (size_t)o * Fp, ext), eoff, tp_quad(tb, epre, lane), false);
-      }
-      if (nxt > 0 && w == 2 && xrow < bs) {  // the ninth tile's columns (the pad ones: 0)
-        const long rr = o + xrow;
-        const int c = 128 + (lane & 31);
-        if ((lane & 31) < 16) {
-          a.MU[rr * Fp + c] = xo[0];
-          a.LV[rr * Fp + c] = xo[1];
-          a.OUT[rr * Fp + c] = xo[2];
-        }
-      }
-    } else {
     // the mu waves' noise, drawn before the wait (independent of the recurrence)
     float epre[4] = {0.f, 0.f, 0.f, 0.f}, mpre[4] = {1.f, 1.f, 1.f, 1.f};
     if (has2 && part == 0 && col2 < F) {
@@ -1403,7 +1286,6 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       } else {
         st4(make_rsrc(a.LV + (size_t)o * Fp, ext), eoff, tp_quad(tb, ev, lane), false);
       }
-    }
     }
     PSTAMP(5);
   }
@@ -3301,13 +3183,13 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, bool EK = false>
+template <int NCC, int NH32, int NM32, bool GRU, bool HPRE>
 static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
-  const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + (EK ? 3 : 2) * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
+  const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, EK>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
@@ -3315,7 +3197,7 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, EK><<<grid, 256, lds, s>>>(b);
+    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
@@ -3326,10 +3208,6 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
 
 template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
-  // EK emit (all 32 members, K split in two) for at most 9 column tiles; ABCD_DECFWD_EK=0: the 18-member emit
-  const char* v = getenv("ABCD_DECFWD_EK");
-  if (!(v && v[0] == '0') && a.Fp <= 144 && NM32 == 8 && a.H / 8 == 32)
-    return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, true>(s, a, launched);
   return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true>(s, a, launched);
 }
 
