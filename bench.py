@@ -480,7 +480,15 @@ def kernel_roofline(step, batches, cfg, run, cfg_name):
             "x6_ceiling": {"peak": round(X6_CEILING_TFLOPS, 1), "frac": round(achieved / X6_CEILING_TFLOPS, 4),
                            "what": "bf16 dense MFMA peak / 6: the split-fp32 products' instruction ceiling"},
             "avg_launch_us": d["avg_launch_us"], "launches": d["launches"],
-            "flops_per_launch": d["flops_per_launch"], "all_kernels": per}
+            "flops_per_launch": d["flops_per_launch"],
+            # where each field comes from: achieved / frac are measured in THIS run;
+            # traffic and mfma_busy are read from rocprofv3 PMC passes committed
+            # under profiles/ (PMC counters cannot run inside the timed bench)
+            "provenance": {"achieved": "live: HIP events on the launch stream, this run",
+                           "traffic": "committed profile: profiles/traffic.json" if traffic is not None else None,
+                           "mfma_busy": "committed profile: profiles/pmc_mfma.json"
+                           if load_mfma(dom, cfg_name) is not None else None},
+            "all_kernels": per}
 
 
 if __name__ == "__main__":

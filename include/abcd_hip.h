@@ -382,8 +382,9 @@ void abcd_dispatch_reset(void);
  * (1 enc fwd, 2 enc bwd, 4 dec fwd, 8 dec bwd) stamp s_memrealtime at their
  * phase boundaries into dev_buf (blocks x T x 8 u64; null: off);
  * abcd_debug_xcc_map -- launches `blocks` one-per-CU workgroups that record
- * their XCC id into dev_out[block] (the placement the persistent kernels'
- * group roles rely on).  Returns 0 / a HIP error. */
+ * their (XCC id, HW_ID) pair into dev_out[2 * block], dev_out[2 * block + 1]
+ * (dev_out holds 2 * blocks u32; the placement the persistent kernels' group
+ * roles rely on).  Returns 0 / a HIP error. */
 void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask);
 int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream);
 /* 0 if no persistent recurrent kernel has timed out waiting for its group

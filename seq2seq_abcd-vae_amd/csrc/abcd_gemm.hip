@@ -11,6 +11,7 @@
 //              pass reduces deterministically.
 #include <numeric>
 #include <cstdlib>
+#include <cstdio>
 
 #include "abcd_common.h"
 #include <mutex>
@@ -1774,13 +1775,25 @@ static int wg3_go1(hipStream_t s, const WgArgs& a, dim3 grid) {
   return 0;
 }
 
+// the DIAG timing probes compute wrong results: they exist only in a
+// diagnostics build (make EXTRA=-DABCD_WG_DIAG); a normal build ignores
+// ABCD_WG3DIAG (with a warning) and always runs the real kernel
 template <int N1, int N2, int W, int WN>
 static int wg3_go(hipStream_t s, const WgArgs& a, dim3 grid, int diag) {
+#ifdef ABCD_WG_DIAG
   switch (diag) {
     case 1: return wg3_go1<N1, N2, W, WN, 1>(s, a, grid);
     case 2: return wg3_go1<N1, N2, W, WN, 2>(s, a, grid);
-    default: return wg3_go1<N1, N2, W, WN, 0>(s, a, grid);
+    default: break;
   }
+#else
+  static bool warned = false;
+  if (diag && !warned) {
+    fprintf(stderr, "libabcd_hip: ABCD_WG3DIAG ignored (timing probes exist only in a -DABCD_WG_DIAG build)\n");
+    warned = true;
+  }
+#endif
+  return wg3_go1<N1, N2, W, WN, 0>(s, a, grid);
 }
 
 template <int N1, int N2, bool W3>

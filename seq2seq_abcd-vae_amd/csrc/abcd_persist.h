@@ -58,6 +58,7 @@ struct PBwdArgs {
 //   emit : mu, lv = Aact W2^T + b2; x = mu + e^{lv/2} eps -> Xin_{t+1}
 struct PDecFwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
+  int L, B;                        // packed rows, rows of step 0 (the data-as-flag fill)
   int flags;                       // hand-off form: 1 per-member flags, 0 group counter
   const int* off;
   unsigned* sync;

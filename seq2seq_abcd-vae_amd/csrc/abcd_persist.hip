@@ -228,6 +228,60 @@ struct GSync {
   }
 };
 
+// Data-as-flag hand-off (MI355X_MICROARCH.md handoff-1to1: the payload is its
+// own flag).  A hand-off buffer whose every word is written exactly ONCE per
+// launch (the decoder forward's Hs / Aact / Xin stash rows: distinct per step)
+// is filled with HANDOFF_EMPTY before the launch; producers store their words
+// write-through (sc1) with no drain and no signal, and a consumer re-reads, with
+// sc1 loads, each 32-deep operand chunk until none of its words is still
+// HANDOFF_EMPTY -- one memory round trip after the producer's store instead of
+// drain + flag + poll + barrier + gather.  Each 4-B word is single-copy
+// atomic, so a word is either the fill or its final value.  HANDOFF_EMPTY is a
+// signalling NaN: arithmetic never produces one (every fp32 op quiets NaNs),
+// so neither real data nor a diverged (NaN) run can look empty.
+constexpr unsigned HANDOFF_EMPTY = 0x7FA5A5A5u;
+DEV bool any_empty(const f4& a, const f4& b) {
+  // (the elements go through scalars: hipcc (ROCm 7.2) lowers
+  // __builtin_bit_cast of a vector-element lvalue to a read of element 0)
+  bool e = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float x = a[k], y = b[k];
+    e |= (__builtin_bit_cast(unsigned, x) == HANDOFF_EMPTY) | (__builtin_bit_cast(unsigned, y) == HANDOFF_EMPTY);
+  }
+  return e;
+}
+// wave_mma_x6's chunk check (abcd_x6.h X6_POLL_CHUNK): a chunk with a word
+// still HANDOFF_EMPTY is re-read; every hand-off wait is bounded (a timeout
+// sets the status and goes on with what it has)
+struct PollEmpty {
+  static constexpr bool on = true;
+  DEV bool empty(const f4& a, const f4& b) const { return any_empty(a, b); }
+  DEV unsigned limit() const { return g_spin_limit; }
+  DEV bool spin(unsigned& spins, unsigned lim) const {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > lim) {
+      if ((threadIdx.x & 63) == 0) spin_timed_out();
+      return false;
+    }
+    return (spins & SPIN_PROBE_MASK) != 0 || !spin_abandoned();
+  }
+};
+// fill [p, p + n4 float4s) with HANDOFF_EMPTY (one kernel per launch, up to 3 ranges)
+struct FillRanges {
+  float* p[3];
+  long n4[3];
+};
+__global__ __launch_bounds__(256) void handoff_fill(FillRanges fr) {
+  const uint4 v = make_uint4(HANDOFF_EMPTY, HANDOFF_EMPTY, HANDOFF_EMPTY, HANDOFF_EMPTY);
+  const long stride = (long)gridDim.x * 256;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    uint4* d = reinterpret_cast<uint4*>(fr.p[k]);
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < fr.n4[k]; i += stride) d[i] = v;
+  }
+}
+
 // diagnostics: thread 0 stamps s_memrealtime (100 MHz, one clock for the whole
 // device, so stamps of different workgroups compare) at the phase boundaries of step i
 #define PSTAMP(k)                                                                                   \
@@ -408,8 +462,9 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
 // ---------------------------------------------------------------------------
 // encoder backward (BPTT): one launch per layer, both directions
 // ---------------------------------------------------------------------------
-// X6 > 0: split-fp32 recurrent MMA over X6 = G * H / 32 chunks (abcd_x6.h)
-template <int G, int PD, int X6>
+// fp32 MFMA gather form, for the widths the split-K forms (enc_bwd_w8 at
+// H = 256, enc_bwd_sk at 64 / 128) do not cover
+template <int G, int PD>
 __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, GH = G * H, nut = H / 16, nchg = GH / 16, T = a.T;
@@ -422,8 +477,7 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
   const int u0 = mem * 16, unit = u0 + r;
   const int row0 = rt * PERSIST_ROWS + w * 16;
   unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
-  if (X6) stage_x6(smem, D.WhhT, GH, GH, 1, GH / 32, 0, GH / 32, [&](int, int rr) { return u0 + rr; });
-  else stage_b_frag(smem, D.WhhT, GH, 1, nchg, [&](int) { return u0; });
+  stage_b_frag(smem, D.WhhT, GH, 1, nchg, [&](int) { return u0; });
   __syncthreads();
   float carry[4] = {0.f, 0.f, 0.f, 0.f};  // LSTM dc*f / GRU dh*z flowing to the predecessor
   const int* off = a.off;
@@ -473,8 +527,7 @@ __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
     acc2_zero(acc);
     if (row0 < bs && succ_valid > 0) {
       const BufKC A{make_rsrc(D.dGH + (size_t)succ_off * GH, (uint32_t)succ_valid * GH * 4u), (uint32_t)GH * 4u};
-      if (X6) wave_mma_x6<1, (X6 > 0 ? X6 : 1), 8>(acc[0], A, row0 + r, smem, X6, lane, q);
-      else wave_mma_lds<1, PD>(acc, A, row0 + r, smem, nchg, lane, q);
+      wave_mma_lds<1, PD>(acc, A, row0 + r, smem, nchg, lane, q);
     }
     acc2_fold(acc);
     PSTAMP(2);
@@ -1068,8 +1121,17 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 // the next step's Hprev rows) -- as two more tiles beside the mlp tile, and
 // carried in registers; step t+1's cell then waits only for x_{t+1} and runs
 // the NCC - 8 input chunks (H = 256: 8 recurrent chunks).
-template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true>
+// DF: the three hand-offs are data-as-flag (HANDOFF_EMPTY above): Hs, Aact and
+// the fed-back Xin rows are filled before the launch, each consumer wave polls
+// its own operand chunks inside the MMA (PollEmpty), and nothing is drained,
+// signalled or waited for at the phase boundaries.  Requires HPRE (the cell
+// then reads no Hprev row written in the launch, so Hprev leaves as a plain
+// stash store).  LVX is double-buffered by step parity: with no group-wide
+// wait per phase, the emit barrier of step t+1 is what orders step t's LVX
+// reads before step t+2's writes.
+template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, bool DF = false>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
+  static_assert(!DF || HPRE, "the data-as-flag form forms the recurrent half in the mlp phase");
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
   const int M = H / 8;
@@ -1093,8 +1155,8 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   f4* BC = smem;                        // cell [x | h]: [2][NCC][3][64]
   f4* B1 = BC + 2 * NCC * 3 * 64;       // mlp tile: [NH32][3][64]
   f4* B2 = B1 + NH32 * 3 * 64;          // emit: mu tile, lv tile: [2][NM32][3][64]
-  float* LVX = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [2][16][16]
-  float* tb = LVX + 2 * 16 * 16 + w * TP_FLOATS;                   // this wave's transpose tile
+  float* LVX0 = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [DF ? 2 : 1][2][16][16]
+  float* tb = LVX0 + (DF ? 2 : 1) * 2 * 16 * 16 + w * TP_FLOATS;   // this wave's transpose tile
   if (nx32)
     stage_x6(BC, a.Wih, Fp, Fp, 2, nx32, 0, NCC,
              [&](int j, int rr) { return GRU ? dec_gru_row(H, u0, j, rr, true) : dec_cell_row(H, u0, j, rr); });
@@ -1128,7 +1190,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         cst[g] = b < bs ? (GRU ? a.Hprev : a.Cprev)[(long)(o + b) * H + unit] : 0.f;
       }
     }
-    if (i > 0) gs.wait(3u * i);
+    if (!DF && i > 0) gs.wait(3u * i);
     PSTAMP(0);
     f4 acc[2];
     acc[0] = acc[1] = f4zero();
@@ -1140,7 +1202,9 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       if (HPRE && i > 0) {
         acc[0] = acch[0];
         acc[1] = acch[1];
-        if constexpr (NXC > 0)
+        if constexpr (NXC > 0 && DF)
+          wave_mma_x6<2, (NXC > 0 ? NXC : 1), 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC, PollEmpty{});
+        else if constexpr (NXC > 0)
           wave_mma_x6<2, (NXC > 0 ? NXC : 1), 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC);
       } else {
         wave_mma_x6<2, NCC, 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NCC);
@@ -1178,10 +1242,10 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       const f4 hq = tp_quad(tb, hv, lane);
       if (row0 < bs) {
         if (!thi) st4(make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), qoff, hq, true);
-        else st4(make_rsrc(a.Hprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, hq, true);
+        else st4(make_rsrc(a.Hprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, hq, !DF);
       }
     }
-    gs.publish();
+    if (!DF) gs.publish();
     PSTAMP(1);
     if (row0 < bs) {  // stashes for the backward pass (plain 16-B stores)
       const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
@@ -1201,7 +1265,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       }
     }
     // ---------------- mlp ----------------
-    gs.wait(3u * i + 1);
+    if (!DF) gs.wait(3u * i + 1);
     PSTAMP(2);
     if (has1) {
       f4 a1[1] = {f4zero()};
@@ -1210,10 +1274,13 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
-          wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
+          if constexpr (DF) wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32, PollEmpty{});
+          else wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
           a1[0] = a3[0];
           acch[0] = a3[1];
           acch[1] = a3[2];
+        } else if constexpr (DF) {
+          wave_mma_x6<1, NH32, 4>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32, PollEmpty{});
         } else {
           wave_mma_x6<1, NH32, 4>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32);
         }
@@ -1225,7 +1292,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         st4(make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
             (uint32_t)((row0 + trow) * 2 * Hm + 16 * mem + tcol) * 4u, aq, true);
     }
-    gs.publish();
+    if (!DF) gs.publish();
     PSTAMP(3);
     // ---------------- emit ----------------
     // the mu waves' noise, drawn before the wait (independent of the recurrence)
@@ -1243,16 +1310,20 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     }
     // polled by wave 3 (an lv wave): the mu waves' noise draw above is ~1 us
     // of VALU that would otherwise delay the poll
-    gs.wait(3u * i + 2, 3);
+    if (!DF) gs.wait(3u * i + 2, 3);
     PSTAMP(4);
+    float* LVX = LVX0 + (DF ? (i & 1) * 2 * 16 * 16 : 0);
     float ev[4] = {0.f, 0.f, 0.f, 0.f};  // mu (part 0) / lv (part 1); sample x kept in epre
     if (has2) {
       f4 ae[1] = {f4zero()};
       if (erow0 < bs) {
         const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
                        (uint32_t)2 * Hm * 4u};
-        wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
-                                mem % NM32);
+        if constexpr (DF)
+          wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q, mem % NM32,
+                                  PollEmpty{});
+        else
+          wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q, mem % NM32);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) ev[g] = col2 < F ? ae[0][g] + b2v : 0.f;
@@ -1277,7 +1348,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       if (a.feedback && erow0 < next_bs)
         st4(make_rsrc(a.Xin + (size_t)next_off * Fp, (uint32_t)next_bs * Fp * 4u), eoff, xq, true);
     }
-    gs.publish();
+    if (!DF) gs.publish();
     if (has2 && erow0 < bs) {
       const uint32_t ext = (uint32_t)bs * Fp * 4u;
       if (part == 0) {
@@ -1467,31 +1538,19 @@ __global__ __launch_bounds__(256) void dec_bwd_persist(PDecBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// decoder backward, split-K form (x6).  Same three phases per step as
-// dec_bwd_persist, but the big product of the BPTT step,
-//     [dx_{t+1} | dh_rec] = dG_{t+1} [W_ih | W_hh]^T-rows   (K = 4H),
-// is split over K by OWNERSHIP: in P2 every member m owns 8 hidden units (32
-// dG columns = 4 gates x 8 units; lanes r and r^8 run the cell backward of
-// the same unit, as dec_fwd_persist's cell phase does forward), and right
-// after its cell backward it multiplies those columns (wave-private LDS
-// transpose, ONE 32-deep x6 chunk) with its 32 rows of [W_ih | W_hh] and
-// publishes the partials of all NXS + NHS 16-column output subtiles in each
-// consumer's accumulator layout.  Consumers sum the M = H/8 partials:
-//   P0 (members < Fp/16): the dx tile -> dMU, dLV (+ emission NLL grads);
-//   P2 (every member):    dh_rec of its 8 units -- read right after the P0
-//                         wait, long before P2's own wait (the partials were
-//                         published one whole step earlier).
-// The gather form reads the 64-row x 4H dG block per wave (64 KiB on each of
-// 25 members, ~50 MiB per step through the fabric); here P0 moves 32 KiB per
-// wave on 9 members and P2's reads leave the critical path.  Partials are
-// double-buffered by step parity (written at step i into slot i&1, read at
-// step i+1; the slot is rewritten at step i+2 only after every member has
-// published P2 of step i+1, i.e. finished its reads).
-// NXS: Fp/16 with self-feedback, else 0; NHS = H/16; NZ = 2Hm/32 (P2's K chunks).
+// split-K BPTT building blocks.  The big product of a BPTT step (decoder:
+// [dx_{t+1} | dh_rec] = dG_{t+1} [W_ih | W_hh]^T-rows, K = 4H) is split over
+// K by OWNERSHIP: every member owns a block of hidden units (their gate
+// columns of dG), multiplies those columns with its rows of the weights right
+// after its cell backward, and publishes one partial of every output subtile
+// in each consumer's accumulator layout; consumers sum the partials
+// (sum_partials).  Partials are double-buffered by step parity (written at
+// step i into slot i & 1, read at step i + 1; rewritten at step i + 2 only
+// after every member has published the next phase, i.e. finished its reads).
+// The 64-row forms of rounds 2-3 (dec_bwd_sk: the dZ gather in P2;
+// dec_bwd_fold: dZ W1cat folded into the partials) were superseded by the
+// 32-row dec_bwd_w16 below and removed.
 // ---------------------------------------------------------------------------
-constexpr int DSK_PITCH = 36;  // floats per row of the wave-private dG transpose
-constexpr int DSK_WAVE_FLOATS = 2 * TP_FLOATS;  // per-wave LDS region: the dG transpose or two tp_quad tiles
-static_assert(16 * DSK_PITCH <= DSK_WAVE_FLOATS, "dG transpose fits the wave's region");
 // acc += sum of NP partial f4s at base + p * 1 KiB, NB loads in flight
 template <int NP, int NB = NP>
 DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc, int rot = 0) {
@@ -1508,633 +1567,8 @@ DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc, int rot
     for (int k = 0; k < NB; ++k) acc += v[k];
   }
 }
-// GRU: the member's 32 columns are dec_fwd_x6's [r | z | n_x | n_h]
-// (dG = [dr, dz, dn, dn r] pre-activation gradients), the split-K image takes
-// the n_x column from W_ih only and n_h from W_hh only, the carry is dh z, and
-// the stash is dGX = (dr, dz, dn), dGH = (dr, dz, dn r) with pitch 3H as the
-// per-step kernels write it.
-template <int NXS, int NHS, int NZ, bool GRU = false>
-__global__ __launch_bounds__(256) void dec_bwd_sk(PDecBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) f4 smem[];
-  constexpr int H = NHS * 16, GH = (GRU ? 3 : 4) * H, M = H / 8, NS = NXS + NHS;
-  const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
-  const int nchx = Fp / 16, nFt = Fp / 16;
-  const Role role = assign_role(a.nrt, M);
-  const int grp = role.grp, mem = role.mem;
-  const int rt = grp;
-  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int row0 = rt * PERSIST_ROWS + w * 16;
-  GSync gs{a.sync + grp * PERSIST_SYNC_STRIDE,
-           a.sync + ((size_t)2 * a.nrt + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
-           M, mem, a.flags, 0u};
-  const int u0 = mem * 8, unit = u0 + (r & 7);
-  const bool lo = r < 8;
-  // LDS: split-K image [NS][3][64] | P2 image [NZ][3][64] | P1 image [nchx][64] | dG transposes [4][16][PITCH]
-  f4* SK = smem;
-  f4* B2 = SK + NS * 3 * 64;
-  f4* B1 = B2 + NZ * 3 * 64;
-  float* Ast = reinterpret_cast<float*>(B1 + nchx * 64) + w * DSK_WAVE_FLOATS;
-  float* tb = Ast;  // the same wave-private region, reused for the 16-B store transposes (tp_quad)
-  const int trow = lane >> 2, tcol = 4 * (lane & 3);
-  // split-K image: subtile s, lane (rr, qq) holds rows k = 8qq + 0..7 (gate qq,
-  // own units 0..7) of output column 16s + rr: [W_ih | W_hh]^T row (col) ...
-  for (int e = threadIdx.x; e < NS * 64; e += 256) {
-    const int s = e >> 6, ln = e & 63, rr = ln & 15, qq = ln >> 4;
-    const bool xs = s < NXS;
-    int col = qq * H + u0;  // gate column (row of W) of the 8 own units
-    if (GRU && qq >= 2) col = (qq == 2) == xs ? 2 * H + u0 : -1;
-    const float* src = (xs ? a.WihT + (long)(16 * s + rr) * GH : a.WhhT + (long)(16 * (s - NXS) + rr) * GH) +
-                       (col < 0 ? 0 : col);
-    bf8 h, m, l;
-    split8(col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src),
-           col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src + 4), h, m, l);
-    SK[(s * 3) * 64 + ln] = __builtin_bit_cast(f4, h);
-    SK[(s * 3 + 1) * 64 + ln] = __builtin_bit_cast(f4, m);
-    SK[(s * 3 + 2) * 64 + ln] = __builtin_bit_cast(f4, l);
-  }
-  // P2: dh of the 8 own units (columns r and r + 8 both map to unit u0 + (r & 7))
-  stage_x6(B2, a.W1T, 2 * Hm, 2 * Hm, 1, NZ, 0, NZ, [&](int, int rr) { return u0 + (rr & 7); });
-  // P1: dZ tile j1 = mem (2Hm/16 == M: checked by the launcher)
-  const bool ismu = mem < Hm / 16;
-  if (ismu) stage_b_frag(B1, a.W2mT, Fp, 1, nchx, [&](int) { return 16 * mem; });
-  else stage_b_frag(B1, a.W2lT, Fp, 1, nchx, [&](int) { return 16 * (mem - Hm / 16); });
-  const float s_em = *a.s_em;
-  __syncthreads();
-  const size_t slot_f = (size_t)a.nrt * NS * 4 * M * 256;  // floats per parity slot
-  const __amdgpu_buffer_rsrc_t pr0 = make_rsrc(a.part, (uint32_t)(slot_f * 4));
-  const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
-  // this wave's block of subtile s: (((grp*NS + s)*4 + w)*M + producer)*256 floats
-  auto blk = [&](int s) { return (uint32_t)((((size_t)grp * NS + s) * 4 + w) * M) * 1024u; };
-  // this member's partial of output subtile s from the split dG tile (a0, a1, a2)
-  auto partial_st = [&](int s, const bf8& a0, const bf8& a1, const bf8& a2, __amdgpu_buffer_rsrc_t pw) {
-    const f4* bp = SK + (s * 3) * 64 + lane;
-    const f4 v = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
-                        __builtin_bit_cast(bf8, bp[128]));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
-                                           blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
-  };
-  float carry[4] = {0.f, 0.f, 0.f, 0.f};
-  // members < ND (the P0 members) defer their dh_rec partial stores from the
-  // end of P2 to the next step's P1 (issued behind the dMU / dLV loads and
-  // drained by the P1 publish): otherwise their next P0 poll -- on the
-  // critical path -- waits for 16 KiB per wave of write-through stores to
-  // drain (in-order vmcnt).  Consumers read those ND producers' partials
-  // after the P2 wait, the others' before it.
-  constexpr int ND = NXS;
-  const bool defer = mem < ND;
-  bool dmk = false;
-  bf8 da0{}, da1{}, da2{};
-  __amdgpu_buffer_rsrc_t dpw = pr0;
-  const int* off = a.off;
-  for (int i = 0; i < T; ++i) {
-    const int t = T - 1 - i;
-    const int o = off[t], bs = off[t + 1] - o;
-    const int succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
-    const bool has_part = i > 0 && row0 < succ_valid;  // step t+1's producers covered this wave's rows
-    const __amdgpu_buffer_rsrc_t prd = (i & 1) ? pr0 : pr1;  // slot (i - 1) & 1
-    // ---------------- P0: dx_{t+1} tile -> dMU, dLV ----------------
-    // emission operands of the tile: independent of the hand-off, loaded before the wait
-    const int col0 = 16 * mem + r;
-    float emu[4], elv[4], eox[4], ey[4], emk[4];
-    if (mem < nFt) {
-      const uint32_t ef = (uint32_t)bs * Fp * 4u;
-      const __amdgpu_buffer_rsrc_t rmu = make_rsrc(a.MU + (size_t)o * Fp, ef), rlv = make_rsrc(a.LV + (size_t)o * Fp, ef),
-                                   rox = make_rsrc(a.OUT + (size_t)o * Fp, ef),
-                                   ryy = make_rsrc(a.Y + (size_t)o * F, (uint32_t)bs * F * 4u);
-      // rows >= succ_valid have no dx (zero partials), so their mask value is irrelevant
-      const __amdgpu_buffer_rsrc_t rmk =
-          make_rsrc(a.xmask ? a.xmask + (size_t)(o + bs) * F : a.Y, a.xmask ? (uint32_t)succ_valid * F * 4u : 0u);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
-        const uint32_t of = col0 < F ? (b * Fp + col0) * 4u : 0x80000000u;
-        const uint32_t oy = col0 < F ? (b * F + col0) * 4u : 0x80000000u;
-        emu[g] = bld(rmu, of);
-        elv[g] = bld(rlv, of);
-        eox[g] = bld(rox, of);
-        ey[g] = bld(ryy, oy);
-        emk[g] = a.xmask ? bld(rmk, oy) : 1.f;
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) emu[g] = elv[g] = eox[g] = ey[g] = 0.f, emk[g] = 1.f;
-    }
-    if (i > 0) gs.wait(3u * i);
-    pin(emu), pin(elv), pin(eox), pin(ey), pin(emk);
-    PSTAMP(0);
-    if (mem < nFt) {
-      f4 dx = f4zero();
-      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(mem) + (uint32_t)lane * 16u, dx, mem % M);
-      float dmu[4], dlv[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        dmu[g] = dlv[g] = 0.f;
-        if (col0 < F) {
-          const float dxv = dx[g] * emk[g], mu = emu[g], lv = elv[g];
-          const float iv = __expf(-lv), d = ey[g] - mu;
-          dmu[g] = dxv + s_em * (-d) * iv;
-          dlv[g] = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);
-        }
-      }
-      const f4 mq = tp_quad(tb, dmu, lane), lq = tp_quad(tb + TP_FLOATS, dlv, lane);
-      if (row0 < bs) {  // rows >= bs fall outside the buffers' extent
-        const uint32_t qo = (uint32_t)((row0 + trow) * Fp + 16 * mem + tcol) * 4u;
-        st4(make_rsrc(a.dMU + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, mq, true);
-        st4(make_rsrc(a.dLV + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, lq, true);
-      }
-    }
-    gs.publish();
-    PSTAMP(1);
-    PSTAMP(6);
-    // ---------------- P1: dZ tile ----------------
-    float zpre[4];
-    {
-      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) zpre[g] = bld(rz, ((uint32_t)(row0 + 4 * q + g) * 2 * Hm + 16 * mem + r) * 4u);
-    }
-    gs.wait(3u * i + 1);
-    pin(zpre);
-    PSTAMP(2);
-    {
-      f4 acc[2][1];
-      acc2_zero(acc);
-      if (row0 < bs) {
-        const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
-        if (ND > 0 && defer && dmk) {
-          mma16<1>(acc, A, row0 + r, B1, nchx, lane, q, [&] {
-#pragma unroll
-            for (int s = NXS; s < NS; ++s) partial_st(s, da0, da1, da2, dpw);
-          });
-        } else {
-          mma16<1>(acc, A, row0 + r, B1, nchx, lane, q);
-        }
-      }
-      acc2_fold(acc);
-      float dz[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) dz[g] = acc[0][0][g] * (1.f - zpre[g] * zpre[g]);
-      const f4 zq = tp_quad(tb, dz, lane);
-      if (row0 < bs)
-        st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
-            (uint32_t)((row0 + trow) * 2 * Hm + 16 * mem + tcol) * 4u, zq, true);
-    }
-    gs.publish();
-    PSTAMP(3);
-    // dh_rec of the own units from step t+1's partials (lane takes column
-    // (mem & 1) * 8 + (r & 7) of subtile NXS + mem / 2 from each producer),
-    // loaded across the P1 -> P2 hand-off.  The producers stored them after
-    // their P2 publish of step t+1; their P0 publish of this step drained them
-    // (vmcnt(0)), and the P1 wait above saw every member's P0 publish.
-    // ---------------- P2: dh -> cell backward -> dG_t -> partials ----------------
-    // cell operands first, then the dh_rec partials: summing those waits for
-    // both in one round trip, before the poll
-    float pg[4][4], pc[4], pcp[4], pdho[4];
-    {
-      const uint32_t eh = (uint32_t)bs * H * 4u;
-      const __amdgpu_buffer_rsrc_t rgs = make_rsrc(a.Gst + (size_t)o * 4 * H, eh * 4u),
-                                   rcs = make_rsrc(a.Cst + (size_t)o * H, GRU ? 0u : eh),
-                                   rcp = make_rsrc((GRU ? a.Hprev : a.Cprev) + (size_t)o * H, eh),
-                                   rdo = make_rsrc(a.DHO + (size_t)o * H, eh);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pg[g][j] = bld(rgs, (b * 4 * H + j * H + unit) * 4u);
-        pc[g] = GRU ? 0.f : bld(rcs, (b * H + unit) * 4u);
-        pcp[g] = bld(rcp, (b * H + unit) * 4u);
-        pdho[g] = bld(rdo, (b * H + unit) * 4u);
-      }
-    }
-    f4 dhr = f4zero();
-    const uint32_t dhb = blk(NXS + (mem >> 1)) + (uint32_t)(q * 16 + (mem & 1) * 8 + (r & 7)) * 16u;
-    if (has_part) sum_partials<M - ND>(prd, dhb + (uint32_t)ND * 1024u, dhr, mem % (M - ND));
-    gs.wait(3u * i + 2);
-    pin(pg[0]), pin(pg[1]), pin(pg[2]), pin(pg[3]), pin(pc), pin(pcp), pin(pdho);
-    PSTAMP(4);
-    f4 dhd[ND > 0 ? ND : 1];
-#pragma unroll
-    for (int p = 0; p < ND; ++p)
-      dhd[p] = has_part ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(prd, dhb + (uint32_t)p * 1024u, 0, 16))
-                        : f4zero();
-    f4 acc[1] = {f4zero()};
-    if (row0 < bs) {
-      const BufKC Az{make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u), (uint32_t)2 * Hm * 4u};
-      wave_mma_x6<1, NZ, 4>(acc, Az, row0 + r, B2, NZ, lane, q, mem % NZ);
-    }
-    if (ND > 0) {  // the deferred producers' partials (issued with the dZ ring's first loads)
-#pragma unroll
-      for (int p = 0; p < ND; ++p) dhr += dhd[p];
-    }
-    PSTAMP(7);
-    float dgh[4][4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dgh[g][j] = 0.f;
-      if (b >= bs) continue;
-      const bool fin = b >= succ_valid;
-      if constexpr (GRU) {
-        // dh_t = dZ W1 + dh_rec + dh_offset + dh_{t+1} z_{t+1} (the carry)
-        const float dh = acc[0][g] + (fin ? 0.f : dhr[g] + carry[g]) + pdho[g];
-        const float r_ = pg[g][0], z_ = pg[g][1], n_ = pg[g][2], ghn = pg[g][3];
-        const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
-        dgh[g][0] = dnp * ghn * r_ * (1.f - r_);
-        dgh[g][1] = dh * (pcp[g] - n_) * z_ * (1.f - z_);
-        dgh[g][2] = dnp;
-        dgh[g][3] = dnp * r_;
-        carry[g] = dh * z_;
-        if (t == 0 && lo) a.DC0[(long)b * H + unit] = dh * z_;
-      } else {
-        const float dh = acc[0][g] + (fin ? 0.f : dhr[g]) + pdho[g];
-        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
-        const float tc = ftanh(pc[g]);
-        const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
-        dgh[g][0] = dc * g_ * i_ * (1.f - i_);
-        dgh[g][1] = dc * pcp[g] * f_ * (1.f - f_);
-        dgh[g][2] = dc * i_ * (1.f - g_ * g_);
-        dgh[g][3] = dh * tc * o_ * (1.f - o_);
-        carry[g] = dc * f_;
-        if (t == 0 && lo) a.DC0[(long)b * H + unit] = dc * f_;
-      }
-    }
-    // partials of this step's dG columns: the dx subtiles (read by the next
-    // step's P0, on the critical path) are drained by this phase's publish;
-    // the dh subtiles (read by the next step's P2, after its P1 wait) go out
-    // after it and are drained by the next P0 publish
-    const bool mk = i + 1 < T && row0 < bs;
-    bf8 a0, a1, a2;
-    if (row0 < bs) {  // dG tile of the wave: rows x [gate j][own unit], read back below for the split and the stash
-      __builtin_amdgcn_wave_barrier();
-      if (lo) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) Ast[(4 * q + g) * DSK_PITCH + 8 * j + r] = dgh[g][j];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (mk) {
-      const float* ar = Ast + r * DSK_PITCH + 8 * q;
-      split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
-    }
-    const __amdgpu_buffer_rsrc_t pw = (i & 1) ? pr1 : pr0;
-    auto partial = [&](int s) { partial_st(s, a0, a1, a2, pw); };
-    if (mk) {
-#pragma unroll
-      for (int s = 0; s < NXS; ++s) partial(s);
-    }
-    gs.publish();
-    PSTAMP(5);
-    if (mk && !defer) {
-#pragma unroll
-      for (int s = NXS; s < NS; ++s) partial(s);
-    }
-    if (defer) {
-      dmk = mk;
-      da0 = a0, da1 = a1, da2 = a2;
-      dpw = pw;
-    }
-    // stash for the weight-gradient GEMMs (plain 16-B stores, after the
-    // publish), straight from the dG tile in LDS: 16 rows x 4 gates x 2 quads
-    // of own units = 2 quads per lane
-    if (row0 < bs) {
-      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.dG + (size_t)o * GH, (uint32_t)bs * GH * 4u);
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-        const int k = lane + 64 * k2, row = k >> 3, gate = (k >> 1) & 3, hf = 4 * (k & 1);
-        const f4 v = *reinterpret_cast<const f4*>(Ast + row * DSK_PITCH + 8 * gate + hf);
-        const uint32_t so = (uint32_t)((row0 + row) * GH + u0 + hf) * 4u;
-        if constexpr (GRU) {  // dGX = (dr, dz, dn), dGH = (dr, dz, dn r)
-          const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.dGH + (size_t)o * GH, (uint32_t)bs * GH * 4u);
-          if (gate < 3) st4(rg, so + (uint32_t)(gate * H) * 4u, v, false);
-          if (gate != 2) st4(rh, so + (uint32_t)((gate == 3 ? 2 : gate) * H) * 4u, v, false);
-        } else {
-          st4(rg, so + (uint32_t)(gate * H) * 4u, v, false);
-        }
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
-// dec_bwd_fold: dec_bwd_sk with the emission-MLP product dZ W1cat folded into
-// the split-K dh partials.
-//
-// In dec_bwd_sk every member gathers the whole 64 x 2Hm dZ tile of its group
-// (128 KiB per member per step) after the P1 -> P2 hand-off and multiplies it
-// by its 8 units' W1cat columns (a 512-deep x6 MMA) -- the largest load and
-// MMA on the step's critical path (P2 6.2 us of 17.9 at c2).
-// dh = dZ W1cat + dG_{t+1} W_hh is linear in both terms, so it splits over
-// the members the way dh_rec already did: in P1 each member, right after its
-// own 16 dZ columns, forms its partial of dh for ALL units,
-//     part_m = dG_{t+1}[:, own 32 gate columns] W_hh[own rows]      (x6, K = 32)
-//            + dZ_t[:, own 16 columns] W1cat[own rows]               (fp32 MFMA, K = 16)
-// and publishes it; P2 sums the M partials of its 8 units (64 KiB per member,
-// as the dh_rec gather did) and runs the cell backward.  The dZ gather and
-// the 512-deep MMA leave P2; dZ is only stashed (plain stores) for the
-// weight-gradient GEMMs.  dx_{t+1} partials are unchanged (P2 -> next P0).
-// LDS: split-K image [NS][3][64] | W1 slice [NHS][64] (fp32 fragments) | P1
-// image [nchx][64] | wave regions: 110 KiB at c2 (dec_bwd_sk: 142).
-// ---------------------------------------------------------------------------
-// (Forming the dG_{t+1} W_hh half at the end of the previous P2 and carrying
-// it in 16 accumulators into P1 measured 3.34 -> 4.24 ms: register pressure.)
-template <int NXS, int NHS, bool GRU = false, bool P0S = true, bool HX = true>
-__global__ __launch_bounds__(256) void dec_bwd_fold(PDecBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) f4 smem[];
-  constexpr int H = NHS * 16, GH = (GRU ? 3 : 4) * H, M = H / 8, NS = NXS + NHS;
-  const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
-  const int nchx = Fp / 16, nFt = Fp / 16;
-  const Role role = assign_role(a.nrt, M);
-  const int grp = role.grp, mem = role.mem;
-  const int rt = grp;
-  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int row0 = rt * PERSIST_ROWS + w * 16;
-  GSync gs{a.sync + grp * PERSIST_SYNC_STRIDE,
-           a.sync + ((size_t)2 * a.nrt + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
-           M, mem, a.flags, 0u};
-  const int u0 = mem * 8, unit = u0 + (r & 7);
-  const bool lo = r < 8;
-  f4* SK = smem;
-  f4* W1I = SK + NS * 3 * 64;
-  f4* B1 = W1I + NHS * 64;
-  float* Ast = reinterpret_cast<float*>(B1 + nchx * 64) + w * DSK_WAVE_FLOATS;
-  float* tb = Ast;  // the same wave-private region, reused for the 16-B store transposes (tp_quad)
-  const int trow = lane >> 2, tcol = 4 * (lane & 3);
-  // split-K image (dec_bwd_sk's): subtile s, lane (rr, qq) holds rows
-  // k = 8qq + 0..7 (gate qq, own units 0..7) of output column 16s + rr
-  for (int e = threadIdx.x; e < NS * 64; e += 256) {
-    const int s = e >> 6, ln = e & 63, rr = ln & 15, qq = ln >> 4;
-    const bool xs = s < NXS;
-    int col = qq * H + u0;
-    if (GRU && qq >= 2) col = (qq == 2) == xs ? 2 * H + u0 : -1;
-    const float* src = (xs ? a.WihT + (long)(16 * s + rr) * GH : a.WhhT + (long)(16 * (s - NXS) + rr) * GH) +
-                       (col < 0 ? 0 : col);
-    bf8 h, m, l;
-    split8(col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src),
-           col < 0 ? f4zero() : *reinterpret_cast<const f4*>(src + 4), h, m, l);
-    SK[(s * 3) * 64 + ln] = __builtin_bit_cast(f4, h);
-    SK[(s * 3 + 1) * 64 + ln] = __builtin_bit_cast(f4, m);
-    SK[(s * 3 + 2) * 64 + ln] = __builtin_bit_cast(f4, l);
-  }
-  // W1 slice: subtile s (units 16s .. 16s + 15), lane (rr, qq): the W1cat
-  // entries of unit 16s + rr at this member's dZ columns 16 mem + 4qq .. + 3
-  for (int e = threadIdx.x; e < NHS * 64; e += 256) {
-    const int s = e >> 6, ln = e & 63, rr = ln & 15, qq = ln >> 4;
-    W1I[e] = *reinterpret_cast<const f4*>(a.W1T + (long)(16 * s + rr) * 2 * Hm + 16 * mem + 4 * qq);
-  }
-  // P1: dZ tile j1 = mem (2Hm/16 == M: checked by the launcher)
-  const bool ismu = mem < Hm / 16;
-  if (ismu) stage_b_frag(B1, a.W2mT, Fp, 1, nchx, [&](int) { return 16 * mem; });
-  else stage_b_frag(B1, a.W2lT, Fp, 1, nchx, [&](int) { return 16 * (mem - Hm / 16); });
-  const float s_em = *a.s_em;
-  __syncthreads();
-  const size_t slot_f = (size_t)a.nrt * NS * 4 * M * 256;  // floats per parity slot
-  const __amdgpu_buffer_rsrc_t pr0 = make_rsrc(a.part, (uint32_t)(slot_f * 4));
-  const __amdgpu_buffer_rsrc_t pr1 = make_rsrc(a.part + slot_f, (uint32_t)(slot_f * 4));
-  // this wave's block of subtile s: (((grp*NS + s)*4 + w)*M + producer)*256 floats
-  auto blk = [&](int s) { return (uint32_t)((((size_t)grp * NS + s) * 4 + w) * M) * 1024u; };
-  // P0 unit of this wave: dx tile jx (16 F columns) of its 16 rows.  P0S: the
-  // (Fp/16 tiles x 4 row blocks) units are dealt over every member's waves
-  // (wave w of member m takes tile (m - nFt w) mod M), so no member gathers
-  // more than two waves' partials; otherwise member m < Fp/16 takes tile m in
-  // all four waves (128 KiB of partials per step on one CU)
-  const int jx = P0S ? ((mem - nFt * w) % M + M) % M : mem;
-  const bool p0 = jx < nFt;
-  float carry[4] = {0.f, 0.f, 0.f, 0.f};
-  bool dgv = false;  // a0..a2: the split dG tile of the previous step (rows < its batch)
-  bf8 a0{}, a1{}, a2{};
-  const int* off = a.off;
-  for (int i = 0; i < T; ++i) {
-    const int t = T - 1 - i;
-    const int o = off[t], bs = off[t + 1] - o;
-    const int succ_valid = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
-    const bool has_part = i > 0 && row0 < succ_valid;  // step t+1's producers covered this wave's rows
-    const __amdgpu_buffer_rsrc_t prd = (i & 1) ? pr0 : pr1;  // step t+1's slot
-    const __amdgpu_buffer_rsrc_t pw = (i & 1) ? pr1 : pr0;   // this step's slot
-    // ---------------- P0: dx_{t+1} tile -> dMU, dLV ----------------
-    const int col0 = 16 * jx + r;
-    float emu[4], elv[4], eox[4], ey[4], emk[4];
-    if (p0) {
-      const uint32_t ef = (uint32_t)bs * Fp * 4u;
-      const __amdgpu_buffer_rsrc_t rmu = make_rsrc(a.MU + (size_t)o * Fp, ef), rlv = make_rsrc(a.LV + (size_t)o * Fp, ef),
-                                   rox = make_rsrc(a.OUT + (size_t)o * Fp, ef),
-                                   ryy = make_rsrc(a.Y + (size_t)o * F, (uint32_t)bs * F * 4u);
-      const __amdgpu_buffer_rsrc_t rmk =
-          make_rsrc(a.xmask ? a.xmask + (size_t)(o + bs) * F : a.Y, a.xmask ? (uint32_t)succ_valid * F * 4u : 0u);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
-        const uint32_t of = col0 < F ? (b * Fp + col0) * 4u : 0x80000000u;
-        const uint32_t oy = col0 < F ? (b * F + col0) * 4u : 0x80000000u;
-        emu[g] = bld(rmu, of);
-        elv[g] = bld(rlv, of);
-        eox[g] = bld(rox, of);
-        ey[g] = bld(ryy, oy);
-        emk[g] = a.xmask ? bld(rmk, oy) : 1.f;
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) emu[g] = elv[g] = eox[g] = ey[g] = 0.f, emk[g] = 1.f;
-    }
-    if (i > 0) gs.wait(3u * i);
-    pin(emu), pin(elv), pin(eox), pin(ey), pin(emk);
-    PSTAMP(0);
-    if (p0) {
-      f4 dx = f4zero();
-      if (NXS > 0 && has_part) sum_partials<M>(prd, blk(jx) + (uint32_t)lane * 16u, dx, mem % M);
-      float dmu[4], dlv[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        dmu[g] = dlv[g] = 0.f;
-        if (col0 < F) {
-          const float dxv = dx[g] * emk[g], mu = emu[g], lv = elv[g];
-          const float iv = __expf(-lv), d = ey[g] - mu;
-          dmu[g] = dxv + s_em * (-d) * iv;
-          dlv[g] = dxv * 0.5f * (eox[g] - mu) + s_em * 0.5f * (1.f - d * d * iv);
-        }
-      }
-      const f4 mq = tp_quad(tb, dmu, lane), lq = tp_quad(tb + TP_FLOATS, dlv, lane);
-      if (row0 < bs) {
-        const uint32_t qo = (uint32_t)((row0 + trow) * Fp + 16 * jx + tcol) * 4u;
-        st4(make_rsrc(a.dMU + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, mq, true);
-        st4(make_rsrc(a.dLV + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), qo, lq, true);
-      }
-    }
-    gs.publish();
-    PSTAMP(1);
-    // HX: the dG_{t+1} W_hh half of this step's dh partials needs nothing of
-    // this step -- formed here, in front of the P1 wait
-    f4 dhp[HX ? NHS : 1];
-    if constexpr (HX) {
-      if (dgv) {
-#pragma unroll
-        for (int s = 0; s < NHS; ++s) {
-          const f4* bp = SK + ((NXS + s) * 3) * 64 + lane;
-          dhp[s] = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
-                          __builtin_bit_cast(bf8, bp[128]));
-        }
-      }
-    }
-    PSTAMP(6);
-    // ---------------- P1: dZ tile -> this member's dh partials ----------------
-    float zpre[4];
-    {
-      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) zpre[g] = bld(rz, ((uint32_t)(row0 + 4 * q + g) * 2 * Hm + 16 * mem + r) * 4u);
-    }
-    gs.wait(3u * i + 1);
-    pin(zpre);
-    PSTAMP(2);
-    if (row0 < bs) {
-      f4 acc[2][1];
-      acc2_zero(acc);
-      const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
-      mma16<1>(acc, A, row0 + r, B1, nchx, lane, q);
-      acc2_fold(acc);
-      float dz[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) dz[g] = acc[0][0][g] * (1.f - zpre[g] * zpre[g]);
-      const f4 zq = tp_quad(tb, dz, lane);
-      // the dZ tile as an A operand: lane (r, q) = row r, columns 4q .. 4q + 3
-      const f4 za = *reinterpret_cast<const f4*>(tb + r * TP_PITCH + 4 * q);
-#pragma unroll
-      for (int s = 0; s < NHS; ++s) {
-        f4 pa = f4zero();
-        if (HX) {
-          if (dgv) pa = dhp[HX ? s : 0];
-        } else if (dgv) {
-          const f4* bp = SK + ((NXS + s) * 3) * 64 + lane;
-          pa = mma_x6(pa, a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
-                      __builtin_bit_cast(bf8, bp[128]));
-        }
-        const f4 wv = W1I[s * 64 + lane];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) pa = mfma4(za[k], wv[k], pa);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, pa), pw,
-                                               blk(NXS + s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
-      }
-      // the dZ stash: read only by the weight-gradient GEMMs after the launch
-      st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
-          (uint32_t)((row0 + trow) * 2 * Hm + 16 * mem + tcol) * 4u, zq, false);
-    }
-    gs.publish();
-    PSTAMP(3);
-    // ---------------- P2: dh -> cell backward -> dG_t -> dx partials ----------------
-    float pg[4][4], pc[4], pcp[4], pdho[4];
-    {
-      const uint32_t eh = (uint32_t)bs * H * 4u;
-      const __amdgpu_buffer_rsrc_t rgs = make_rsrc(a.Gst + (size_t)o * 4 * H, eh * 4u),
-                                   rcs = make_rsrc(a.Cst + (size_t)o * H, GRU ? 0u : eh),
-                                   rcp = make_rsrc((GRU ? a.Hprev : a.Cprev) + (size_t)o * H, eh),
-                                   rdo = make_rsrc(a.DHO + (size_t)o * H, eh);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t b = (uint32_t)(row0 + 4 * q + g);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pg[g][j] = bld(rgs, (b * 4 * H + j * H + unit) * 4u);
-        pc[g] = GRU ? 0.f : bld(rcs, (b * H + unit) * 4u);
-        pcp[g] = bld(rcp, (b * H + unit) * 4u);
-        pdho[g] = bld(rdo, (b * H + unit) * 4u);
-      }
-    }
-    gs.wait(3u * i + 2);
-    pin(pg[0]), pin(pg[1]), pin(pg[2]), pin(pg[3]), pin(pc), pin(pcp), pin(pdho);
-    PSTAMP(4);
-    // dh of the own units: the M members' partials (lane takes column
-    // (mem & 1) * 8 + (r & 7) of subtile NXS + mem / 2)
-    f4 dhr = f4zero();
-    if (row0 < bs)
-      sum_partials<M>(pw, blk(NXS + (mem >> 1)) + (uint32_t)(q * 16 + (mem & 1) * 8 + (r & 7)) * 16u, dhr, mem % M);
-    PSTAMP(7);
-    float dgh[4][4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int b = row0 + 4 * q + g;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dgh[g][j] = 0.f;
-      if (b >= bs) continue;
-      const bool fin = b >= succ_valid;
-      if constexpr (GRU) {
-        // dh_t = dZ W1 + dh_rec + dh_offset + dh_{t+1} z_{t+1} (the carry)
-        const float dh = dhr[g] + (fin ? 0.f : carry[g]) + pdho[g];
-        const float r_ = pg[g][0], z_ = pg[g][1], n_ = pg[g][2], ghn = pg[g][3];
-        const float dnp = dh * (1.f - z_) * (1.f - n_ * n_);
-        dgh[g][0] = dnp * ghn * r_ * (1.f - r_);
-        dgh[g][1] = dh * (pcp[g] - n_) * z_ * (1.f - z_);
-        dgh[g][2] = dnp;
-        dgh[g][3] = dnp * r_;
-        carry[g] = dh * z_;
-        if (t == 0 && lo) a.DC0[(long)b * H + unit] = dh * z_;
-      } else {
-        const float dh = dhr[g] + pdho[g];
-        const float i_ = pg[g][0], f_ = pg[g][1], g_ = pg[g][2], o_ = pg[g][3];
-        const float tc = ftanh(pc[g]);
-        const float dc = (fin ? 0.f : carry[g]) + dh * o_ * (1.f - tc * tc);
-        dgh[g][0] = dc * g_ * i_ * (1.f - i_);
-        dgh[g][1] = dc * pcp[g] * f_ * (1.f - f_);
-        dgh[g][2] = dc * i_ * (1.f - g_ * g_);
-        dgh[g][3] = dh * tc * o_ * (1.f - o_);
-        carry[g] = dc * f_;
-        if (t == 0 && lo) a.DC0[(long)b * H + unit] = dc * f_;
-      }
-    }
-    const bool mk = i + 1 < T && row0 < bs;
-    if (row0 < bs) {  // dG tile of the wave: rows x [gate j][own unit]
-      __builtin_amdgcn_wave_barrier();
-      if (lo) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) Ast[(4 * q + g) * DSK_PITCH + 8 * j + r] = dgh[g][j];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (mk) {  // split once: the dx partials below and the next step's P1 dh partials
-      const float* ar = Ast + r * DSK_PITCH + 8 * q;
-      split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
-    }
-    dgv = mk;
-    if (mk && NXS > 0) {
-#pragma unroll
-      for (int s = 0; s < NXS; ++s) {
-        const f4* bp = SK + (s * 3) * 64 + lane;
-        const f4 v = mma_x6(f4zero(), a0, a1, a2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
-                            __builtin_bit_cast(bf8, bp[128]));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
-                                               blk(s) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
-      }
-    }
-    gs.publish();
-    PSTAMP(5);
-    // stash for the weight-gradient GEMMs (plain 16-B stores after the publish)
-    if (row0 < bs) {
-      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.dG + (size_t)o * GH, (uint32_t)bs * GH * 4u);
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-        const int k = lane + 64 * k2, row = k >> 3, gate = (k >> 1) & 3, hf = 4 * (k & 1);
-        const f4 v = *reinterpret_cast<const f4*>(Ast + row * DSK_PITCH + 8 * gate + hf);
-        const uint32_t so = (uint32_t)((row0 + row) * GH + u0 + hf) * 4u;
-        if constexpr (GRU) {  // dGX = (dr, dz, dn), dGH = (dr, dz, dn r)
-          const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.dGH + (size_t)o * GH, (uint32_t)bs * GH * 4u);
-          if (gate < 3) st4(rg, so + (uint32_t)(gate * H) * 4u, v, false);
-          if (gate != 2) st4(rh, so + (uint32_t)((gate == 3 ? 2 : gate) * H) * 4u, v, false);
-        } else {
-          st4(rg, so + (uint32_t)(gate * H) * 4u, v, false);
-        }
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// dec_bwd_w16 (round 4): dec_bwd_fold's split-K BPTT with HALF the exchange.
+// dec_bwd_w16 (round 4): the split-K decoder BPTT in 32-row groups.
 //
 // Per step a split-K member writes one partial of every output column for
 // every row of its group, so the bytes a step moves chip-wide are
@@ -2171,17 +1605,21 @@ constexpr int W16_ROWS = 32;    // rows per group
 constexpr int W16_M = 16;       // members per group (16 units each)
 constexpr int W16_DTP = 68;     // pitch (floats) of the group's 32 x 64 dG tile in LDS
 constexpr int W16_ZTP = 36;     // pitch of the 32 x 32 dZ tile
-// ZX: the P1 dZ product on waves 0 / 1 only (row block w, both of the
-// member's dZ column tiles, x6 over K = Fp in ceil(Fp / 32) chunks): each
-// row block's dMU / dLV rows are loaded once per member instead of twice;
-// otherwise one (row block, tile) per wave in fp32 MFMA (mma16)
-template <int NXS, bool GRU = false, bool ZX = true>
+// The P1 dZ product runs on waves 0 / 1 only (row block w, both of the
+// member's dZ column tiles, x6 over K = Fp in ceil(Fp / 32) chunks), so each
+// row block's dMU / dLV rows are loaded once per member.
+// GRU: the member's gate columns are dec_fwd_x6's [r | z | n_x | n_h]
+// (dG = [dr, dz, dn, dn r] pre-activation gradients), the split-K images take
+// the n_x column from W_ih only and n_h from W_hh only, the carry is dh z, and
+// the stash is dGX = (dr, dz, dn), dGH = (dr, dz, dn r) with pitch 3H as the
+// per-step kernels write it.
+template <int NXS, bool GRU = false>
 __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   constexpr int H = 256, NHS = 16, GH = (GRU ? 3 : 4) * H, M = W16_M;
   const int Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
-  const int nchx = Fp / 16, nFt = Fp / 16;
-  constexpr int NCZ = (NXS > 0 ? NXS : 9) / 2 + 1;  // ZX: x6 chunks of K = Fp (Fp = 16 NXS with feedback)
+  const int nFt = Fp / 16;
+  constexpr int NCZ = (NXS > 0 ? NXS : 9) / 2 + 1;  // x6 chunks of K = Fp (Fp = 16 NXS with feedback)
   const int ncz = (Fp + 31) / 32;
   const int ng = a.nrt;  // 32-row groups (the launcher's count)
   const Role role = assign_role(ng, M);
@@ -2193,12 +1631,12 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
            a.sync + ((size_t)2 * ng + PERSIST_REG_LINES + (size_t)grp * PERSIST_FLAG_LINES) * PERSIST_SYNC_STRIDE,
            M, mem, a.flags, 0u};
   const int u0 = mem * 16;
-  // LDS: dx image [NXS][2][3][64] | fold image [NHS][3][64] | P1 W2 fragments [2][nchx][64]
+  // LDS: dx image [NXS][2][3][64] | fold image [NHS][3][64] | P1 W2 image [2][ncz][3][64]
   //      | dG tile [32][68] | dZ tile [32][36] | dh half-sums [2][64] | wave transposes [4][2 TP]
   f4* DXI = smem;
   f4* W1X = DXI + NXS * 2 * 3 * 64;
   f4* B1 = W1X + NHS * 3 * 64;
-  float* DT = reinterpret_cast<float*>(B1 + (ZX ? 2 * ncz * 3 * 64 : 2 * nchx * 64));
+  float* DT = reinterpret_cast<float*>(B1 + 2 * ncz * 3 * 64);
   float* ZT = DT + W16_ROWS * W16_DTP;
   f4* DHX = reinterpret_cast<f4*>(ZT + W16_ROWS * W16_ZTP);
   float* tb = reinterpret_cast<float*>(DHX + 2 * 64) + w * 2 * TP_FLOATS;
@@ -2236,12 +1674,8 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
   }
   // P1 dZ column tiles 2 mem, 2 mem + 1 (mu tiles for mem < Hm / 32, else lv)
   const bool ismu = 2 * mem < Hm / 16;
-  if (ZX)
-    stage_x6(B1, ismu ? a.W2mT : a.W2lT, Fp, Fp, 2, ncz, 0, ncz,
-             [&](int j, int rr) { return 16 * (2 * mem + j) - (ismu ? 0 : Hm) + rr; });
-  else
-    stage_b_frag(B1, ismu ? a.W2mT : a.W2lT, Fp, 2, nchx,
-                 [&](int j) { return 16 * (2 * mem + j) - (ismu ? 0 : Hm); });
+  stage_x6(B1, ismu ? a.W2mT : a.W2lT, Fp, Fp, 2, ncz, 0, ncz,
+           [&](int j, int rr) { return 16 * (2 * mem + j) - (ismu ? 0 : Hm) + rr; });
   // this wave's quarter of the W_hh image (units 64w .. 64w + 63), resident in registers
   bf8 Bh[4][2][3];
 #pragma unroll
@@ -2269,8 +1703,6 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
   const int prb = p0 ? pk / nFt : 0, jx = p0 ? pk % nFt : 0;
   const int prow0 = rowg + 16 * prb;
   // P1 dZ unit of this wave: row block w >> 1, column tile 2 mem + (w & 1)
-  const int zrb = w >> 1, zj = w & 1;
-  const int zrow0 = rowg + 16 * zrb;
   // P2: dh half-sum of row block w & 1 over producers 8 (w >> 1) .. + 7; waves 0 / 1 run the cell
   const int crb = w & 1;
   const int crow0 = rowg + 16 * crb;
@@ -2360,60 +1792,38 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
     PSTAMP(6);
 #endif
     // ---------------- P1: dZ tile -> this member's dh partials ----------------
-    float zpre[2][4];  // ZX: the activations of both tiles of row block w (waves 0 / 1)
+    float zpre[2][4];  // the activations of both tiles of row block w (waves 0 / 1)
     {
-      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (ZX && w >= 2) ? 0u : (uint32_t)bs * 2 * Hm * 4u);
-      const int zr0 = ZX ? rowg + 16 * w : zrow0;
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, w >= 2 ? 0u : (uint32_t)bs * 2 * Hm * 4u);
+      const int zr0 = rowg + 16 * w;
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          zpre[jj][g] = (ZX || jj == 0) ? bld(rz, ((uint32_t)(zr0 + 4 * q + g) * 2 * Hm + 32 * mem + 16 * (ZX ? jj : zj) + r) * 4u)
-                                        : 0.f;
+          zpre[jj][g] = bld(rz, ((uint32_t)(zr0 + 4 * q + g) * 2 * Hm + 32 * mem + 16 * jj + r) * 4u);
     }
     gs.wait(3u * i + 1);
     pin(zpre[0]), pin(zpre[1]);
     PSTAMP(2);
-    if (ZX) {
-      if (w < 2) {
-        const int zr0 = rowg + 16 * w;
-        f4 acc[2] = {f4zero(), f4zero()};
-        if (zr0 < bs) {
-          const __amdgpu_buffer_rsrc_t ra = make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u);
-          const BufKC2x A{ra, ra, (uint32_t)Fp * 4u, (uint32_t)Fp * 4u, ncz, Fp};  // k >= Fp reads 0
-          wave_mma_x6<2, NCZ, 4>(acc, A, zr0 + r, B1, ncz, lane, q);
-        }
-        const __amdgpu_buffer_rsrc_t rzs = make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          float dz[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) dz[g] = acc[jj][g] * (1.f - zpre[jj][g] * zpre[jj][g]);
-#pragma unroll
-          for (int g = 0; g < 4; ++g) ZT[(16 * w + 4 * q + g) * W16_ZTP + 16 * jj + r] = dz[g];
-          const f4 zq = tp_quad(tb, dz, lane);
-          if (zr0 < bs) st4(rzs, (uint32_t)((zr0 + trow) * 2 * Hm + 32 * mem + 16 * jj + tcol) * 4u, zq, false);
-        }
+    if (w < 2) {
+      const int zr0 = rowg + 16 * w;
+      f4 acc[2] = {f4zero(), f4zero()};
+      if (zr0 < bs) {
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u);
+        const BufKC2x A{ra, ra, (uint32_t)Fp * 4u, (uint32_t)Fp * 4u, ncz, Fp};  // k >= Fp reads 0
+        wave_mma_x6<2, NCZ, 4>(acc, A, zr0 + r, B1, ncz, lane, q);
       }
-    } else {
-      float (&zp)[4] = zpre[0];
-      f4 acc[2][1];
-      acc2_zero(acc);
-      if (zrow0 < bs) {
-        const BufKC A{make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u), (uint32_t)Fp * 4u};
-        mma16<1>(acc, A, zrow0 + r, B1 + zj * nchx * 64, nchx, lane, q);
+      const __amdgpu_buffer_rsrc_t rzs = make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        float dz[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dz[g] = acc[jj][g] * (1.f - zpre[jj][g] * zpre[jj][g]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) ZT[(16 * w + 4 * q + g) * W16_ZTP + 16 * jj + r] = dz[g];
+        const f4 zq = tp_quad(tb, dz, lane);
+        if (zr0 < bs) st4(rzs, (uint32_t)((zr0 + trow) * 2 * Hm + 32 * mem + 16 * jj + tcol) * 4u, zq, false);
       }
-      acc2_fold(acc);
-      float dz[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) dz[g] = acc[0][0][g] * (1.f - zp[g] * zp[g]);
-      // the dZ tile for the fold (rows 16 zrb + .., columns 16 zj + r) and the stash
-#pragma unroll
-      for (int g = 0; g < 4; ++g) ZT[(16 * zrb + 4 * q + g) * W16_ZTP + 16 * zj + r] = dz[g];
-      const f4 zq = tp_quad(tb, dz, lane);
-      if (zrow0 < bs)
-        st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
-            (uint32_t)((zrow0 + trow) * 2 * Hm + 32 * mem + 16 * zj + tcol) * 4u, zq, false);
     }
 #ifdef ABCD_STAMP_DIAG
     PSTAMP(6);  // diagnostics build: dZ tile done (before the barrier)
@@ -3025,21 +2435,21 @@ static int launch_fwd(hipStream_t s, const PFwdArgs& a, bool* launched) {
   *launched = true;
   return 0;
 }
-template <int G, int PD, int X6>
+template <int G, int PD>
 static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   const int grid = a.nd * a.nrt * (a.H / 16);
-  const size_t lds = (size_t)16 * G * a.H * (X6 ? 6 : 4);
+  const size_t lds = (size_t)16 * G * a.H * 4;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(enc_bwd_persist<G, PD, X6>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(enc_bwd_persist<G, PD>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
   PBwdArgs b = a;
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_ENC_BWD);
-    enc_bwd_persist<G, PD, X6><<<grid, 256, lds, s>>>(b);
+    enc_bwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_ENC_BWD, "enc_bwd_persist<%d,%d,%d> grid %d", G, PD, X6, grid);
+  note_dispatch(TK_ENC_BWD, "enc_bwd_persist<%d,%d> grid %d", G, PD, grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -3088,14 +2498,10 @@ static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
 }
 
 
-// enc_bwd_w8 by default (32-row groups of 8 members: half the split-K
-// exchange): same-box A/B at c2 against enc_bwd_sk, enc_bwd 1.90 / 1.89 ->
-// 1.60 / 1.59 ms per launch, step 9.51 / 9.53 -> 9.26 / 9.23 ms; c5gru 5.10 /
-// 5.21 -> 3.98 / 4.02 ms.  ABCD_ENCBWD=sk: enc_bwd_sk (A/B timing)
-static bool enc_bwd_w8_on() {
-  const char* v = getenv("ABCD_ENCBWD");
-  return !(v && v[0] == 's');
-}
+// enc_bwd_w8 at H = 256 (32-row groups of 8 members: half the split-K
+// exchange of the 64-row enc_bwd_sk<G, 16>, which it replaced): same-box A/B
+// at c2, enc_bwd 1.90 / 1.89 -> 1.60 / 1.59 ms per launch, step 9.51 / 9.53 ->
+// 9.26 / 9.23 ms; c5gru 5.10 / 5.21 -> 3.98 / 4.02 ms
 template <int G>
 static int launch_bwd_w8(hipStream_t s, const PBwdArgs& a, bool* launched) {
   const int nrt = cdiv(a.B, W8_ROWS);
@@ -3123,39 +2529,23 @@ static int launch_bwd_w8(hipStream_t s, const PBwdArgs& a, bool* launched) {
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled()) return 0;
-  if (a.H == 256 && a.part && enc_bwd_w8_on()) {
+  if (a.part && a.H == 256) {
     const int rc = G == 4 ? launch_bwd_w8<4>(s, a, launched) : launch_bwd_w8<3>(s, a, launched);
     if (rc || *launched) return rc;
+  } else if (a.part && (a.H == 64 || a.H == 128)) {  // split-K in 64-row groups of H / 16 members
+    if (G == 4) return a.H == 64 ? launch_bwd_sk<4, 4>(s, a, launched) : launch_bwd_sk<4, 8>(s, a, launched);
+    return a.H == 64 ? launch_bwd_sk<3, 4>(s, a, launched) : launch_bwd_sk<3, 8>(s, a, launched);
   }
-  if (x6_enabled(a.H) && a.part) {
-    if (G == 4) {
-      if (a.H == 64) return launch_bwd_sk<4, 4>(s, a, launched);
-      if (a.H == 128) return launch_bwd_sk<4, 8>(s, a, launched);
-      return launch_bwd_sk<4, 16>(s, a, launched);
-    }
-    if (a.H == 64) return launch_bwd_sk<3, 4>(s, a, launched);
-    if (a.H == 128) return launch_bwd_sk<3, 8>(s, a, launched);
-    return launch_bwd_sk<3, 16>(s, a, launched);
-  }
-  if (x6_enabled(a.H)) {
-    if (G == 4) {
-      if (a.H == 64) return launch_bwd<4, 16, 8>(s, a, launched);
-      if (a.H == 128) return launch_bwd<4, 16, 16>(s, a, launched);
-      return launch_bwd<4, 16, 32>(s, a, launched);
-    }
-    if (a.H == 64) return launch_bwd<3, 16, 6>(s, a, launched);
-    if (a.H == 128) return launch_bwd<3, 16, 12>(s, a, launched);
-    return launch_bwd<3, 16, 24>(s, a, launched);
-  }
+  if (x6_enabled(a.H)) return 0;  // H = 256 that enc_bwd_w8 cannot hold resident: the per-step kernels
   const int pd = ring_depth(G * a.H / 16);
   if (G == 4) {
-    if (pd == 16) return launch_bwd<4, 16, 0>(s, a, launched);
-    if (pd == 4) return launch_bwd<4, 4, 0>(s, a, launched);
-    return launch_bwd<4, 1, 0>(s, a, launched);
+    if (pd == 16) return launch_bwd<4, 16>(s, a, launched);
+    if (pd == 4) return launch_bwd<4, 4>(s, a, launched);
+    return launch_bwd<4, 1>(s, a, launched);
   }
-  if (pd == 16) return launch_bwd<3, 16, 0>(s, a, launched);
-  if (pd == 4) return launch_bwd<3, 4, 0>(s, a, launched);
-  return launch_bwd<3, 1, 0>(s, a, launched);
+  if (pd == 16) return launch_bwd<3, 16>(s, a, launched);
+  if (pd == 4) return launch_bwd<3, 4>(s, a, launched);
+  return launch_bwd<3, 1>(s, a, launched);
 }
 
 
@@ -3183,32 +2573,50 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32, bool GRU, bool HPRE>
+template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, bool DF>
 static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
-  const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
+  const size_t lds =
+      (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + (DF ? 2 : 1) * 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, DF>, grid, lds, &ok));
   if (!ok) return 0;
+  if (DF) {  // every word the launch hands off starts as HANDOFF_EMPTY
+    if (a.L <= 0 || a.B <= 0 || a.B > a.L) return (int)hipErrorInvalidValue;
+    FillRanges fr{};
+    fr.p[0] = a.Hs; fr.n4[0] = (long)a.L * a.H / 4;
+    fr.p[1] = a.Aact; fr.n4[1] = (long)a.L * 2 * a.Hm / 4;
+    if (a.feedback) { fr.p[2] = a.Xin + (size_t)a.B * a.Fp; fr.n4[2] = (long)(a.L - a.B) * a.Fp / 4; }
+    const long n4 = fr.n4[0] + fr.n4[1] + fr.n4[2];
+    handoff_fill<<<(int)std::min<long>(2048, std::max<long>(1, n4 / 1024)), 256, 0, s>>>(fr);
+    ABCD_TRY(hipGetLastError());
+  }
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
+    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, DF><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM", grid);
+  note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM",
+                DF ? ",DF" : "", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
 }
 
-
+// the data-as-flag hand-offs by default; ABCD_DECFWD_DF=0 keeps the
+// per-member flag form (same-box A/B)
+static bool dec_fwd_df_on() {
+  const char* v = getenv("ABCD_DECFWD_DF");
+  return !(v && v[0] == '0');
+}
 template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
-  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true>(s, a, launched);
+  if (dec_fwd_df_on()) return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, true>(s, a, launched);
+  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, false>(s, a, launched);
 }
 
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {
@@ -3240,87 +2648,19 @@ int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launch
 }
 
 
-template <int NXS, int NHS, int NZ, bool GRU = false>
-static int launch_dec_bwd_sk(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
-  constexpr int NS = NXS + NHS, M = NHS * 2;
-  const size_t lds = (size_t)(NS + NZ) * 3 * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * DSK_WAVE_FLOATS * 4;
-  const int grid = a.nrt * M;
-  bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_sk<NXS, NHS, NZ, GRU>, grid, lds, &ok));
-  if (!ok) return 0;
-  ABCD_TRY(zero_sync(s, a.sync, a.nrt));
-  PDecBwdArgs b = a;
-  b.flags = 1;  // per-member flags (the group-counter form measured slower)
-  b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
-  {
-    TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_sk<NXS, NHS, NZ, GRU><<<grid, 256, lds, s>>>(b);
-  }
-  note_dispatch(TK_DEC_BWD, "dec_bwd_sk<%d,%d,%d,%s> grid %d", NXS, NHS, NZ, GRU ? "GRU" : "LSTM", grid);
-  ABCD_CHECK_LAUNCH();
-  *launched = true;
-  return 0;
-}
-
-template <int NXS, int NHS, bool GRU, bool P0S, bool HX>
-static int launch_dec_bwd_fold_k(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
-  constexpr int NS = NXS + NHS, M = NHS * 2;
-  const size_t lds = (size_t)(NS * 3 + NHS) * 64 * 16 + (size_t)(a.Fp / 16) * 64 * 16 + (size_t)4 * DSK_WAVE_FLOATS * 4;
-  const int grid = a.nrt * M;
-  bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_fold<NXS, NHS, GRU, P0S, HX>, grid, lds, &ok));
-  if (!ok) return 0;
-  ABCD_TRY(zero_sync(s, a.sync, a.nrt));
-  PDecBwdArgs b = a;
-  b.flags = 1;
-  b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
-  {
-    TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_fold<NXS, NHS, GRU, P0S, HX><<<grid, 256, lds, s>>>(b);
-  }
-  note_dispatch(TK_DEC_BWD, "dec_bwd_fold<%d,%d,%s> grid %d", NXS, NHS, GRU ? "GRU" : "LSTM", grid);
-  ABCD_CHECK_LAUNCH();
-  *launched = true;
-  return 0;
-}
-// By default the P0 units are dealt over every member (same-box A/B at c2:
-// dec_bwd 3.35 / 3.34 -> 3.28 / 3.29 ms) and the x6 half of the P1 partials
-// runs in front of the P1 wait (3.29 / 3.29 -> 3.08 / 3.06 ms, step 10.47 ->
-// 10.27 ms).  ABCD_P0S=0 / ABCD_HX=0 restore either (A/B timing).
-template <int NXS, int NHS, bool GRU = false>
-static int launch_dec_bwd_fold(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
-  const char* v = getenv("ABCD_P0S");
-  const char* x = getenv("ABCD_HX");
-  const bool p0s = !(v && v[0] == '0'), hx = !(x && x[0] == '0');
-  if (!p0s) return launch_dec_bwd_fold_k<NXS, NHS, GRU, false, false>(s, a, launched);
-  if (hx) return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, true>(s, a, launched);
-  return launch_dec_bwd_fold_k<NXS, NHS, GRU, true, false>(s, a, launched);
-}
-// dec_bwd_fold by default: same-box A/B at c2, 3.70 / 3.72 -> 3.34 / 3.33 ms
-// per launch, step 10.85 -> 10.50 ms; ABCD_DECBWD=sk: dec_bwd_sk (A/B timing)
-static bool dec_bwd_folded() {
-  const char* v = getenv("ABCD_DECBWD");
-  return !(v && v[0] == 's');
-}
-// dec_bwd_w16 by default (32-row groups of 16 members: half the split-K
-// exchange): same-box A/B at c2 against dec_bwd_fold, dec_bwd 3.08 / 3.06 ->
-// 2.55 / 2.55 ms per launch, step 9.99 / 9.99 -> 9.49 / 9.47 ms.
-// ABCD_DECBWD=f: dec_bwd_fold, =sk: dec_bwd_sk (A/B timing)
-static bool dec_bwd_w16_on() {
-  const char* v = getenv("ABCD_DECBWD");
-  return !(v && (v[0] == 'f' || v[0] == 's'));
-}
-template <int NXS, bool GRU, bool ZX>
-static int launch_dec_bwd_w16_k(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
+// dec_bwd_w16 (32-row groups of 16 members: half the split-K exchange of the
+// 64-row dec_bwd_fold it replaced): same-box A/B at c2, dec_bwd 3.08 / 3.06 ->
+// 2.55 / 2.55 ms per launch, step 9.99 / 9.99 -> 9.49 / 9.47 ms
+template <int NXS, bool GRU>
+static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
   const int ng = cdiv(a.B, W16_ROWS), nchx = a.Fp / 16, ncz = (a.Fp + 31) / 32;
-  const size_t b1 = ZX ? (size_t)2 * ncz * 3 * 64 * 16 : (size_t)2 * nchx * 64 * 16;
-  const size_t lds = (size_t)NXS * 2 * 3 * 64 * 16 + (size_t)16 * 3 * 64 * 16 + b1 +
+  const size_t lds = (size_t)NXS * 2 * 3 * 64 * 16 + (size_t)16 * 3 * 64 * 16 + (size_t)2 * ncz * 3 * 64 * 16 +
                      (size_t)W16_ROWS * (W16_DTP + W16_ZTP) * 4 + (size_t)2 * 64 * 16 + (size_t)4 * 2 * TP_FLOATS * 4;
   const int grid = ng * W16_M;
   if (a.B <= 0 || 2 * nchx > 4 * W16_M) return 0;
-  if (ZX && ncz != (NXS > 0 ? NXS : 9) / 2 + 1) return 0;  // the kernel's compile-time chunk count
+  if (ncz != (NXS > 0 ? NXS : 9) / 2 + 1) return 0;  // the kernel's compile-time chunk count
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_bwd_w16<NXS, GRU, ZX>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_bwd_w16<NXS, GRU>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, ng));
   PDecBwdArgs b = a;
@@ -3329,67 +2669,28 @@ static int launch_dec_bwd_w16_k(hipStream_t s, const PDecBwdArgs& a, bool* launc
   b.prof = (g_prof_mask & 8) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_BWD);
-    dec_bwd_w16<NXS, GRU, ZX><<<grid, 256, lds, s>>>(b);
+    dec_bwd_w16<NXS, GRU><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_DEC_BWD, "dec_bwd_w16<%d,%s> grid %d", NXS, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
 }
-// ABCD_W16Z=0: the P1 dZ tiles on all four waves in fp32 MFMA (A/B timing)
-template <int NXS, bool GRU>
-static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launched) {
-  const char* v = getenv("ABCD_W16Z");
-  if (v && v[0] == '0') return launch_dec_bwd_w16_k<NXS, GRU, false>(s, a, launched);
-  const int rc = launch_dec_bwd_w16_k<NXS, GRU, true>(s, a, launched);
-  if (rc || *launched) return rc;
-  return launch_dec_bwd_w16_k<NXS, GRU, false>(s, a, launched);
-}
-
 
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {
   *launched = false;
   if (!persist_enabled() || a.H % 8) return 0;
-  if (G == 3) {  // GRU: the split-K form only
-    if (!(a.part && a.Hprev && a.dGH && x6_enabled(a.H) && a.H == 256 && a.Hm == a.H &&
-          a.Fp / 16 <= a.H / 8))
-      return 0;
+  // the split-K form: H = Hm = 256, Fp / 16 <= 16 (the GRU has no other persistent form)
+  if (a.part && x6_enabled(a.H) && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8 &&
+      (G == 4 || (a.Hprev && a.dGH))) {
     const int nxs = a.feedback ? a.Fp / 16 : 0;
-    if (dec_bwd_w16_on()) {
-      if (nxs == 9) return launch_dec_bwd_w16<9, true>(s, a, launched);
-      if (nxs == 5) return launch_dec_bwd_w16<5, true>(s, a, launched);
-      if (nxs == 0) return launch_dec_bwd_w16<0, true>(s, a, launched);
-    }
-    if (dec_bwd_folded()) {
-      if (nxs == 9) return launch_dec_bwd_fold<9, 16, true>(s, a, launched);
-      if (nxs == 5) return launch_dec_bwd_fold<5, 16, true>(s, a, launched);
-      if (nxs == 0) return launch_dec_bwd_fold<0, 16, true>(s, a, launched);
-      return 0;
-    }
-    if (nxs == 9) return launch_dec_bwd_sk<9, 16, 16, true>(s, a, launched);
-    if (nxs == 5) return launch_dec_bwd_sk<5, 16, 16, true>(s, a, launched);
-    if (nxs == 0) return launch_dec_bwd_sk<0, 16, 16, true>(s, a, launched);
-    return 0;
+    int rc = 0;
+    if (nxs == 9) rc = G == 4 ? launch_dec_bwd_w16<9, false>(s, a, launched) : launch_dec_bwd_w16<9, true>(s, a, launched);
+    else if (nxs == 5) rc = G == 4 ? launch_dec_bwd_w16<5, false>(s, a, launched) : launch_dec_bwd_w16<5, true>(s, a, launched);
+    else if (nxs == 0) rc = G == 4 ? launch_dec_bwd_w16<0, false>(s, a, launched) : launch_dec_bwd_w16<0, true>(s, a, launched);
+    if (rc || *launched) return rc;
   }
-  if (G != 4) return 0;
-  // split-K form: H = 256 (32 members), 2Hm/16 == members, Fp/16 <= members
-  if (a.part && x6_enabled(a.H) && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8) {
-    const int nxs = a.feedback ? a.Fp / 16 : 0;
-    if (dec_bwd_w16_on()) {
-      if (nxs == 9) return launch_dec_bwd_w16<9, false>(s, a, launched);
-      if (nxs == 5) return launch_dec_bwd_w16<5, false>(s, a, launched);
-      if (nxs == 0) return launch_dec_bwd_w16<0, false>(s, a, launched);
-    }
-    if (dec_bwd_folded()) {
-      if (nxs == 9) return launch_dec_bwd_fold<9, 16>(s, a, launched);
-      if (nxs == 5) return launch_dec_bwd_fold<5, 16>(s, a, launched);
-      if (nxs == 0) return launch_dec_bwd_fold<0, 16>(s, a, launched);
-    } else {
-      if (nxs == 9) return launch_dec_bwd_sk<9, 16, 16>(s, a, launched);
-      if (nxs == 5) return launch_dec_bwd_sk<5, 16, 16>(s, a, launched);
-      if (nxs == 0) return launch_dec_bwd_sk<0, 16, 16>(s, a, launched);
-    }
-  }
+  if (G != 4) return 0;  // GRU: the per-step kernels
   const int M = a.H / 8, nchg = 4 * a.H / 16, nchx = a.Fp / 16, nchz = 2 * a.Hm / 16;
   const int n0 = cdiv(a.Fp / 16 + a.H / 16, M), n1 = cdiv(2 * a.Hm / 16, M);
   const size_t lds = (size_t)64 * 16 * (n0 * nchg + n1 * nchx + nchz);
@@ -3413,10 +2714,10 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
 
 }  // namespace abcd
 
-// diagnostics only (not in the public header): which XCD (HW_REG_XCC_ID) and
+// diagnostics (abcd_hip.h: abcd_debug_xcc_map): which XCD (HW_REG_XCC_ID) and
 // which CU (HW_REG_HW_ID) each workgroup of a one-per-CU grid runs on, the
 // placement the persistent kernels' group_role assumes (blocks b and b + 8
-// share an XCD)
+// share an XCD); out holds 2 u32 per block
 namespace abcd {
 __global__ __launch_bounds__(256) void xcc_map_kernel(unsigned* out) {
   extern __shared__ float pad_lds[];
@@ -3439,8 +2740,8 @@ extern "C" int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream) {
   return (int)hipGetLastError();
 }
 
-// diagnostics only (not in the public header): stamp buffer for the
-// persistent kernels selected by mask, grid x T x 5 u64, or null to disable
+// diagnostics (abcd_hip.h: abcd_debug_persist_prof): stamp buffer for the
+// persistent kernels selected by mask, grid x T x 8 u64, or null to disable
 extern "C" void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask) {
   abcd::g_prof = dev_buf;
   abcd::g_prof_mask = mask;

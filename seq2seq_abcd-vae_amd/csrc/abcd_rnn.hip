@@ -1169,7 +1169,7 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
   bool done = false;
   {
     PDecFwdArgs pa{};
-    pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS);
+    pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS); pa.L = L; pa.B = B;
     pa.feedback = c->feedback;
     pa.off = w.off; pa.sync = w.sync;
     pa.Wih = w.Wihp; pa.Whh = cw.w_hh; pa.bias = G == 4 ? w.bcomb : w.bgru;

@@ -132,8 +132,33 @@ DEV void stage_x6(f4* dst, const float* W, long ldw, int kvalid, int nsub, int n
 // Bl: the chunk-major x6
 // image with `nch` chunks per subtile (nch >= NCH; a segment of a wider image
 // starts at Bl + c0 * 3 * 64).
-template <int NR, int NCH, int PD, class OA>
-DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q, int rot = 0) {
+// Chk: the operand as its own hand-off flag (abcd_persist.hip's PollEmpty):
+// before a chunk is split, chk.empty() tells whether any of its words has not
+// arrived yet; if so the chunk AND the rest of the ring are re-read (one round
+// trip for the ring instead of one per chunk) until it has, chk.spin()
+// bounding the wait.  NoChk: plain operands.
+struct NoChk {
+  static constexpr bool on = false;
+  DEV bool empty(const f4&, const f4&) const { return false; }
+  DEV unsigned limit() const { return 0; }
+  DEV bool spin(unsigned&, unsigned) const { return false; }
+};
+#define X6_POLL_CHUNK(c, p)                                                                    \
+  if constexpr (Chk::on) {                                                                     \
+    if (__builtin_amdgcn_ballot_w64(chk.empty(ra[p], rb[p]))) {                                \
+      unsigned spins = 0;                                                                      \
+      const unsigned lim = chk.limit();                                                        \
+      do {                                                                                     \
+        if (!chk.spin(spins, lim)) break;                                                      \
+        asm volatile("" ::: "memory"); /* the re-reads are new loads (never hoisted) */        \
+        _Pragma("unroll") for (int d = 0; d < P; ++d) if (c + d < NCH)                         \
+            A.frag8(arow, cc(c + d), q, ra[(c + d) % P], rb[(c + d) % P]);                     \
+      } while (__builtin_amdgcn_ballot_w64(chk.empty(ra[p], rb[p])));                          \
+    }                                                                                          \
+  }
+template <int NR, int NCH, int PD, class OA, class Chk = NoChk>
+DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q, int rot = 0,
+                     Chk chk = Chk()) {
   constexpr int P = PD < NCH ? PD : NCH;
   // chunk order rotated by `rot` (wave-uniform, < NCH): consumers of one
   // hand-off tile start on different lines instead of all on chunk 0.  The
@@ -165,6 +190,7 @@ DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch
         for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bl[((j * nch + cc(c + 1)) * 3 + pl) * 64 + lane];
     }
     bf8 a0, a1, a2;
+    X6_POLL_CHUNK(c, p)
     split8(ra[p], rb[p], a0, a1, a2);
     if (c + P < NCH) A.frag8(arow, cc(c + P), q, ra[p], rb[p]);
     __builtin_amdgcn_sched_barrier(0);
@@ -184,9 +210,9 @@ DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch
 
 // wave_mma_x6 with one image segment per output tile: chunk c of tile j at
 // Bp[j] + c * 3 * 64 (tiles from different LDS images sharing one A operand)
-template <int NR, int NCH, int PD, class OA>
+template <int NR, int NCH, int PD, class OA, class Chk = NoChk>
 DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp)[NR], int lane, int q,
-                      int rot = 0) {
+                      int rot = 0, Chk chk = Chk()) {
   constexpr int P = PD < NCH ? PD : NCH;
   auto cc = [&](int c) { const int x = c + rot; return x >= NCH ? x - NCH : x; };
   f4 ra[P], rb[P];
@@ -209,6 +235,7 @@ DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp
         for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bp[j][(cc(c + 1) * 3 + pl) * 64 + lane];
     }
     bf8 a0, a1, a2;
+    X6_POLL_CHUNK(c, p)
     split8(ra[p], rb[p], a0, a1, a2);
     if (c + P < NCH) A.frag8(arow, cc(c + P), q, ra[p], rb[p]);
     __builtin_amdgcn_sched_barrier(0);

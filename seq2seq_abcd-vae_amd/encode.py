@@ -67,7 +67,11 @@ class Encoder(learning.Learner):
         per batch, encode.py:38-55)."""
         output = output or OUTPUT
         var_name, value_name = COLUMNS[output]
-        rename_existing_file(save_path)
+        # the table is written to a temporary path and takes save_path (the
+        # earlier output kept as .prev) only once every batch is written and
+        # the device status is clean: a timed-out persistent launch or an error
+        # part way leaves no invalid or partial table behind
+        tmp_path = save_path + ".partial"
         ann = None
         if "label" in dataset.df_annotation.columns:
             ann = dataset.df_annotation.drop(columns=["onset_ix", "offset_ix", "length"])
@@ -82,22 +86,30 @@ class Encoder(learning.Learner):
             if ann is not None:
                 extra = ann.reindex(table["data_ix"].to_numpy()).reset_index(drop=True)
                 table = pd.concat([table, extra], axis=1)
-            table.to_csv(save_path, index=False, mode="w" if state["header"] else "a", header=state["header"])
+            table.to_csv(tmp_path, index=False, mode="w" if state["header"] else "a", header=state["header"])
             state["header"] = False
 
-        pending = None
-        for packed, _, _, ix in data_utils.DataLoader(dataset, batch_size=batch_size):
-            vals = self._device_output(packed, output)
-            host = torch.empty(vals.shape, dtype=vals.dtype, pin_memory=True)
-            host.copy_(vals, non_blocking=True)
-            event = torch.cuda.Event()
-            event.record()
+        try:
+            pending = None
+            for packed, _, _, ix in data_utils.DataLoader(dataset, batch_size=batch_size):
+                vals = self._device_output(packed, output)
+                host = torch.empty(vals.shape, dtype=vals.dtype, pin_memory=True)
+                host.copy_(vals, non_blocking=True)
+                event = torch.cuda.Event()
+                event.record()
+                if pending is not None:
+                    write(*pending)
+                pending = (host, event, np.asarray(ix, dtype=np.int64))
             if pending is not None:
                 write(*pending)
-            pending = (host, event, np.asarray(ix, dtype=np.int64))
-        if pending is not None:
-            write(*pending)
-        _native.op_status.sync("encode_dataset")  # a timed-out persistent launch fails the run, not the table
+            _native.op_status.sync("encode_dataset")  # a timed-out persistent launch fails the run, not the table
+        except BaseException:
+            if os.path.isfile(tmp_path):
+                os.remove(tmp_path)
+            raise
+        if os.path.isfile(tmp_path):  # (an empty dataset writes no table, as the reference)
+            rename_existing_file(save_path)
+            os.replace(tmp_path, save_path)
 
 
 def rename_existing_file(filepath):

@@ -232,7 +232,13 @@ class _OpStatus:
     (abcd_step_status) and copied without blocking into pinned host memory;
     the next probe reads the previous copy once its event has completed and
     raises PersistTimeout on a non-zero value.  sync() is the blocking form
-    for the end of a batch of work (encode.py)."""
+    for the end of a batch of work (encode.py).
+
+    A probe folds (and so clears) the device's per-launch timeout word, which
+    FusedStep's STATUS slot also folds: use the op surface's probes and
+    FusedStep in separate processes (the trainer uses FusedStep only, the
+    encode CLIs the op surface only), or a timeout may be reported by one of
+    them only."""
 
     def __init__(self):
         self.host = None
@@ -247,7 +253,11 @@ class _OpStatus:
         raise_on_status(float(self.host[0]), self.where)
 
     def probe(self, device, where):
-        self._read(False)
+        try:
+            self._read(False)
+        except PersistTimeout:
+            lib().abcd_device_status()  # reported once: clear the sticky word as sync() does
+            raise
         if self.event is not None:  # the previous copy is still in flight; the word keeps any new timeout
             return
         if self.host is None:

@@ -40,22 +40,15 @@ LOSS_TOL = 1e-4
 GRAD_TOL = 1e-3
 
 KERNELS = {
-    "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_w8<4>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
-    "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_w8<3>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_w16<9,GRU>"),
+    "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_w8<4>", "dec_fwd_x6<13,8,8,LSTM{DF}>", "dec_bwd_w16<9,LSTM>"),
+    "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_w8<3>", "dec_fwd_x6<13,8,8,GRU{DF}>", "dec_bwd_w16<9,GRU>"),
 }
-# A/B runs of the earlier decoder BPTT forms (64-row groups of 32 members)
-_DB = os.environ.get("ABCD_DECBWD", "")
-W16 = not _DB.startswith(("f", "s"))
-if _DB.startswith("s"):
-    KERNELS = {r: k[:3] + (f"dec_bwd_sk<9,16,16,{r}>",) for r, k in KERNELS.items()}
-elif _DB.startswith("f"):
-    KERNELS = {r: k[:3] + (f"dec_bwd_fold<9,16,{r}>",) for r, k in KERNELS.items()}
-W8 = not os.environ.get("ABCD_ENCBWD", "").startswith("s")  # the 32-row / 8-member encoder BPTT (default)
+# the decoder forward's data-as-flag hand-offs (default; ABCD_DECFWD_DF=0: per-member flags)
+_DF = "" if os.environ.get("ABCD_DECFWD_DF", "") == "0" else ",DF"
+KERNELS = {r: tuple(x.replace("{DF}", _DF) for x in k) for r, k in KERNELS.items()}
 # the encoder weight-gradient form (ABCD_WG3=0: gemm_wg2; ABCD_WG3W=2/8/4: gemm_wg3; default gemm_wg3b)
 WG_FORM = ("gemm_wg2" if os.environ.get("ABCD_WG3", "") == "0"
            else "gemm_wg3" if os.environ.get("ABCD_WG3W", "")[:1] in ("2", "8", "4") else "gemm_wg3b")
-if not W8:
-    KERNELS = {r: (k[0], f"enc_bwd_sk<{4 if r == 'LSTM' else 3},16>") + k[2:] for r, k in KERNELS.items()}
 
 
 # (bench config, batch, seed of the synthetic batch)
@@ -102,9 +95,8 @@ def test_full_shape_step_vs_oracle(name, B, seed):
     assert N.lib().abcd_device_status() == 0
     ran = N.dispatch()
     tiles = (B + 63) // 64
-    grids = {"enc_fwd": tiles * 2 * 16, "enc_bwd": (B + 31) // 32 * 2 * 8 if W8 else tiles * 2 * 16,
-             "dec_fwd": tiles * 32,
-             "dec_bwd": (B + 31) // 32 * 16 if W16 else tiles * 32}
+    grids = {"enc_fwd": tiles * 2 * 16, "enc_bwd": (B + 31) // 32 * 2 * 8, "dec_fwd": tiles * 32,
+             "dec_bwd": (B + 31) // 32 * 16}
     for role, kern in zip(("enc_fwd", "enc_bwd", "dec_fwd", "dec_bwd"), KERNELS[cfg["rnn"]]):
         assert ran[role][0] == f"{kern} grid {grids[role]}", (role, ran[role])
         assert ran[role][1] == 1, (role, ran[role])

@@ -33,16 +33,9 @@ EXPECT = {
     "GRU": {"enc_fwd": "enc_fwd_persist<3,16,8>", "enc_bwd": "enc_bwd_w8<3>",
             "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_w16<9,GRU>"},
 }
-_DB = os.environ.get("ABCD_DECBWD", "")  # A/B runs of the earlier decoder BPTT forms
+_DF = "" if os.environ.get("ABCD_DECFWD_DF", "") == "0" else ",DF"  # data-as-flag decoder forward (default)
 for _r in EXPECT:
-    if _DB.startswith("s"):
-        EXPECT[_r]["dec_bwd"] = f"dec_bwd_sk<9,16,16,{_r}>"
-    elif _DB.startswith("f"):
-        EXPECT[_r]["dec_bwd"] = f"dec_bwd_fold<9,16,{_r}>"
-W16 = not _DB.startswith(("f", "s"))  # the 32-row / 16-member decoder BPTT (default)
-if os.environ.get("ABCD_ENCBWD", "").startswith("s"):  # A/B runs of the 64-row / 16-member encoder BPTT
-    for _r in EXPECT:
-        EXPECT[_r]["enc_bwd"] = f"enc_bwd_sk<{4 if _r == 'LSTM' else 3},16>"
+    EXPECT[_r]["dec_fwd"] = f"dec_fwd_x6<13,8,8,{_r}{_DF}>"
 
 
 def _noise(inp):
@@ -69,7 +62,7 @@ def test_fused_step_prod_vs_reference(name):
         assert ran[role][0].startswith(kern), (role, ran[role])
         assert ran[role][1] == 1, (role, ran[role])
     # 2 row groups x 32 members (dec_bwd_w16: 3 groups of 32 rows x 16 members)
-    assert ran["dec_bwd"][0].endswith("grid 48" if W16 else "grid 64") and ran["dec_fwd"][0].endswith("grid 64")
+    assert ran["dec_bwd"][0].endswith("grid 48") and ran["dec_fwd"][0].endswith("grid 64")
     if not meta.get("plain"):  # the fused sampler head, 5 tiles of 16 rows (the last one ragged: 72 = 4 x 16 + 8)
         assert "samp_head_fwd grid 5" in ran["samp_fwd"][0] and ran["samp_fwd"][1] == 1, ran["samp_fwd"]
         assert ran["samp_bwd"][0].startswith("samp_head_bwd grid 5") and ran["samp_bwd"][1] == 1, ran["samp_bwd"]
