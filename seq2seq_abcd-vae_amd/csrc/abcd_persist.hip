@@ -267,6 +267,34 @@ struct PollEmpty {
     return (spins & SPIN_PROBE_MASK) != 0 || !spin_abandoned();
   }
 };
+// A consumer first waits on ONE word per producer (the last word of the
+// producer's store for the consumer's rows: lane l probes producer l) --
+// a 256-B poll instead of re-reading the whole operand while it is still
+// arriving (polling the operand itself multiplied the gather traffic and cost
+// +40 % at 8 row groups) -- and only then gathers, still checking every word
+// (PollEmpty: a word of a producer's store that lands after its probe word is
+// simply re-read).  probe_issue goes out early; the caller places independent
+// work (deferred stash stores, the noise draw) between it and probe_spin.
+DEV unsigned probe_issue(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 16);
+}
+DEV void probe_spin(__amdgpu_buffer_rsrc_t rs, uint32_t off, unsigned v) {
+  if (!__builtin_amdgcn_ballot_w64(v == HANDOFF_EMPTY)) return;
+  unsigned spins = 0;
+  const unsigned lim = g_spin_limit;
+  do {
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");  // a new load every pass
+    v = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 16);
+    if (++spins > lim) {
+      if ((threadIdx.x & 63) == 0) spin_timed_out();
+      return;
+    }
+    if ((spins & SPIN_PROBE_MASK) == 0 && spin_abandoned()) return;
+  } while (__builtin_amdgcn_ballot_w64(v == HANDOFF_EMPTY));
+}
+constexpr uint32_t PROBE_NONE = 0x80000000u;  // past every buffer's extent: reads 0
+
 // fill [p, p + n4 float4s) with HANDOFF_EMPTY (one kernel per launch, up to 3 ranges)
 struct FillRanges {
   float* p[3];
@@ -1128,8 +1156,9 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 // then reads no Hprev row written in the launch, so Hprev leaves as a plain
 // stash store).  LVX is double-buffered by step parity: with no group-wide
 // wait per phase, the emit barrier of step t+1 is what orders step t's LVX
-// reads before step t+2's writes.
-template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, bool DF = false>
+// reads before step t+2's writes.  DF > 0 is also the depth of the operand
+// ring (chunks in flight) of the polled gathers.
+template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, int DF = 0>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   static_assert(!DF || HPRE, "the data-as-flag form forms the recurrent half in the mlp phase");
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
@@ -1177,6 +1206,22 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   constexpr int NXC = NCC - 8;  // input chunks of the cell product (H = 256)
   f4 acch[2] = {f4zero(), f4zero()};  // HPRE: h_{t-1} W_hh^T of this step, from the previous mlp phase
   const int* off = a.off;
+  // the last emit phase's stash values (mu or lv, and the sample x): stored
+  // at once (flag form) or behind the next cell's probe (DF)
+  float sev[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+  int s_o = 0, s_bs = 0;
+  auto emit_stash = [&]() {
+    if (has2 && erow0 < s_bs) {
+      const uint32_t ext = (uint32_t)s_bs * Fp * 4u;
+      const uint32_t eoff = (uint32_t)((erow0 + (lane >> 2)) * Fp + 16 * j2 + 4 * (lane & 3)) * 4u;
+      if (part == 0) {
+        st4(make_rsrc(a.MU + (size_t)s_o * Fp, ext), eoff, tp_quad(tb, sev, lane), false);
+        st4(make_rsrc(a.OUT + (size_t)s_o * Fp, ext), eoff, tp_quad(tb, sx, lane), false);
+      } else {
+        st4(make_rsrc(a.LV + (size_t)s_o * Fp, ext), eoff, tp_quad(tb, sev, lane), false);
+      }
+    }
+  };
   for (int i = 0; i < T; ++i) {
     const int t = i;
     const int o = off[t], bs = off[t + 1] - o;
@@ -1192,6 +1237,16 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     }
     if (!DF && i > 0) gs.wait(3u * i);
     PSTAMP(0);
+    if constexpr (DF) {
+      // probe the emit producers' x rows, then the previous step's emit stashes
+      const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.Xin + (size_t)o * Fp, (uint32_t)bs * Fp * 4u);
+      const int pr = min(row0 + 15, bs - 1);
+      const uint32_t poff =
+          (i > 0 && NXC > 0 && row0 < bs && lane < n2t) ? (uint32_t)(pr * Fp + 16 * lane + 15) * 4u : PROBE_NONE;
+      const unsigned pv = probe_issue(rx, poff);
+      if (i > 0) emit_stash();
+      probe_spin(rx, poff, pv);
+    }
     f4 acc[2];
     acc[0] = acc[1] = f4zero();
     if (row0 < bs) {
@@ -1203,7 +1258,8 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         acc[0] = acch[0];
         acc[1] = acch[1];
         if constexpr (NXC > 0 && DF)
-          wave_mma_x6<2, (NXC > 0 ? NXC : 1), 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC, PollEmpty{});
+          wave_mma_x6<2, (NXC > 0 ? NXC : 1), (DF > 0 ? DF : 4)>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC,
+                                                                 PollEmpty{});
         else if constexpr (NXC > 0)
           wave_mma_x6<2, (NXC > 0 ? NXC : 1), 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC);
       } else {
@@ -1247,25 +1303,37 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     }
     if (!DF) gs.publish();
     PSTAMP(1);
-    if (row0 < bs) {  // stashes for the backward pass (plain 16-B stores)
-      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
-      const uint32_t goff = (uint32_t)((row0 + trow) * 4 * H + u0 + tc) * 4u;
-      {
-        const float v[4] = {lo ? gi[0] : gg[0], lo ? gi[1] : gg[1], lo ? gi[2] : gg[2], lo ? gi[3] : gg[3]};
-        st4(rg, goff + (uint32_t)(thi ? 2 * H : 0) * 4u, tp_quad(tb, v, lane), false);  // i | g
+    // stashes for the backward pass (plain 16-B stores); DF: behind the mlp probe
+    auto cell_stash = [&]() {
+      if (row0 < bs) {
+        const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
+        const uint32_t goff = (uint32_t)((row0 + trow) * 4 * H + u0 + tc) * 4u;
+        {
+          const float v[4] = {lo ? gi[0] : gg[0], lo ? gi[1] : gg[1], lo ? gi[2] : gg[2], lo ? gi[3] : gg[3]};
+          st4(rg, goff + (uint32_t)(thi ? 2 * H : 0) * 4u, tp_quad(tb, v, lane), false);  // i | g
+        }
+        {
+          const float v[4] = {lo ? gf[0] : go[0], lo ? gf[1] : go[1], lo ? gf[2] : go[2], lo ? gf[3] : go[3]};
+          st4(rg, goff + (uint32_t)(thi ? 3 * H : H) * 4u, tp_quad(tb, v, lane), false);  // f | o
+        }
+        if constexpr (!GRU) {  // c -> Cst (lo half), -> the next step's Cprev row (hi half)
+          const f4 cq = tp_quad(tb, cst, lane);
+          if (!thi) st4(make_rsrc(a.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qoff, cq, false);
+          else st4(make_rsrc(a.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, cq, false);
+        }
       }
-      {
-        const float v[4] = {lo ? gf[0] : go[0], lo ? gf[1] : go[1], lo ? gf[2] : go[2], lo ? gf[3] : go[3]};
-        st4(rg, goff + (uint32_t)(thi ? 3 * H : H) * 4u, tp_quad(tb, v, lane), false);  // f | o
-      }
-      if constexpr (!GRU) {  // c -> Cst (lo half), -> the next step's Cprev row (hi half)
-        const f4 cq = tp_quad(tb, cst, lane);
-        if (!thi) st4(make_rsrc(a.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qoff, cq, false);
-        else st4(make_rsrc(a.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, cq, false);
-      }
-    }
+    };
+    if constexpr (!DF) cell_stash();
     // ---------------- mlp ----------------
     if (!DF) gs.wait(3u * i + 1);
+    if constexpr (DF) {
+      const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u);
+      const int pr = min(row0 + 15, bs - 1);
+      const uint32_t poff = (has1 && row0 < bs && lane < M) ? (uint32_t)(pr * H + 8 * lane + 7) * 4u : PROBE_NONE;
+      const unsigned pv = probe_issue(rh, poff);
+      cell_stash();
+      probe_spin(rh, poff, pv);
+    }
     PSTAMP(2);
     if (has1) {
       f4 a1[1] = {f4zero()};
@@ -1274,13 +1342,13 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
-          if constexpr (DF) wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32, PollEmpty{});
+          if constexpr (DF) wave_mma_x6p<3, NH32, (DF > 0 ? DF : 4)>(a3, Hs, row0 + r, bp, lane, q, mem % NH32, PollEmpty{});
           else wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
           a1[0] = a3[0];
           acch[0] = a3[1];
           acch[1] = a3[2];
         } else if constexpr (DF) {
-          wave_mma_x6<1, NH32, 4>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32, PollEmpty{});
+          wave_mma_x6<1, NH32, (DF > 0 ? DF : 4)>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32, PollEmpty{});
         } else {
           wave_mma_x6<1, NH32, 4>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32);
         }
@@ -1297,6 +1365,15 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     // ---------------- emit ----------------
     // the mu waves' noise, drawn before the wait (independent of the recurrence)
     float epre[4] = {0.f, 0.f, 0.f, 0.f}, mpre[4] = {1.f, 1.f, 1.f, 1.f};
+    const __amdgpu_buffer_rsrc_t rae =
+        make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u);
+    uint32_t epoff = PROBE_NONE;
+    unsigned epv = 0;
+    if constexpr (DF) {  // probe the Hm / 16 mlp producers of this wave's Aact half
+      const int pr = min(erow0 + 15, bs - 1);
+      if (has2 && erow0 < bs && lane < Hm / 16) epoff = (uint32_t)(pr * 2 * Hm + 16 * lane + 15) * 4u;
+      epv = probe_issue(rae, epoff);
+    }
     if (has2 && part == 0 && col2 < F) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1311,17 +1388,17 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     // polled by wave 3 (an lv wave): the mu waves' noise draw above is ~1 us
     // of VALU that would otherwise delay the poll
     if (!DF) gs.wait(3u * i + 2, 3);
+    if constexpr (DF) probe_spin(rae, epoff, epv);
     PSTAMP(4);
     float* LVX = LVX0 + (DF ? (i & 1) * 2 * 16 * 16 : 0);
     float ev[4] = {0.f, 0.f, 0.f, 0.f};  // mu (part 0) / lv (part 1); sample x kept in epre
     if (has2) {
       f4 ae[1] = {f4zero()};
       if (erow0 < bs) {
-        const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
-                       (uint32_t)2 * Hm * 4u};
+        const BufKC Aa{rae, (uint32_t)2 * Hm * 4u};
         if constexpr (DF)
-          wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q, mem % NM32,
-                                  PollEmpty{});
+          wave_mma_x6<1, NM32, (DF > 0 ? DF : 4)>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
+                                                  mem % NM32, PollEmpty{});
         else
           wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q, mem % NM32);
       }
@@ -1349,17 +1426,18 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         st4(make_rsrc(a.Xin + (size_t)next_off * Fp, (uint32_t)next_bs * Fp * 4u), eoff, xq, true);
     }
     if (!DF) gs.publish();
-    if (has2 && erow0 < bs) {
-      const uint32_t ext = (uint32_t)bs * Fp * 4u;
-      if (part == 0) {
-        st4(make_rsrc(a.MU + (size_t)o * Fp, ext), eoff, tp_quad(tb, ev, lane), false);
-        st4(make_rsrc(a.OUT + (size_t)o * Fp, ext), eoff, tp_quad(tb, epre, lane), false);
-      } else {
-        st4(make_rsrc(a.LV + (size_t)o * Fp, ext), eoff, tp_quad(tb, ev, lane), false);
-      }
+    // MU / LV / OUT stashes (plain); DF: behind the next cell's probe
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      sev[g] = ev[g];
+      sx[g] = epre[g];
     }
+    s_o = o;
+    s_bs = bs;
+    if constexpr (!DF) emit_stash();
     PSTAMP(5);
   }
+  if constexpr (DF) emit_stash();
 }
 
 // ---------------------------------------------------------------------------
@@ -2573,7 +2651,7 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, bool DF>
+template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, int DF>
 static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
   const size_t lds =
@@ -2608,15 +2686,17 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
 }
 
 // the data-as-flag hand-offs by default; ABCD_DECFWD_DF=0 keeps the
-// per-member flag form (same-box A/B)
-static bool dec_fwd_df_on() {
+// per-member flag form, =8 polls with 8 chunks in flight (same-box A/B)
+static int dec_fwd_df() {
   const char* v = getenv("ABCD_DECFWD_DF");
-  return !(v && v[0] == '0');
+  return !(v && v[0]) ? 4 : v[0] == '0' ? 0 : v[0] == '8' ? 8 : 4;
 }
 template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
-  if (dec_fwd_df_on()) return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, true>(s, a, launched);
-  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, false>(s, a, launched);
+  const int df = dec_fwd_df();
+  if (df == 8) return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, 8>(s, a, launched);
+  if (df == 4) return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, 4>(s, a, launched);
+  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, 0>(s, a, launched);
 }
 
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {
