@@ -58,7 +58,6 @@ struct PBwdArgs {
 //   emit : mu, lv = Aact W2^T + b2; x = mu + e^{lv/2} eps -> Xin_{t+1}
 struct PDecFwdArgs {
   int H, Hm, F, Fp, T, nrt, feedback;
-  int L, B;                        // packed rows, rows of step 0 (the data-as-flag fill)
   int flags;                       // hand-off form: 1 per-member flags, 0 group counter
   const int* off;
   unsigned* sync;
@@ -92,7 +91,7 @@ struct PDecBwdArgs {
   const float* xmask;              // input-dropout noise (rows x F) of the cell inputs; null: none
   float *dG, *dMU, *dLV, *dZ, *DHR, *DC0;
   float* dGH;                      // GRU: the recurrent-side gate gradients (dG holds the input side)
-  float* part;  // split-K partials (dec_bwd_sk): 2 parity slots x groups x (Fp+H)/16 subtiles x 4 waves x H/8 x 256
+  float* part;  // split-K partials (dec_bwd_w16): 2 parity slots x 32-row groups x (Fp+H)/16 subtiles x 2 row blocks x 16 producers x 256
 };
 inline size_t dec_part_floats(int B, int H, int Fp) {
   return 2 * (size_t)cdiv(B, 64) * (size_t)((Fp + H) / 16) * 4 * (size_t)(H / 8) * 256;
@@ -106,10 +105,10 @@ inline size_t persist_part_floats(int nd, int B, int H) {
   const size_t nut = (size_t)H / 16;
   return 2 * (size_t)persist_groups(nd, B) * nut * 4 * nut * 256;
 }
-// group counters + the role registry (abcd_persist.hip: 8 XCD ticket lines + 1
-// arrival line) + a second counter per group (dec_bwd_sk: split-K partials
-// drained) + 64 per-member flag lines per group (flag-form hand-offs)
-// sized for 32-row groups (dec_bwd_w16), a superset of the 64-row layouts
+// group counters + the role registry (abcd_persist.hip: 9 lines) + a second
+// counter per group + 64 per-member flag lines per group (flag-form
+// hand-offs), sized for 32-row groups (dec_bwd_w16, enc_bwd_w8), a superset
+// of the 64-row layouts
 inline size_t persist_sync_uints(int nd, int B) { return (size_t)(66 * nd * cdiv(B, 32) + 9) * PERSIST_SYNC_STRIDE; }
 
 // Copy off[0..T] to device memory `dst` on stream s through a pinned ring

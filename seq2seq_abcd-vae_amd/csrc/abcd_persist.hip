@@ -228,88 +228,6 @@ struct GSync {
   }
 };
 
-// Data-as-flag hand-off (MI355X_MICROARCH.md handoff-1to1: the payload is its
-// own flag).  A hand-off buffer whose every word is written exactly ONCE per
-// launch (the decoder forward's Hs / Aact / Xin stash rows: distinct per step)
-// is filled with HANDOFF_EMPTY before the launch; producers store their words
-// write-through (sc1) with no drain and no signal, and a consumer re-reads, with
-// sc1 loads, each 32-deep operand chunk until none of its words is still
-// HANDOFF_EMPTY -- one memory round trip after the producer's store instead of
-// drain + flag + poll + barrier + gather.  Each 4-B word is single-copy
-// atomic, so a word is either the fill or its final value.  HANDOFF_EMPTY is a
-// signalling NaN: arithmetic never produces one (every fp32 op quiets NaNs),
-// so neither real data nor a diverged (NaN) run can look empty.
-constexpr unsigned HANDOFF_EMPTY = 0x7FA5A5A5u;
-DEV bool any_empty(const f4& a, const f4& b) {
-  // (the elements go through scalars: hipcc (ROCm 7.2) lowers
-  // __builtin_bit_cast of a vector-element lvalue to a read of element 0)
-  bool e = false;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float x = a[k], y = b[k];
-    e |= (__builtin_bit_cast(unsigned, x) == HANDOFF_EMPTY) | (__builtin_bit_cast(unsigned, y) == HANDOFF_EMPTY);
-  }
-  return e;
-}
-// wave_mma_x6's chunk check (abcd_x6.h X6_POLL_CHUNK): a chunk with a word
-// still HANDOFF_EMPTY is re-read; every hand-off wait is bounded (a timeout
-// sets the status and goes on with what it has)
-struct PollEmpty {
-  static constexpr bool on = true;
-  DEV bool empty(const f4& a, const f4& b) const { return any_empty(a, b); }
-  DEV unsigned limit() const { return g_spin_limit; }
-  DEV bool spin(unsigned& spins, unsigned lim) const {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > lim) {
-      if ((threadIdx.x & 63) == 0) spin_timed_out();
-      return false;
-    }
-    return (spins & SPIN_PROBE_MASK) != 0 || !spin_abandoned();
-  }
-};
-// A consumer first waits on ONE word per producer (the last word of the
-// producer's store for the consumer's rows: lane l probes producer l) --
-// a 256-B poll instead of re-reading the whole operand while it is still
-// arriving (polling the operand itself multiplied the gather traffic and cost
-// +40 % at 8 row groups) -- and only then gathers, still checking every word
-// (PollEmpty: a word of a producer's store that lands after its probe word is
-// simply re-read).  probe_issue goes out early; the caller places independent
-// work (deferred stash stores, the noise draw) between it and probe_spin.
-DEV unsigned probe_issue(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 16);
-}
-DEV void probe_spin(__amdgpu_buffer_rsrc_t rs, uint32_t off, unsigned v) {
-  if (!__builtin_amdgcn_ballot_w64(v == HANDOFF_EMPTY)) return;
-  unsigned spins = 0;
-  const unsigned lim = g_spin_limit;
-  do {
-    __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");  // a new load every pass
-    v = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 16);
-    if (++spins > lim) {
-      if ((threadIdx.x & 63) == 0) spin_timed_out();
-      return;
-    }
-    if ((spins & SPIN_PROBE_MASK) == 0 && spin_abandoned()) return;
-  } while (__builtin_amdgcn_ballot_w64(v == HANDOFF_EMPTY));
-}
-constexpr uint32_t PROBE_NONE = 0x80000000u;  // past every buffer's extent: reads 0
-
-// fill [p, p + n4 float4s) with HANDOFF_EMPTY (one kernel per launch, up to 3 ranges)
-struct FillRanges {
-  float* p[3];
-  long n4[3];
-};
-__global__ __launch_bounds__(256) void handoff_fill(FillRanges fr) {
-  const uint4 v = make_uint4(HANDOFF_EMPTY, HANDOFF_EMPTY, HANDOFF_EMPTY, HANDOFF_EMPTY);
-  const long stride = (long)gridDim.x * 256;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    uint4* d = reinterpret_cast<uint4*>(fr.p[k]);
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < fr.n4[k]; i += stride) d[i] = v;
-  }
-}
-
 // diagnostics: thread 0 stamps s_memrealtime (100 MHz, one clock for the whole
 // device, so stamps of different workgroups compare) at the phase boundaries of step i
 #define PSTAMP(k)                                                                                   \
@@ -1149,18 +1067,12 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 // the next step's Hprev rows) -- as two more tiles beside the mlp tile, and
 // carried in registers; step t+1's cell then waits only for x_{t+1} and runs
 // the NCC - 8 input chunks (H = 256: 8 recurrent chunks).
-// DF: the three hand-offs are data-as-flag (HANDOFF_EMPTY above): Hs, Aact and
-// the fed-back Xin rows are filled before the launch, each consumer wave polls
-// its own operand chunks inside the MMA (PollEmpty), and nothing is drained,
-// signalled or waited for at the phase boundaries.  Requires HPRE (the cell
-// then reads no Hprev row written in the launch, so Hprev leaves as a plain
-// stash store).  LVX is double-buffered by step parity: with no group-wide
-// wait per phase, the emit barrier of step t+1 is what orders step t's LVX
-// reads before step t+2's writes.  DF > 0 is also the depth of the operand
-// ring (chunks in flight) of the polled gathers.
-template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, int DF = 0>
+// LATEH: those two recurrent tiles are multiplied AFTER the mlp publish, from
+// the Hs chunks the mlp tile's product kept in registers (wave_mma_x6_keep /
+// _from): the mlp -> emit hand-off no longer waits for 96 of the phase's 144
+// MFMAs; they run in the emit phase's wait instead.
+template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, bool LATEH = true>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
-  static_assert(!DF || HPRE, "the data-as-flag form forms the recurrent half in the mlp phase");
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
   const int M = H / 8;
@@ -1184,8 +1096,8 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   f4* BC = smem;                        // cell [x | h]: [2][NCC][3][64]
   f4* B1 = BC + 2 * NCC * 3 * 64;       // mlp tile: [NH32][3][64]
   f4* B2 = B1 + NH32 * 3 * 64;          // emit: mu tile, lv tile: [2][NM32][3][64]
-  float* LVX0 = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [DF ? 2 : 1][2][16][16]
-  float* tb = LVX0 + (DF ? 2 : 1) * 2 * 16 * 16 + w * TP_FLOATS;   // this wave's transpose tile
+  float* LVX = reinterpret_cast<float*>(B2 + 2 * NM32 * 3 * 64);  // lv hand-over: [2][16][16]
+  float* tb = LVX + 2 * 16 * 16 + w * TP_FLOATS;                   // this wave's transpose tile
   if (nx32)
     stage_x6(BC, a.Wih, Fp, Fp, 2, nx32, 0, NCC,
              [&](int j, int rr) { return GRU ? dec_gru_row(H, u0, j, rr, true) : dec_cell_row(H, u0, j, rr); });
@@ -1206,22 +1118,6 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   constexpr int NXC = NCC - 8;  // input chunks of the cell product (H = 256)
   f4 acch[2] = {f4zero(), f4zero()};  // HPRE: h_{t-1} W_hh^T of this step, from the previous mlp phase
   const int* off = a.off;
-  // the last emit phase's stash values (mu or lv, and the sample x): stored
-  // at once (flag form) or behind the next cell's probe (DF)
-  float sev[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
-  int s_o = 0, s_bs = 0;
-  auto emit_stash = [&]() {
-    if (has2 && erow0 < s_bs) {
-      const uint32_t ext = (uint32_t)s_bs * Fp * 4u;
-      const uint32_t eoff = (uint32_t)((erow0 + (lane >> 2)) * Fp + 16 * j2 + 4 * (lane & 3)) * 4u;
-      if (part == 0) {
-        st4(make_rsrc(a.MU + (size_t)s_o * Fp, ext), eoff, tp_quad(tb, sev, lane), false);
-        st4(make_rsrc(a.OUT + (size_t)s_o * Fp, ext), eoff, tp_quad(tb, sx, lane), false);
-      } else {
-        st4(make_rsrc(a.LV + (size_t)s_o * Fp, ext), eoff, tp_quad(tb, sev, lane), false);
-      }
-    }
-  };
   for (int i = 0; i < T; ++i) {
     const int t = i;
     const int o = off[t], bs = off[t + 1] - o;
@@ -1235,18 +1131,8 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         cst[g] = b < bs ? (GRU ? a.Hprev : a.Cprev)[(long)(o + b) * H + unit] : 0.f;
       }
     }
-    if (!DF && i > 0) gs.wait(3u * i);
+    if (i > 0) gs.wait(3u * i);
     PSTAMP(0);
-    if constexpr (DF) {
-      // probe the emit producers' x rows, then the previous step's emit stashes
-      const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.Xin + (size_t)o * Fp, (uint32_t)bs * Fp * 4u);
-      const int pr = min(row0 + 15, bs - 1);
-      const uint32_t poff =
-          (i > 0 && NXC > 0 && row0 < bs && lane < n2t) ? (uint32_t)(pr * Fp + 16 * lane + 15) * 4u : PROBE_NONE;
-      const unsigned pv = probe_issue(rx, poff);
-      if (i > 0) emit_stash();
-      probe_spin(rx, poff, pv);
-    }
     f4 acc[2];
     acc[0] = acc[1] = f4zero();
     if (row0 < bs) {
@@ -1257,10 +1143,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       if (HPRE && i > 0) {
         acc[0] = acch[0];
         acc[1] = acch[1];
-        if constexpr (NXC > 0 && DF)
-          wave_mma_x6<2, (NXC > 0 ? NXC : 1), (DF > 0 ? DF : 4)>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC,
-                                                                 PollEmpty{});
-        else if constexpr (NXC > 0)
+        if constexpr (NXC > 0)
           wave_mma_x6<2, (NXC > 0 ? NXC : 1), 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NXC);
       } else {
         wave_mma_x6<2, NCC, 4>(acc, A, row0 + r, BC, NCC, lane, q, mem % NCC);
@@ -1298,57 +1181,47 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       const f4 hq = tp_quad(tb, hv, lane);
       if (row0 < bs) {
         if (!thi) st4(make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), qoff, hq, true);
-        else st4(make_rsrc(a.Hprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, hq, !DF);
+        else st4(make_rsrc(a.Hprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, hq, true);
       }
     }
-    if (!DF) gs.publish();
+    gs.publish();
     PSTAMP(1);
-    // stashes for the backward pass (plain 16-B stores); DF: behind the mlp probe
-    auto cell_stash = [&]() {
-      if (row0 < bs) {
-        const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
-        const uint32_t goff = (uint32_t)((row0 + trow) * 4 * H + u0 + tc) * 4u;
-        {
-          const float v[4] = {lo ? gi[0] : gg[0], lo ? gi[1] : gg[1], lo ? gi[2] : gg[2], lo ? gi[3] : gg[3]};
-          st4(rg, goff + (uint32_t)(thi ? 2 * H : 0) * 4u, tp_quad(tb, v, lane), false);  // i | g
-        }
-        {
-          const float v[4] = {lo ? gf[0] : go[0], lo ? gf[1] : go[1], lo ? gf[2] : go[2], lo ? gf[3] : go[3]};
-          st4(rg, goff + (uint32_t)(thi ? 3 * H : H) * 4u, tp_quad(tb, v, lane), false);  // f | o
-        }
-        if constexpr (!GRU) {  // c -> Cst (lo half), -> the next step's Cprev row (hi half)
-          const f4 cq = tp_quad(tb, cst, lane);
-          if (!thi) st4(make_rsrc(a.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qoff, cq, false);
-          else st4(make_rsrc(a.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, cq, false);
-        }
+    if (row0 < bs) {  // stashes for the backward pass (plain 16-B stores)
+      const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
+      const uint32_t goff = (uint32_t)((row0 + trow) * 4 * H + u0 + tc) * 4u;
+      {
+        const float v[4] = {lo ? gi[0] : gg[0], lo ? gi[1] : gg[1], lo ? gi[2] : gg[2], lo ? gi[3] : gg[3]};
+        st4(rg, goff + (uint32_t)(thi ? 2 * H : 0) * 4u, tp_quad(tb, v, lane), false);  // i | g
       }
-    };
-    if constexpr (!DF) cell_stash();
-    // ---------------- mlp ----------------
-    if (!DF) gs.wait(3u * i + 1);
-    if constexpr (DF) {
-      const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u);
-      const int pr = min(row0 + 15, bs - 1);
-      const uint32_t poff = (has1 && row0 < bs && lane < M) ? (uint32_t)(pr * H + 8 * lane + 7) * 4u : PROBE_NONE;
-      const unsigned pv = probe_issue(rh, poff);
-      cell_stash();
-      probe_spin(rh, poff, pv);
+      {
+        const float v[4] = {lo ? gf[0] : go[0], lo ? gf[1] : go[1], lo ? gf[2] : go[2], lo ? gf[3] : go[3]};
+        st4(rg, goff + (uint32_t)(thi ? 3 * H : H) * 4u, tp_quad(tb, v, lane), false);  // f | o
+      }
+      if constexpr (!GRU) {  // c -> Cst (lo half), -> the next step's Cprev row (hi half)
+        const f4 cq = tp_quad(tb, cst, lane);
+        if (!thi) st4(make_rsrc(a.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qoff, cq, false);
+        else st4(make_rsrc(a.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qoff, cq, false);
+      }
     }
+    // ---------------- mlp ----------------
+    gs.wait(3u * i + 1);
     PSTAMP(2);
+    f4 ka[NH32][2];    // LATEH: this wave's Hs chunks, for the recurrent tiles after the publish
+    bool late = false;
     if (has1) {
       f4 a1[1] = {f4zero()};
       if (row0 < bs) {
         const BufKC Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
-        if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
+        if (LATEH && HPRE && i + 1 < T) {
+          wave_mma_x6_keep<1, NH32, 4>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32, ka);
+          late = true;
+        } else if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
-          if constexpr (DF) wave_mma_x6p<3, NH32, (DF > 0 ? DF : 4)>(a3, Hs, row0 + r, bp, lane, q, mem % NH32, PollEmpty{});
-          else wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
+          wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
           a1[0] = a3[0];
           acch[0] = a3[1];
           acch[1] = a3[2];
-        } else if constexpr (DF) {
-          wave_mma_x6<1, NH32, (DF > 0 ? DF : 4)>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32, PollEmpty{});
         } else {
           wave_mma_x6<1, NH32, 4>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32);
         }
@@ -1360,20 +1233,18 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         st4(make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
             (uint32_t)((row0 + trow) * 2 * Hm + 16 * mem + tcol) * 4u, aq, true);
     }
-    if (!DF) gs.publish();
+    gs.publish();
+    if (LATEH && late) {  // the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
+      f4 a2[2] = {f4zero(), f4zero()};
+      const f4* const bp2[2] = {BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
+      wave_mma_x6_from<2, NH32>(a2, ka, bp2, lane, mem % NH32);
+      acch[0] = a2[0];
+      acch[1] = a2[1];
+    }
     PSTAMP(3);
     // ---------------- emit ----------------
     // the mu waves' noise, drawn before the wait (independent of the recurrence)
     float epre[4] = {0.f, 0.f, 0.f, 0.f}, mpre[4] = {1.f, 1.f, 1.f, 1.f};
-    const __amdgpu_buffer_rsrc_t rae =
-        make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u);
-    uint32_t epoff = PROBE_NONE;
-    unsigned epv = 0;
-    if constexpr (DF) {  // probe the Hm / 16 mlp producers of this wave's Aact half
-      const int pr = min(erow0 + 15, bs - 1);
-      if (has2 && erow0 < bs && lane < Hm / 16) epoff = (uint32_t)(pr * 2 * Hm + 16 * lane + 15) * 4u;
-      epv = probe_issue(rae, epoff);
-    }
     if (has2 && part == 0 && col2 < F) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1387,20 +1258,16 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     }
     // polled by wave 3 (an lv wave): the mu waves' noise draw above is ~1 us
     // of VALU that would otherwise delay the poll
-    if (!DF) gs.wait(3u * i + 2, 3);
-    if constexpr (DF) probe_spin(rae, epoff, epv);
+    gs.wait(3u * i + 2, 3);
     PSTAMP(4);
-    float* LVX = LVX0 + (DF ? (i & 1) * 2 * 16 * 16 : 0);
     float ev[4] = {0.f, 0.f, 0.f, 0.f};  // mu (part 0) / lv (part 1); sample x kept in epre
     if (has2) {
       f4 ae[1] = {f4zero()};
       if (erow0 < bs) {
-        const BufKC Aa{rae, (uint32_t)2 * Hm * 4u};
-        if constexpr (DF)
-          wave_mma_x6<1, NM32, (DF > 0 ? DF : 4)>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
-                                                  mem % NM32, PollEmpty{});
-        else
-          wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q, mem % NM32);
+        const BufKC Aa{make_rsrc(a.Aact + (size_t)o * 2 * Hm + part * Hm, (uint32_t)(bs * 2 * Hm - part * Hm) * 4u),
+                       (uint32_t)2 * Hm * 4u};
+        wave_mma_x6<1, NM32, 4>(ae, Aa, erow0 + r, B2 + part * NM32 * 3 * 64, NM32, lane, q,
+                                mem % NM32);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) ev[g] = col2 < F ? ae[0][g] + b2v : 0.f;
@@ -1425,19 +1292,18 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
       if (a.feedback && erow0 < next_bs)
         st4(make_rsrc(a.Xin + (size_t)next_off * Fp, (uint32_t)next_bs * Fp * 4u), eoff, xq, true);
     }
-    if (!DF) gs.publish();
-    // MU / LV / OUT stashes (plain); DF: behind the next cell's probe
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      sev[g] = ev[g];
-      sx[g] = epre[g];
+    gs.publish();
+    if (has2 && erow0 < bs) {
+      const uint32_t ext = (uint32_t)bs * Fp * 4u;
+      if (part == 0) {
+        st4(make_rsrc(a.MU + (size_t)o * Fp, ext), eoff, tp_quad(tb, ev, lane), false);
+        st4(make_rsrc(a.OUT + (size_t)o * Fp, ext), eoff, tp_quad(tb, epre, lane), false);
+      } else {
+        st4(make_rsrc(a.LV + (size_t)o * Fp, ext), eoff, tp_quad(tb, ev, lane), false);
+      }
     }
-    s_o = o;
-    s_bs = bs;
-    if constexpr (!DF) emit_stash();
     PSTAMP(5);
   }
-  if constexpr (DF) emit_stash();
 }
 
 // ---------------------------------------------------------------------------
@@ -2651,52 +2517,36 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, int DF>
+template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, bool LATEH>
 static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
-  const size_t lds =
-      (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + (DF ? 2 : 1) * 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
+  const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, DF>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, LATEH>, grid, lds, &ok));
   if (!ok) return 0;
-  if (DF) {  // every word the launch hands off starts as HANDOFF_EMPTY
-    if (a.L <= 0 || a.B <= 0 || a.B > a.L) return (int)hipErrorInvalidValue;
-    FillRanges fr{};
-    fr.p[0] = a.Hs; fr.n4[0] = (long)a.L * a.H / 4;
-    fr.p[1] = a.Aact; fr.n4[1] = (long)a.L * 2 * a.Hm / 4;
-    if (a.feedback) { fr.p[2] = a.Xin + (size_t)a.B * a.Fp; fr.n4[2] = (long)(a.L - a.B) * a.Fp / 4; }
-    const long n4 = fr.n4[0] + fr.n4[1] + fr.n4[2];
-    handoff_fill<<<(int)std::min<long>(2048, std::max<long>(1, n4 / 1024)), 256, 0, s>>>(fr);
-    ABCD_TRY(hipGetLastError());
-  }
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, DF><<<grid, 256, lds, s>>>(b);
+    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, LATEH><<<grid, 256, lds, s>>>(b);
   }
-  note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM",
-                DF ? ",DF" : "", grid);
+  note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
 }
 
-// the data-as-flag hand-offs by default; ABCD_DECFWD_DF=0 keeps the
-// per-member flag form, =8 polls with 8 chunks in flight (same-box A/B)
-static int dec_fwd_df() {
-  const char* v = getenv("ABCD_DECFWD_DF");
-  return !(v && v[0]) ? 4 : v[0] == '0' ? 0 : v[0] == '8' ? 8 : 4;
-}
+
+// the recurrent tiles after the mlp publish by default; ABCD_DECFWD_LATEH=0
+// keeps them inside the mlp product (same-box A/B)
 template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
-  const int df = dec_fwd_df();
-  if (df == 8) return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, 8>(s, a, launched);
-  if (df == 4) return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, 4>(s, a, launched);
-  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, 0>(s, a, launched);
+  const char* v = getenv("ABCD_DECFWD_LATEH");
+  if (v && v[0] == '0') return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, false>(s, a, launched);
+  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, true>(s, a, launched);
 }
 
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {

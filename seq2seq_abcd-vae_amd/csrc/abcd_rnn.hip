@@ -941,6 +941,15 @@ __global__ void dec_feats_bwd(const float* dFS, int D, int S, int B, const int64
     demb[i] = acc;
   }
 }
+// the decoder's Philox noise of every (row, feature) at once: element e of the
+// stream (seed, offset) is philox_normal(seed, offset + e), the value the
+// decoder forward draws for row e / F, feature e % F -- so the persistent
+// kernel reads it with one load instead of ~1 us of VALU per step on its
+// critical path
+__global__ __launch_bounds__(256) void philox_normal_fill(float* out, long n, uint64_t seed, uint64_t offset) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256)
+    out[e] = philox_normal(seed, offset + (uint64_t)e);
+}
 // copy a padded (rows x Fp) stash into a user (rows x F) buffer
 __global__ void unpad_rows(const float* src, int Fp, float* dst, int F, long rows) {
   const long n = rows * F;
@@ -954,6 +963,7 @@ struct DecWS {
   float *WihTp, *WhhT, *W2mT, *W2lT, *W1catT, *W1oT, *Wf2hT;
   // forward stash
   float *FS, *Hinit, *Xin, *Hprev, *Cprev, *Gst, *Cst, *Hs, *Aact, *MU, *LV, *OUT, *Zo, *offlog, *dlog_raw, *bce;
+  float* EPS;  // the Philox decoder noise, rows x F (philox_normal_fill)
   float* dWb;  // [dW_ih | db] of the cell (bias column folded into the GEMM)
   double* part;
   // backward
@@ -993,6 +1003,7 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
   w.Cst = G == 4 ? A.f((size_t)L * H) : nullptr;
   w.Hs = A.f((size_t)L * H); w.Aact = A.f((size_t)L * 2 * Hm);
   w.MU = A.f((size_t)L * Fp); w.LV = A.f((size_t)L * Fp); w.OUT = A.f((size_t)L * Fp);
+  w.EPS = A.f((size_t)L * F);
   w.Zo = A.f((size_t)L * Hm); w.offlog = A.f(L); w.dlog_raw = A.f(L); w.bce = A.f(L);
   w.part = A.d(2048);
   w.dGX = A.f((size_t)L * GH);
@@ -1013,6 +1024,10 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
 }
 
 static int launch_grid(long n) { return (int)std::max<long>(1, std::min<long>(4096, cdiv(n, 256))); }
+static bool dec_eps_fill() {
+  const char* v = getenv("ABCD_DEC_EPSFILL");
+  return !(v && v[0] == '0');
+}
 
 }  // namespace abcd
 
@@ -1169,13 +1184,18 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
   bool done = false;
   {
     PDecFwdArgs pa{};
-    pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS); pa.L = L; pa.B = B;
+    pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS);
     pa.feedback = c->feedback;
     pa.off = w.off; pa.sync = w.sync;
     pa.Wih = w.Wihp; pa.Whh = cw.w_hh; pa.bias = G == 4 ? w.bcomb : w.bgru;
     pa.W1 = w.W1cat; pa.b1 = w.b1cat;
     pa.W2m = w.W2mp; pa.W2l = w.W2lp; pa.b2m = w.b2mp; pa.b2l = w.b2lp;
     pa.eps = eps; pa.seed = seed; pa.offset = offset; pa.xmask = xmask;
+    if (!eps && persist_enabled() && dec_eps_fill()) {  // Philox noise drawn up front (ABCD_DEC_EPSFILL=0: in-kernel)
+      philox_normal_fill<<<launch_grid((long)L * F), 256, 0, s>>>(w.EPS, (long)L * F, seed, offset);
+      ABCD_CHECK_LAUNCH();
+      pa.eps = w.EPS;
+    }
     pa.Xin = w.Xin; pa.Hprev = w.Hprev; pa.Cprev = w.Cprev; pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Hs = w.Hs;
     pa.Aact = w.Aact; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
     if (persist_enabled()) ABCD_TRY((hipError_t)stage_offsets(s, off, w.off));

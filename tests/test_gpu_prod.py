@@ -33,9 +33,6 @@ EXPECT = {
     "GRU": {"enc_fwd": "enc_fwd_persist<3,16,8>", "enc_bwd": "enc_bwd_w8<3>",
             "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_w16<9,GRU>"},
 }
-_DF = "" if os.environ.get("ABCD_DECFWD_DF", "") == "0" else ",DF"  # data-as-flag decoder forward (default)
-for _r in EXPECT:
-    EXPECT[_r]["dec_fwd"] = f"dec_fwd_x6<13,8,8,{_r}{_DF}>"
 
 
 def _noise(inp):
