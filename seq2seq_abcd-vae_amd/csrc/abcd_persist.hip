@@ -1067,11 +1067,10 @@ __global__ __launch_bounds__(256) void dec_fwd_persist(PDecFwdArgs a) {
 // the next step's Hprev rows) -- as two more tiles beside the mlp tile, and
 // carried in registers; step t+1's cell then waits only for x_{t+1} and runs
 // the NCC - 8 input chunks (H = 256: 8 recurrent chunks).
-// LATEH: those two recurrent tiles are multiplied AFTER the mlp publish, from
-// the Hs chunks the mlp tile's product kept in registers (wave_mma_x6_keep /
-// _from): the mlp -> emit hand-off no longer waits for 96 of the phase's 144
-// MFMAs; they run in the emit phase's wait instead.
-template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true, bool LATEH = true>
+// (Multiplying those two tiles after the mlp publish instead, from the Hs
+// chunks kept in registers, measured slower: dec_fwd 2.17 / 2.20 -> 2.29 /
+// 2.33 ms, same box.)
+template <int NCC, int NH32, int NM32, bool GRU = false, bool HPRE = true>
 __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
   const int H = a.H, Hm = a.Hm, Fp = a.Fp, F = a.F, T = a.T;
@@ -1206,16 +1205,11 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     // ---------------- mlp ----------------
     gs.wait(3u * i + 1);
     PSTAMP(2);
-    f4 ka[NH32][2];    // LATEH: this wave's Hs chunks, for the recurrent tiles after the publish
-    bool late = false;
     if (has1) {
       f4 a1[1] = {f4zero()};
       if (row0 < bs) {
         const BufKC Hs{make_rsrc(a.Hs + (size_t)o * H, (uint32_t)bs * H * 4u), (uint32_t)H * 4u};
-        if (LATEH && HPRE && i + 1 < T) {
-          wave_mma_x6_keep<1, NH32, 4>(a1, Hs, row0 + r, B1, NH32, lane, q, mem % NH32, ka);
-          late = true;
-        } else if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
+        if (HPRE && i + 1 < T) {  // + the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
           f4 a3[3] = {f4zero(), f4zero(), f4zero()};
           const f4* const bp[3] = {B1, BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
           wave_mma_x6p<3, NH32, 4>(a3, Hs, row0 + r, bp, lane, q, mem % NH32);
@@ -1234,13 +1228,6 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
             (uint32_t)((row0 + trow) * 2 * Hm + 16 * mem + tcol) * 4u, aq, true);
     }
     gs.publish();
-    if (LATEH && late) {  // the next cell's recurrent tiles (chunks NXC.. of both BC subtiles)
-      f4 a2[2] = {f4zero(), f4zero()};
-      const f4* const bp2[2] = {BC + NXC * 3 * 64, BC + (NCC + NXC) * 3 * 64};
-      wave_mma_x6_from<2, NH32>(a2, ka, bp2, lane, mem % NH32);
-      acch[0] = a2[0];
-      acch[1] = a2[1];
-    }
     PSTAMP(3);
     // ---------------- emit ----------------
     // the mu waves' noise, drawn before the wait (independent of the recurrence)
@@ -2517,13 +2504,13 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   return 0;
 }
 
-template <int NCC, int NH32, int NM32, bool GRU, bool HPRE, bool LATEH>
+template <int NCC, int NH32, int NM32, bool GRU, bool HPRE>
 static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8;
   const size_t lds = (size_t)64 * 16 * 3 * (2 * NCC + NH32 + 2 * NM32) + 2 * 16 * 16 * 4 + 4 * TP_FLOATS * 4;
   const int grid = a.nrt * M;
   bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, LATEH>, grid, lds, &ok));
+  ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE>, grid, lds, &ok));
   if (!ok) return 0;
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
@@ -2531,7 +2518,7 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_DEC_FWD);
-    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE, LATEH><<<grid, 256, lds, s>>>(b);
+    dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_DEC_FWD, "dec_fwd_x6<%d,%d,%d,%s> grid %d", NCC, NH32, NM32, GRU ? "GRU" : "LSTM", grid);
   ABCD_CHECK_LAUNCH();
@@ -2540,13 +2527,9 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
 }
 
 
-// the recurrent tiles after the mlp publish by default; ABCD_DECFWD_LATEH=0
-// keeps them inside the mlp product (same-box A/B)
 template <int NCC, int NH32, int NM32, bool GRU = false>
 static int launch_dec_fwd_x6(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
-  const char* v = getenv("ABCD_DECFWD_LATEH");
-  if (v && v[0] == '0') return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, false>(s, a, launched);
-  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true, true>(s, a, launched);
+  return launch_dec_fwd_x6_k<NCC, NH32, NM32, GRU, true>(s, a, launched);
 }
 
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched) {

@@ -182,86 +182,6 @@ DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch
   }
 }
 
-// wave_mma_x6 that also hands back the raw A chunks it read (ka[c] = loop
-// chunk c, i.e. image chunk (c + rot) mod NCH), so a second product over the
-// same operand (wave_mma_x6_from) needs no second gather.
-template <int NR, int NCH, int PD, class OA>
-DEV void wave_mma_x6_keep(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q, int rot,
-                          f4 (&ka)[NCH][2]) {
-  constexpr int P = PD < NCH ? PD : NCH;
-  auto cc = [&](int c) { const int x = c + rot; return x >= NCH ? x - NCH : x; };
-#pragma unroll
-  for (int p = 0; p < P; ++p) A.frag8(arow, cc(p), q, ka[p][0], ka[p][1]);
-  f4 bw[NR][3];
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bl[((j * nch + cc(0)) * 3 + pl) * 64 + lane];
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    f4 bn[NR][3];
-    if (c + 1 < NCH) {
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bl[((j * nch + cc(c + 1)) * 3 + pl) * 64 + lane];
-    }
-    bf8 a0, a1, a2;
-    split8(ka[c][0], ka[c][1], a0, a1, a2);
-    // the ring is the kept array itself: chunk c + P's loads go to their own slot
-    if (c + P < NCH) A.frag8(arow, cc(c + P), q, ka[c + P][0], ka[c + P][1]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-      acc[j] = mma_x6(acc[j], a0, a1, a2, __builtin_bit_cast(bf8, bw[j][0]), __builtin_bit_cast(bf8, bw[j][1]),
-                      __builtin_bit_cast(bf8, bw[j][2]));
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < NCH) {
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bw[j][pl] = bn[j][pl];
-    }
-  }
-}
-// acc[j] += (kept A) * B_j over the chunks of wave_mma_x6_keep, in the same
-// order (so the sums round exactly as one wave_mma_x6p over both products);
-// B_j chunk k at Bp[j] + k * 3 * 64
-template <int NR, int NCH>
-DEV void wave_mma_x6_from(f4 (&acc)[NR], const f4 (&ka)[NCH][2], const f4* const (&Bp)[NR], int lane, int rot) {
-  auto cc = [&](int c) { const int x = c + rot; return x >= NCH ? x - NCH : x; };
-  f4 bw[NR][3];
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bp[j][(cc(0) * 3 + pl) * 64 + lane];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    f4 bn[NR][3];
-    if (c + 1 < NCH) {
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bp[j][(cc(c + 1) * 3 + pl) * 64 + lane];
-    }
-    bf8 a0, a1, a2;
-    split8(ka[c][0], ka[c][1], a0, a1, a2);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-      acc[j] = mma_x6(acc[j], a0, a1, a2, __builtin_bit_cast(bf8, bw[j][0]), __builtin_bit_cast(bf8, bw[j][1]),
-                      __builtin_bit_cast(bf8, bw[j][2]));
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < NCH) {
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bw[j][pl] = bn[j][pl];
-    }
-  }
-}
-
 // wave_mma_x6 with one image segment per output tile: chunk c of tile j at
 // Bp[j] + c * 3 * 64 (tiles from different LDS images sharing one A operand)
 template <int NR, int NCH, int PD, class OA>
