@@ -406,156 +406,6 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// enc_fwd_ks: enc_fwd_persist<G, 16, 8> (H = 256) with TWO waves per SIMD.
-// enc_fwd_persist's step is one wave per SIMD running, in series, the 16-KiB
-// gather of the Hprev rows, the splits and G x 8 x 6 MFMAs (192 for the LSTM:
-// ~1.3 us of matrix-core time alone).  Here waves w and w + 4 share the row
-// block (rows 16 (w & 3)) and split K: wave w multiplies chunks 0-3, wave
-// w + 4 chunks 4-7 (8 KiB gather, 96 MFMAs each), so the two waves of a SIMD
-// overlap each other's load latency, splits and MFMAs; the K-halves meet in
-// LDS (RX) and the low wave runs the cell update, the hand-off and the
-// stashes as before.  Reference: the bi-LSTM / GRU forward, model.py:53,60-66.
-// ---------------------------------------------------------------------------
-template <int G>
-__global__ __launch_bounds__(512) void enc_fwd_ks(PFwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) f4 smem[];
-  constexpr int H = 256, NCH = 8;
-  const int nut = H / 16, T = a.T;
-  const Role role = assign_role(a.nd * a.nrt, nut);
-  const int grp = role.grp, mem = role.mem;
-  const int dir = grp / a.nrt, rt = grp % a.nrt;
-  const PFwdDir& D = a.d[dir];
-  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 .. 7
-  const int rb = w & 3, kh = w >> 2;                                // row block, K half
-  const int u0 = mem * 16, unit = u0 + r;
-  const int row0 = rt * PERSIST_ROWS + rb * 16;
-  unsigned* cnt = a.sync + grp * PERSIST_SYNC_STRIDE;
-  if (threadIdx.x < 256)
-    stage_x6(smem, D.Whh, H, H, G, NCH, 0, NCH, [&](int j, int rr) { return j * H + u0 + rr; });
-  float bh[G];
-#pragma unroll
-  for (int j = 0; j < G; ++j) bh[j] = (G == 3) ? D.bhh[j * H + unit] : 0.f;
-  f4* RX = smem + (size_t)G * 16 * H * 6 / 16;                   // [4 row blocks][G][64] K-half sums
-  float* tb = reinterpret_cast<float*>(RX + 4 * G * 64) + w * TP_FLOATS;
-  const int trow = lane >> 2, tcol = 4 * (lane & 3);
-  __syncthreads();
-  float st[4] = {0.f, 0.f, 0.f, 0.f};  // c (LSTM) / h (GRU) of the lane's 4 cells (low waves)
-  const int* off = a.off;
-  for (int i = 0; i < T; ++i) {
-    const int t = D.rev ? T - 1 - i : i;
-    const int o = off[t], bs = off[t + 1] - o;
-    int prev_valid, next_off, next_bs;
-    if (D.rev) {
-      prev_valid = t == T - 1 ? 0 : off[t + 2] - off[t + 1];
-      next_off = t >= 1 ? off[t - 1] : 0;
-      next_bs = t >= 1 ? bs : 0;
-    } else {
-      prev_valid = t == 0 ? 0 : bs;
-      next_off = off[t + 1];
-      next_bs = t + 1 < T ? off[t + 2] - off[t + 1] : 0;
-    }
-    PSTAMP(0);
-    float gxp[4][G];
-    {  // the low waves' input projection rows, loaded before the wait
-      const __amdgpu_buffer_rsrc_t rgx =
-          make_rsrc(D.GX + (size_t)o * D.ldgx, kh == 0 ? (uint32_t)bs * D.ldgx * 4u : 0u);
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int j = 0; j < G; ++j) gxp[g][j] = bld(rgx, ((uint32_t)(row0 + 4 * q + g) * D.ldgx + j * H + unit) * 4u);
-    }
-    if (i > 0) group_wait(cnt, (unsigned)(nut * i));
-#pragma unroll
-    for (int g = 0; g < 4; ++g) pin(gxp[g]);
-    PSTAMP(1);
-    f4 acc[G];
-#pragma unroll
-    for (int j = 0; j < G; ++j) acc[j] = f4zero();
-    if (row0 < bs && prev_valid > 0) {
-      const BufKC A{make_rsrc(D.Hprev + (size_t)o * H + kh * (H / 2), (uint32_t)(prev_valid * H - kh * (H / 2)) * 4u),
-                    (uint32_t)H * 4u};
-      wave_mma_x6<G, NCH / 2, 4>(acc, A, row0 + r, smem + kh * (NCH / 2) * 3 * 64, NCH, lane, q);
-    }
-    if (kh == 1) {
-#pragma unroll
-      for (int j = 0; j < G; ++j) RX[(rb * G + j) * 64 + lane] = acc[j];
-    }
-    __syncthreads();
-    if (kh == 0) {
-#pragma unroll
-      for (int j = 0; j < G; ++j) acc[j] += RX[(rb * G + j) * 64 + lane];
-    }
-    PSTAMP(2);
-    float gv[4][4], hv[4], cv[4];
-    if (kh == 0) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int b = row0 + 4 * q + g;
-        const bool haspred = b < prev_valid;
-        if (G == 4) {
-          gv[g][0] = fsigmoid(gxp[g][0] + acc[0][g]);
-          gv[g][1] = fsigmoid(gxp[g][1] + acc[1][g]);
-          gv[g][2] = ftanh(gxp[g][2] + acc[2][g]);
-          gv[g][3] = fsigmoid(gxp[g][3] + acc[3 % G][g]);
-          cv[g] = gv[g][1] * (haspred ? st[g] : 0.f) + gv[g][0] * gv[g][2];
-          hv[g] = gv[g][3] * ftanh(cv[g]);
-          st[g] = cv[g];
-        } else {
-          const float ghr = acc[0][g] + bh[0], ghz = acc[1][g] + bh[1], ghn = acc[2][g] + bh[2 % G];
-          gv[g][0] = fsigmoid(gxp[g][0] + ghr);
-          gv[g][1] = fsigmoid(gxp[g][1] + ghz);
-          gv[g][2] = ftanh(gxp[g][2 % G] + gv[g][0] * ghn);
-          gv[g][3] = ghn;
-          hv[g] = (1.f - gv[g][1]) * gv[g][2] + gv[g][1] * (haspred ? st[g] : 0.f);
-          cv[g] = 0.f;
-          st[g] = hv[g];
-        }
-      }
-      // h -> the next step's operand rows (write-through; rows >= next_bs outside the extent)
-      const uint32_t qh = (uint32_t)((row0 + trow) * H + u0 + tcol) * 4u;
-      const f4 hq = tp_quad(tb, hv, lane);
-      if (row0 < next_bs) st4(make_rsrc(D.Hprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qh, hq, true);
-    }
-    PSTAMP(3);
-    group_publish(cnt);
-    if (kh == 0) {  // stashes and outputs (plain 16-B stores), drained while the next step waits
-      const uint32_t qh = (uint32_t)((row0 + trow) * H + u0 + tcol) * 4u;
-      if (row0 < bs) {
-        const __amdgpu_buffer_rsrc_t rg = make_rsrc(D.Gst + (size_t)o * 4 * H, (uint32_t)bs * 4 * H * 4u);
-        const uint32_t go = (uint32_t)((row0 + trow) * 4 * H + u0 + tcol) * 4u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v[4] = {gv[0][j], gv[1][j], gv[2][j], gv[3][j]};
-          st4(rg, go + (uint32_t)(j * H) * 4u, tp_quad(tb, v, lane), false);
-        }
-        if (G == 4) st4(make_rsrc(D.Cst + (size_t)o * H, (uint32_t)bs * H * 4u), qh, tp_quad(tb, cv, lane), false);
-        if (D.Y)
-          st4(make_rsrc(D.Y + (size_t)o * D.ldy, (uint32_t)bs * D.ldy * 4u),
-              (uint32_t)((row0 + trow) * D.ldy + u0 + tcol) * 4u, tp_quad(tb, hv, lane), false);
-        if (G == 4 && row0 < next_bs)
-          st4(make_rsrc(D.Cprev + (size_t)next_off * H, (uint32_t)next_bs * H * 4u), qh, tp_quad(tb, cv, lane), false);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {  // rows without a predecessor / whose sequence ends here (rare)
-        const int b = row0 + 4 * q + g;
-        if (b >= bs) continue;
-        const long rr = o + b;
-        if (b >= prev_valid) {
-          if (G == 4) D.Cprev[rr * H + unit] = 0.f;
-          D.Hprev[rr * H + unit] = 0.f;
-        }
-        if (b >= next_bs && D.out) {
-          D.out[(long)b * D.ldo + D.hcol + unit] = hv[g];
-          if (G == 4) D.out[(long)b * D.ldo + D.ccol + unit] = cv[g];
-        }
-      }
-    }
-    PSTAMP(4);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // encoder backward (BPTT): one launch per layer, both directions
 // ---------------------------------------------------------------------------
 // fp32 MFMA gather form, for the widths the split-K forms (enc_bwd_w8 at
@@ -2409,7 +2259,7 @@ int stage_offsets(hipStream_t s, const std::vector<int>& off, int* dst) {
 }
 
 template <class K>
-static int fits_resident(K kernel, int grid, size_t lds, bool* ok, int threads = 256) {
+static int fits_resident(K kernel, int grid, size_t lds, bool* ok) {
   *ok = false;
   if (lds > 160 * 1024) return 0;
   // (kernel, LDS bytes, device) -> resident workgroups on the chip; the
@@ -2433,7 +2283,7 @@ static int fits_resident(K kernel, int grid, size_t lds, bool* ok, int threads =
     int cus = 0, per = 0;
     ABCD_TRY(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     ABCD_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    ABCD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kernel, threads, lds));
+    ABCD_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kernel, 256, lds));
     cap = (long)cus * per;
     std::lock_guard<std::mutex> lk(mu);
     cache.push_back({Key{(const void*)kernel, lds, dev}, cap});
@@ -2537,35 +2387,9 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
 }
 
 template <int G>
-static int launch_fwd_ks(hipStream_t s, const PFwdArgs& a, bool* launched) {
-  const int grid = a.nd * a.nrt * (a.H / 16);
-  const size_t lds = (size_t)G * 16 * a.H * 6 + (size_t)4 * G * 64 * 16 + (size_t)8 * TP_FLOATS * 4;
-  bool ok = false;
-  ABCD_TRY((hipError_t)fits_resident(enc_fwd_ks<G>, grid, lds, &ok, 512));
-  if (!ok) return 0;
-  ABCD_TRY(zero_sync(s, a.sync, a.nd * a.nrt));
-  PFwdArgs b = a;
-  b.prof = (g_prof_mask & 1) ? g_prof : nullptr;
-  {
-    TimedScope ts(s, TK_ENC_FWD);
-    enc_fwd_ks<G><<<grid, 512, lds, s>>>(b);
-  }
-  note_dispatch(TK_ENC_FWD, "enc_fwd_ks<%d> grid %d", G, grid);
-  ABCD_CHECK_LAUNCH();
-  *launched = true;
-  return 0;
-}
-// H = 256: the 8-wave K-split form by default; ABCD_ENCFWD_KS=0 keeps
-// enc_fwd_persist (same-box A/B)
-template <int G>
 static int launch_fwd_x6(hipStream_t s, const PFwdArgs& a, bool* launched) {
   if (a.H == 64) return launch_fwd<G, 16, 2>(s, a, launched);
   if (a.H == 128) return launch_fwd<G, 16, 4>(s, a, launched);
-  const char* v = getenv("ABCD_ENCFWD_KS");
-  if (!(v && v[0] == '0')) {
-    const int rc = launch_fwd_ks<G>(s, a, launched);
-    if (rc || *launched) return rc;
-  }
   return launch_fwd<G, 16, 8>(s, a, launched);
 }
 

@@ -39,12 +39,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LOSS_TOL = 1e-4
 GRAD_TOL = 1e-3
 
-# the encoder forward at H = 256: the 8-wave K-split form (default; ABCD_ENCFWD_KS=0: enc_fwd_persist)
-ENC_FWD = ({"LSTM": "enc_fwd_persist<4,16,8>", "GRU": "enc_fwd_persist<3,16,8>"}
-           if os.environ.get("ABCD_ENCFWD_KS", "") == "0" else {"LSTM": "enc_fwd_ks<4>", "GRU": "enc_fwd_ks<3>"})
 KERNELS = {
-    "LSTM": (ENC_FWD["LSTM"], "enc_bwd_w8<4>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
-    "GRU": (ENC_FWD["GRU"], "enc_bwd_w8<3>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_w16<9,GRU>"),
+    "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_w8<4>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
+    "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_w8<3>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_w16<9,GRU>"),
 }
 # the encoder weight-gradient form (ABCD_WG3=0: gemm_wg2; ABCD_WG3W=2/8/4: gemm_wg3; default gemm_wg3b)
 WG_FORM = ("gemm_wg2" if os.environ.get("ABCD_WG3", "") == "0"

@@ -27,13 +27,10 @@ LOSS_TOL = 1e-4
 GRAD_TOL = 1e-3
 
 # the kernels bench.py's configs dispatch at H = Hm = 256, F = 129 (Fp = 144)
-# the encoder forward at H = 256: the 8-wave K-split form (default; ABCD_ENCFWD_KS=0: enc_fwd_persist)
-ENC_FWD = ({"LSTM": "enc_fwd_persist<4,16,8>", "GRU": "enc_fwd_persist<3,16,8>"}
-           if os.environ.get("ABCD_ENCFWD_KS", "") == "0" else {"LSTM": "enc_fwd_ks<4>", "GRU": "enc_fwd_ks<3>"})
 EXPECT = {
-    "LSTM": {"enc_fwd": ENC_FWD["LSTM"], "enc_bwd": "enc_bwd_w8<4>",
+    "LSTM": {"enc_fwd": "enc_fwd_persist<4,16,8>", "enc_bwd": "enc_bwd_w8<4>",
              "dec_fwd": "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd": "dec_bwd_w16<9,LSTM>"},
-    "GRU": {"enc_fwd": ENC_FWD["GRU"], "enc_bwd": "enc_bwd_w8<3>",
+    "GRU": {"enc_fwd": "enc_fwd_persist<3,16,8>", "enc_bwd": "enc_bwd_w8<3>",
             "dec_fwd": "dec_fwd_x6<13,8,8,GRU>", "dec_bwd": "dec_bwd_w16<9,GRU>"},
 }
 
