@@ -8,7 +8,7 @@ TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_prod.py tests/test_gpu_fullshape.py tests/test_gpu_persist.py \
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_prod.py tests/test_gpu_fullshape.py tests/test_gpu_persist.py} \
   -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 grep -E "passed|failed" $OUT/pytest.log | tail -1
 for rep in 1 2; do

@@ -123,6 +123,64 @@ __global__ __launch_bounds__(256) void gemm_ks_kernel(OA A, OB B, int nch, int c
   }
 }
 
+// gemm_tn_batch: gemm_ks_kernel's 32 x 64 tile over the whole K for every
+// tile of every job of the batch, one launch (the sampler's and the decoder
+// initial state's weight gradients: four GEMMs, each 8-128 tiles at K = 512 /
+// 1024, were four split-K launches + four slab reductions).  The job table
+// travels in the kernel arguments; blockIdx.x walks the jobs' tiles in order.
+struct GemmBatchArgs {
+  GemmJob j[GEMM_BATCH_MAX];
+  int tile0[GEMM_BATCH_MAX + 1];  // first tile of each job; tile0[n] = total
+  int n;
+};
+template <int MR, int NR>
+__global__ __launch_bounds__(256) void gemm_tn_batch_kernel(GemmBatchArgs b) {
+  constexpr int TM = 16 * MR, TN = 16 * NR, LD = TN + 4;
+  __shared__ __attribute__((aligned(16))) float lds[4 * TM * LD];
+  int ji = 0;
+  while (ji + 1 < b.n && (int)blockIdx.x >= b.tile0[ji + 1]) ++ji;
+  const GemmJob J = b.j[ji];
+  const int t = (int)blockIdx.x - b.tile0[ji], tn = (J.N + TN - 1) / TN;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int m0 = (t / tn) * TM, n0 = (t % tn) * TN;
+  const KM A{J.A, J.lda, J.M, J.K}, B{J.B, J.ldb, J.N, J.K};
+  int ar[MR], br[NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) ar[i] = m0 + 16 * i + r;
+#pragma unroll
+  for (int j = 0; j < NR; ++j) br[j] = n0 + 16 * j + r;
+  f4 acc[MR][NR];
+  acc_zero(acc);
+  wave_mma<MR, NR>(acc, A, ar, B, br, w, (J.K + 15) / 16, 4, q);
+  reduce_waves_to_lds<MR, NR>(acc, lds, w, lane);
+  const EpiArgs e{J.C, J.ldc, J.M, J.N, J.alpha, J.beta, nullptr, ACT_NONE, nullptr};
+  for (int x = threadIdx.x; x < TM * TN; x += 256) {
+    const int lr = x / TN, lc = x % TN;
+    const int row = m0 + lr, col = n0 + lc;
+    if (row < e.M && col < e.N) e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, lds[lr * LD + lc]);
+  }
+}
+int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
+  if (n <= 0) return 0;
+  if (n > GEMM_BATCH_MAX) return (int)hipErrorInvalidValue;
+  GemmBatchArgs b{};
+  int tiles = 0, k = 0;
+  for (int i = 0; i < n; ++i) {
+    if (jobs[i].M <= 0 || jobs[i].N <= 0) continue;
+    b.j[k] = jobs[i];
+    b.tile0[k] = tiles;
+    tiles += cdiv(jobs[i].M, 32) * cdiv(jobs[i].N, 64);
+    ++k;
+  }
+  b.n = k;
+  b.tile0[k] = tiles;
+  if (!tiles) return 0;
+  gemm_tn_batch_kernel<2, 4><<<tiles, 256, 0, s>>>(b);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
 // Sum of the Z raw split-K slabs + the epilogue.  A thread owns 4 consecutive
 // outputs (one 16-B load per slab when the slabs are 16-B aligned) and keeps
 // SR_DEPTH slabs' loads in flight, adding them in slab order (the same sum as

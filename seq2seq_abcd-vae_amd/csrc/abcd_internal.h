@@ -35,6 +35,20 @@ inline Operand opKM(const float* p, long ld, int nrows) { return Operand{p, ld, 
 
 // C[m][n] = alpha * sum_k A(m,k) B(n,k) + beta * C[m][n] + bias[n], then act.
 // Stores rows < M, cols < N.  `scratch` (may be null) enables split-K slabs.
+// One launch for up to GEMM_BATCH_MAX small GEMMs whose operands are both
+// K-major (the batch-reduction weight gradients, K = the batch's rows):
+// C_j = alpha_j A_j^T B_j + beta_j C_j, A_j element (m, k) at A[k * lda + m],
+// B_j element (n, k) at B[k * ldb + n]; no split-K slabs, no second pass.
+constexpr int GEMM_BATCH_MAX = 8;
+struct GemmJob {
+  const float* A; long lda;
+  const float* B; long ldb;
+  float* C; long ldc;
+  int M, N, K;
+  float alpha, beta;
+};
+int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n);
+
 int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, long ldc, float alpha,
          float beta, const float* bias, int act, float* scratch, size_t scratch_floats);
 

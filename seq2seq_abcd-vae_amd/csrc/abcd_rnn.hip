@@ -415,6 +415,9 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
                                   Inp));
       ABCD_TRY((hipError_t)pk.add(W.b_ih, G * H, 1, G * H, false, w.bcat[l] + d * G * H, G * H, 1, G * H,
                                   G == 4 ? W.b_hh : nullptr));
+      // W_hh^T for the backward pass (read from this workspace by abcd_encoder_backward*),
+      // packed here in the same launch instead of in front of the BPTT
+      ABCD_TRY((hipError_t)pk.add(W.w_hh, H, H, G * H, true, w.WhhT[l][d], G * H, H, G * H));
     }
     ABCD_TRY((hipError_t)pk.flush());
     const float* X = l == 0 ? w.Xp : w.Y[l - 1];
@@ -526,8 +529,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
   // gate that started them DURING the BPTT measured no gain)
   for (int l = c->layers - 1; l >= 0; --l) {
     const int In = l == 0 ? F : D * H;
-    for (int d = 0; d < D; ++d)
-      ABCD_TRY((hipError_t)pack2d(s, p->w[l][d].w_hh, H, H, GH, true, w.WhhT[l][d], GH, H, GH));
+    // w.WhhT[l][d] = W_hh^T: packed by the forward pass into this workspace
     bool done = false;
     {
       PBwdArgs pa{};

@@ -1315,19 +1315,16 @@ static int samp_fused_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* 
   note_dispatch(TK_SAMP_BWD, "samp_head_bwd grid %d + d_h gemm", grid);
   ABCD_TRY((hipError_t)stream_fork(s, sw, 1));
   {
-    SideWork side(s, sw);
-    float* sc = w.scratch;
-    const size_t scf = w.scratch_floats;
-    // dC = [d_feats; U]^T [Y; dL / sqrt(D)]  (the sample and the logits products in one reduction)
-    if (g->codebook)
-      ABCD_TRY((hipError_t)gemm(sw, D, K, 2 * B, opKM(w.FU, D, D), opKM(w.YdL, K, K), g->codebook, K, 1.f, 0.f,
-                                nullptr, ACT_NONE, sc, scf));
-    if (mg.w2)
-      ABCD_TRY((hipError_t)gemm(sw, D, Hm, B, opKM(w.dU, D, D), opKM(w.Z1[0], Hm, Hm), mg.w2, Hm, 1.f, 0.f, nullptr,
-                                ACT_NONE, sc, scf));
-    if (mg.w1)
-      ABCD_TRY((hipError_t)gemm(sw, Hm, E, B, opKM(w.dZ1[0], Hm, Hm), opKM(h, E, E), mg.w1, E, 1.f, 0.f, nullptr,
-                                ACT_NONE, sc, scf));
+    // the three parameter gradients in ONE launch (gemm_tn_batch; four split-K
+    // GEMM + slab-reduction pairs before, ~85 us at c2):
+    // dC = [d_feats; U]^T [Y; dL / sqrt(D)]  (the sample and the logits products in one reduction),
+    // dW2 = dU^T Z1, dW1 = dZ1^T h
+    GemmJob jobs[3];
+    int nj = 0;
+    if (g->codebook) jobs[nj++] = GemmJob{w.FU, D, w.YdL, K, g->codebook, K, D, K, 2 * B, 1.f, 0.f};
+    if (mg.w2) jobs[nj++] = GemmJob{w.dU, D, w.Z1[0], Hm, mg.w2, Hm, D, Hm, B, 1.f, 0.f};
+    if (mg.w1) jobs[nj++] = GemmJob{w.dZ1[0], Hm, h, E, mg.w1, E, Hm, E, B, 1.f, 0.f};
+    ABCD_TRY((hipError_t)gemm_tn_batch(sw, jobs, nj));
   }
   if (d_h)
     ABCD_TRY((hipError_t)gemm(s, B, E, Hm, opKC(w.dZ1[0], Hm, B), opKM(m.w1, E, E), d_h, E, 1.f, 0.f, nullptr,
