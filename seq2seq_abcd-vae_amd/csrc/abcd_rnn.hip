@@ -943,15 +943,6 @@ __global__ void dec_feats_bwd(const float* dFS, int D, int S, int B, const int64
     demb[i] = acc;
   }
 }
-// the decoder's Philox noise of every (row, feature) at once: element e of the
-// stream (seed, offset) is philox_normal(seed, offset + e), the value the
-// decoder forward draws for row e / F, feature e % F -- so the persistent
-// kernel reads it with one load instead of ~1 us of VALU per step on its
-// critical path
-__global__ __launch_bounds__(256) void philox_normal_fill(float* out, long n, uint64_t seed, uint64_t offset) {
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256)
-    out[e] = philox_normal(seed, offset + (uint64_t)e);
-}
 // copy a padded (rows x Fp) stash into a user (rows x F) buffer
 __global__ void unpad_rows(const float* src, int Fp, float* dst, int F, long rows) {
   const long n = rows * F;
@@ -1193,9 +1184,12 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
     pa.W1 = w.W1cat; pa.b1 = w.b1cat;
     pa.W2m = w.W2mp; pa.W2l = w.W2lp; pa.b2m = w.b2mp; pa.b2l = w.b2lp;
     pa.eps = eps; pa.seed = seed; pa.offset = offset; pa.xmask = xmask;
-    if (!eps && persist_enabled() && dec_eps_fill()) {  // Philox noise drawn up front (ABCD_DEC_EPSFILL=0: in-kernel)
-      philox_normal_fill<<<launch_grid((long)L * F), 256, 0, s>>>(w.EPS, (long)L * F, seed, offset);
-      ABCD_CHECK_LAUNCH();
+    // Philox noise drawn up front (abcd_fill_normal: the same philox_normal(seed,
+    // offset + row * F + col) the kernel would draw), read with one load per
+    // element instead of ~1 us of VALU per step on the emit phase's path
+    // (dec_fwd 2.31 -> 2.17 ms at c2).  ABCD_DEC_EPSFILL=0: drawn in-kernel.
+    if (!eps && persist_enabled() && dec_eps_fill()) {
+      ABCD_TRY((hipError_t)abcd_fill_normal(w.EPS, (long)L * F, seed, offset, s));
       pa.eps = w.EPS;
     }
     pa.Xin = w.Xin; pa.Hprev = w.Hprev; pa.Cprev = w.Cprev; pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Hs = w.Hs;

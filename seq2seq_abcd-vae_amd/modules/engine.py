@@ -174,12 +174,11 @@ class FusedStep:
         if enc_noise is not None and self.pad is not None:
             de = self.pad.dims[0]
             enc_noise = [_pad.pad_col_blocks(n, de.dirs, de.H, de.Hp) for n in enc_noise]
-        N.check(L_.abcd_encoder_forward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(h),
-                                                N.ptr(ws_e), ws_e.numel(), st), "encoder forward")
+        # the sampler's and the decoder's draws, in the reference's order, taken
+        # up front: the decoder's Philox block (L x F normals) is then drawn on
+        # the side stream while the encoder runs (VALU work beside a
+        # hand-off-bound kernel) instead of in front of the decoder
         W = ksamp._logit_width()
-        logits = torch.empty(B, W, device=dev)
-        feats = torch.empty(B, self.Dfeat, device=dev)
-        self._inspect(h, feats)  # kept for inspection (encode paths, parity tests)
         if self.plain:
             mode, tau = 0, 1.0
             nt, seed, off = _noise.normal(B, self.sampler._feat_dim(), dev, width=self.Dfeat)
@@ -188,6 +187,20 @@ class FusedStep:
         else:
             mode, tau = N.SAMPLE_GUMBEL, float(self.sampler.temperature)
             nt, seed, off = _noise.gumbel(B, self.sampler._logit_width(), dev, width=W)
+        F = kdec.rnn_cell.cell.input_size
+        pdrop = self.decoder._input_dropout_p() if train else 0.0
+        eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
+        side = self._side_stream()
+        if eps is None:  # Philox mode: eps[row, f] = philox_normal(eseed, eoff + row * F + f)
+            eps = self._workspace("eps", L * F * 4)[:L * F * 4].view(torch.float32)
+            side.wait_stream(torch.cuda.current_stream(dev))  # eps is free (the previous step is queued before)
+            N.check(L_.abcd_fill_normal(N.ptr(eps), L * F, eseed, eoff, N.c_void_p(side.cuda_stream)),
+                    "decoder noise")
+        N.check(L_.abcd_encoder_forward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(h),
+                                                N.ptr(ws_e), ws_e.numel(), st), "encoder forward")
+        logits = torch.empty(B, W, device=dev)
+        feats = torch.empty(B, self.Dfeat, device=dev)
+        self._inspect(h, feats)  # kept for inspection (encode paths, parity tests)
         # feature_sampler(h) -> .sample(logits) -> .kl_divergence(logits, N)
         # (learning.py:149-153): ABCD = the split-K MLP GEMM + one row-tiled
         # sampler-head kernel (logits, Gumbel-softmax, y C^T, KL) per step
@@ -196,20 +209,22 @@ class FusedStep:
                                               N.ptr(sc[KL:KL + 1]),
                                               None if self.plain else N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 2]),
                                               N.ptr(ws_s), ws_s.numel(), st), "sampler")
-        F = kdec.rnn_cell.cell.input_size
-        pdrop = self.decoder._input_dropout_p() if train else 0.0
-        eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
+        torch.cuda.current_stream(dev).wait_stream(side)  # the decoder noise
         spk = None
         if kdec.embed_speaker is not None:
             spk = speakers.to(dev, torch.int64).contiguous()
         gt_off = is_offset.contiguous()
+        # the loss reductions (emission NLL, offset BCE, the total) only feed the
+        # reported scalars: they run on the side stream beside the offset head
+        side_p = N.c_void_p(side.cuda_stream)
         N.check(L_.abcd_decoder_forward_split(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
                                               N.ptr(eps), N.ptr(xmask), eseed, eoff, None, None, None, None,
-                                              N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st, None),
+                                              N.ptr(sc[EM:EM + 2]), N.ptr(ws_d), ws_d.numel(), st, side_p),
                 "decoder forward")
-        N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), Bn, N.ptr(sc[LOSS:LOSS + 1]), st),
-                "total loss")
+        N.check(L_.abcd_total_loss(N.ptr(sc[EM:EM + 2]), N.ptr(sc[KL:KL + 1]), Bn, N.ptr(sc[LOSS:LOSS + 1]),
+                                   side_p), "total loss")
         if not train:
+            torch.cuda.current_stream(dev).wait_stream(side)
             N.check(L_.abcd_step_status(N.ptr(sc[STATUS:STATUS + 1]), st), "step status")
             return sc, self._real_logits(logits)
         inv = self._inv_b(Bn)
@@ -217,10 +232,9 @@ class FusedStep:
         # the decoder's weight-gradient reductions run on a side stream beside
         # the sampler + encoder backward (joined below, before clip + SGD):
         # measured at c2 ~0.5 ms/step shorter than serial (DESIGN.md §3 Streams)
-        side = self._side_stream()
         N.check(L_.abcd_decoder_backward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
                                                  N.ptr(xmask), N.ptr(inv), N.ptr(inv), N.ptr(d_feats), self.dec_g,
-                                                 N.ptr(ws_d), ws_d.numel(), st, N.c_void_p(side.cuda_stream)),
+                                                 N.ptr(ws_d), ws_d.numel(), st, side_p),
                 "decoder backward")
         d_h = torch.empty(B, self.E, device=dev)
         N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
