@@ -123,64 +123,6 @@ __global__ __launch_bounds__(256) void gemm_ks_kernel(OA A, OB B, int nch, int c
   }
 }
 
-// gemm_tn_batch: gemm_ks_kernel's 32 x 64 tile over the whole K for every
-// tile of every job of the batch, one launch (the sampler's and the decoder
-// initial state's weight gradients: four GEMMs, each 8-128 tiles at K = 512 /
-// 1024, were four split-K launches + four slab reductions).  The job table
-// travels in the kernel arguments; blockIdx.x walks the jobs' tiles in order.
-struct GemmBatchArgs {
-  GemmJob j[GEMM_BATCH_MAX];
-  int tile0[GEMM_BATCH_MAX + 1];  // first tile of each job; tile0[n] = total
-  int n;
-};
-template <int MR, int NR>
-__global__ __launch_bounds__(256) void gemm_tn_batch_kernel(GemmBatchArgs b) {
-  constexpr int TM = 16 * MR, TN = 16 * NR, LD = TN + 4;
-  __shared__ __attribute__((aligned(16))) float lds[4 * TM * LD];
-  int ji = 0;
-  while (ji + 1 < b.n && (int)blockIdx.x >= b.tile0[ji + 1]) ++ji;
-  const GemmJob J = b.j[ji];
-  const int t = (int)blockIdx.x - b.tile0[ji], tn = (J.N + TN - 1) / TN;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = lane & 15, q = lane >> 4;
-  const int m0 = (t / tn) * TM, n0 = (t % tn) * TN;
-  const KM A{J.A, J.lda, J.M, J.K}, B{J.B, J.ldb, J.N, J.K};
-  int ar[MR], br[NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i) ar[i] = m0 + 16 * i + r;
-#pragma unroll
-  for (int j = 0; j < NR; ++j) br[j] = n0 + 16 * j + r;
-  f4 acc[MR][NR];
-  acc_zero(acc);
-  wave_mma<MR, NR>(acc, A, ar, B, br, w, (J.K + 15) / 16, 4, q);
-  reduce_waves_to_lds<MR, NR>(acc, lds, w, lane);
-  const EpiArgs e{J.C, J.ldc, J.M, J.N, J.alpha, J.beta, nullptr, ACT_NONE, nullptr};
-  for (int x = threadIdx.x; x < TM * TN; x += 256) {
-    const int lr = x / TN, lc = x % TN;
-    const int row = m0 + lr, col = n0 + lc;
-    if (row < e.M && col < e.N) e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, lds[lr * LD + lc]);
-  }
-}
-int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
-  if (n <= 0) return 0;
-  if (n > GEMM_BATCH_MAX) return (int)hipErrorInvalidValue;
-  GemmBatchArgs b{};
-  int tiles = 0, k = 0;
-  for (int i = 0; i < n; ++i) {
-    if (jobs[i].M <= 0 || jobs[i].N <= 0) continue;
-    b.j[k] = jobs[i];
-    b.tile0[k] = tiles;
-    tiles += cdiv(jobs[i].M, 32) * cdiv(jobs[i].N, 64);
-    ++k;
-  }
-  b.n = k;
-  b.tile0[k] = tiles;
-  if (!tiles) return 0;
-  gemm_tn_batch_kernel<2, 4><<<tiles, 256, 0, s>>>(b);
-  ABCD_CHECK_LAUNCH();
-  return 0;
-}
-
 // Sum of the Z raw split-K slabs + the epilogue.  A thread owns 4 consecutive
 // outputs (one 16-B load per slab when the slabs are 16-B aligned) and keeps
 // SR_DEPTH slabs' loads in flight, adding them in slab order (the same sum as
@@ -285,21 +227,20 @@ DEV dim3 xcd_tile(bool remap) {
   return dim3(i % gx, (i / gx) % gy, i / (gx * gy));
 }
 
+template <int MR, int NR>
+constexpr int tn_lds_floats() { return 2 * 16 * (32 * MR + 4) + 2 * 16 * (32 * NR + 4); }
+// one (32 MR) x (32 NR) output tile at (m0, n0) over K range [kb, ke); the
+// result goes to `dst` (ldd) through the epilogue, or raw when `raw` (a split-K slab)
 template <int MR, int NR, bool AKC = false, bool BKC = false>
-__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict__ A, long lda,
-                                                      const float* __restrict__ B, long ldb, int K, int kps,
-                                                      EpiArgs e, int remap) {
-  const dim3 bid = xcd_tile(remap != 0);
+DEV void gemm_tn_tile(float* smab, const float* __restrict__ A, long lda, const float* __restrict__ B, long ldb,
+                      int kb, int ke, int m0, int n0, const EpiArgs& e, float* dst, long ldd, bool raw) {
   constexpr int BM = 32 * MR, BN = 32 * NR, BK = 16, LA = BM + 4, LB = BN + 4;
   constexpr int AVT = BK * BM / 4, BVT = BK * BN / 4;   // f4 per slab
   constexpr int AV = (AVT + 255) / 256, BV = (BVT + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float smab[2 * BK * LA + 2 * BK * LB];
   float* const As = smab;                  // [2][BK * LA]
   float* const Bs = smab + 2 * BK * LA;    // [2][BK * LB]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
   const int wm = w >> 1, wn = w & 1;
-  const int m0 = bid.y * BM, n0 = bid.x * BN;
-  const int kb = bid.z * kps, ke = min(K, kb + kps);
   const int M = e.M, N = e.N;
   f4 ra[AV], rb[BV];
   // slab element -> (k, row) of f4 x: K-major: 4 rows at one k; K-contiguous: 4 k of one row
@@ -383,8 +324,6 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict
   // row pieces from the accumulator layout
   constexpr int SW = 16 * NR, SP = SW + 4;  // strip width, pitch (16 x SW floats = 64 NR f4 per strip)
   float* stg = smab + w * 16 * SP;
-  float* const dst = e.slab ? e.slab + (long)bid.z * M * N : e.C;
-  const long ldd = e.slab ? (long)N : e.ldc;
   const bool vec = (ldd % 4 == 0) && (((uintptr_t)dst & 15) == 0);
 #pragma unroll
   for (int i = 0; i < MR; ++i) {
@@ -401,7 +340,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict
       const int row = m0 + wm * 16 * MR + 16 * i + lr;
       f4 v = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
       if (row < M) {
-        if (!e.slab) {
+        if (!raw) {
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             if (gcol + t < N) v[t] = apply_epi(e, row, gcol + t, v[t]);
@@ -417,6 +356,63 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+template <int MR, int NR, bool AKC = false, bool BKC = false>
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict__ A, long lda,
+                                                      const float* __restrict__ B, long ldb, int K, int kps,
+                                                      EpiArgs e, int remap) {
+  __shared__ __attribute__((aligned(16))) float smab[tn_lds_floats<MR, NR>()];
+  const dim3 bid = xcd_tile(remap != 0);
+  const int kb = bid.z * kps, ke = min(K, kb + kps);
+  float* const dst = e.slab ? e.slab + (long)bid.z * e.M * e.N : e.C;
+  gemm_tn_tile<MR, NR, AKC, BKC>(smab, A, lda, B, ldb, kb, ke, bid.y * 32 * MR, bid.x * 32 * NR, e, dst,
+                                 e.slab ? (long)e.N : e.ldc, e.slab != nullptr);
+}
+
+// gemm_tn_batch: gemm_tn's LDS-staged tile (64 x 64, fp32 MFMA) over the
+// whole K for every tile of every job of the batch, one launch (the sampler's and the decoder
+// initial state's weight gradients: four GEMMs, each 8-128 tiles at K = 512 /
+// 1024, were four split-K launches + four slab reductions).  The job table
+// travels in the kernel arguments; blockIdx.x walks the jobs' tiles in order.
+struct GemmBatchArgs {
+  GemmJob j[GEMM_BATCH_MAX];
+  int tile0[GEMM_BATCH_MAX + 1];  // first tile of each job; tile0[n] = total
+  int n;
+};
+template <int MR, int NR>
+__global__ __launch_bounds__(256, 2) void gemm_tn_batch_kernel(GemmBatchArgs b) {
+  __shared__ __attribute__((aligned(16))) float smab[tn_lds_floats<MR, NR>()];
+  int ji = 0;
+  while (ji + 1 < b.n && (int)blockIdx.x >= b.tile0[ji + 1]) ++ji;
+  const GemmJob J = b.j[ji];
+  const int t = (int)blockIdx.x - b.tile0[ji], tn = (J.N + 32 * NR - 1) / (32 * NR);
+  const EpiArgs e{J.C, J.ldc, J.M, J.N, J.alpha, J.beta, nullptr, ACT_NONE, nullptr};
+  gemm_tn_tile<MR, NR>(smab, J.A, J.lda, J.B, J.ldb, 0, J.K, (t / tn) * 32 * MR, (t % tn) * 32 * NR, e, J.C, J.ldc,
+                       false);
+}
+int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
+  if (n <= 0) return 0;
+  if (n > GEMM_BATCH_MAX) return (int)hipErrorInvalidValue;
+  GemmBatchArgs b{};
+  int tiles = 0, k = 0;
+  for (int i = 0; i < n; ++i) {
+    if (jobs[i].M <= 0 || jobs[i].N <= 0) continue;
+    // gemm_tn_tile's staging: 16-B loads of 4 rows at one k
+    if (jobs[i].lda % 4 || jobs[i].ldb % 4 || jobs[i].M % 4 || jobs[i].N % 4 || ((uintptr_t)jobs[i].A & 15) ||
+        ((uintptr_t)jobs[i].B & 15))
+      return ABCD_EINVAL;
+    b.j[k] = jobs[i];
+    b.tile0[k] = tiles;
+    tiles += cdiv(jobs[i].M, 64) * cdiv(jobs[i].N, 64);
+    ++k;
+  }
+  b.n = k;
+  b.tile0[k] = tiles;
+  if (!tiles) return 0;
+  gemm_tn_batch_kernel<2, 2><<<tiles, 256, 0, s>>>(b);
+  ABCD_CHECK_LAUNCH();
+  return 0;
 }
 
 template <int MR, int NR, bool AKC = false, bool BKC = false>
