@@ -193,11 +193,22 @@ int abcd_sampler_backward(const abcd_sampler_cfg* cfg, const abcd_sampler_params
  * (d_logits, dU, dZ1, the bias / prior column sums and d posterior_shape_logits
  * in its last tile) + the d_h GEMM on `stream`; codebook / W2 / W1 GEMMs on
  * wgrad_stream.
- * The caller joins wgrad_stream before reading the gradients. */
+ * The caller joins wgrad_stream before reading the gradients.
+ * wgrad_stream == ABCD_DEFER_PARAMS (fused ABCD path only): the codebook / W2
+ * / W1 gradients are not launched; the caller runs
+ * abcd_sampler_backward_params with the same workspace (and h) later -- the
+ * training step queues them after the encoder BPTT, off its critical path. */
+#define ABCD_DEFER_PARAMS ((void*)(intptr_t)-1)
 int abcd_sampler_backward_split(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
                                 int mode, float temperature, double entire_data_size, const float* d_feats,
                                 const float* d_kl, float* d_h, const abcd_sampler_grads* g, void* ws,
                                 size_t ws_bytes, void* stream, void* wgrad_stream);
+/* the deferred codebook / W2 / W1 gradients of a preceding
+ * abcd_sampler_backward_split(..., ABCD_DEFER_PARAMS): one batched launch
+ * (dC = [d_feats; U]^T [Y; dL / sqrt(D)], dW2 = dU^T Z1, dW1 = dZ1^T h) on
+ * `stream`; returns 0 without work when that call took another path. */
+int abcd_sampler_backward_params(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
+                                 const abcd_sampler_grads* g, void* ws, size_t ws_bytes, void* stream);
 /* The same backward split the way autograd sees the three reference methods:
  * sample_backward:  d_feats -> d_logits (written), d_codebook (written, may be NULL)
  *                   (plain: d_feats -> d[mean | log_var])

@@ -1291,6 +1291,27 @@ static int samp_fwd_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p,
   return 0;
 }
 
+// the codebook / W2 / W1 gradients of the fused path, from the workspace its
+// head kernel filled: ONE batched launch (gemm_tn_batch; four split-K GEMM +
+// slab-reduction pairs before, ~85 us at c2)
+// dC = [d_feats; U]^T [Y; dL / sqrt(D)] (the sample and the logits products in one reduction),
+// dW2 = dU^T Z1, dW1 = dZ1^T h
+static int samp_fused_params(const abcd_sampler_cfg* c, const float* h, int B, const abcd_sampler_grads* g,
+                             const SampWS& w, hipStream_t s) {
+  const int E = c->input_size, Hm = c->mlp_hidden, D = c->feature_dim, K = c->num_categories;
+  const abcd_mlp_g& mg = g->mlp[0];
+  GemmJob jobs[3];
+  int nj = 0;
+  if (g->codebook) jobs[nj++] = GemmJob{w.FU, D, w.YdL, K, g->codebook, K, D, K, 2 * B, 1.f, 0.f};
+  if (mg.w2) jobs[nj++] = GemmJob{w.dU, D, w.Z1[0], Hm, mg.w2, Hm, D, Hm, B, 1.f, 0.f};
+  if (mg.w1) jobs[nj++] = GemmJob{w.dZ1[0], Hm, h, E, mg.w1, E, Hm, E, B, 1.f, 0.f};
+  return gemm_tn_batch(s, jobs, nj);
+}
+static bool samp_fused_ok(const abcd_sampler_cfg* c, const float* d_feats, const float* d_kl) {
+  return !c->plain && d_feats && d_kl && c->num_categories <= 1024 &&
+         head_bwd_lds(c->mlp_hidden, c->feature_dim, c->num_categories) <= HEAD_LDS_MAX;
+}
+
 // the fused training-step backward (ABCD, d_feats and d_kl both present):
 // samp_head_bwd + the d_h GEMM on `s`; codebook / W2 / W1 gradients on `sw`
 static int samp_fused_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h, int B, int mode,
@@ -1313,18 +1334,9 @@ static int samp_fused_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* 
   const int grid = cdiv(B, HEAD_ROWS);
   ABCD_TRY((hipError_t)head_dispatch<HeadBwdLaunch>(K, a, grid, lds, s));
   note_dispatch(TK_SAMP_BWD, "samp_head_bwd grid %d + d_h gemm", grid);
-  ABCD_TRY((hipError_t)stream_fork(s, sw, 1));
-  {
-    // the three parameter gradients in ONE launch (gemm_tn_batch; four split-K
-    // GEMM + slab-reduction pairs before, ~85 us at c2):
-    // dC = [d_feats; U]^T [Y; dL / sqrt(D)]  (the sample and the logits products in one reduction),
-    // dW2 = dU^T Z1, dW1 = dZ1^T h
-    GemmJob jobs[3];
-    int nj = 0;
-    if (g->codebook) jobs[nj++] = GemmJob{w.FU, D, w.YdL, K, g->codebook, K, D, K, 2 * B, 1.f, 0.f};
-    if (mg.w2) jobs[nj++] = GemmJob{w.dU, D, w.Z1[0], Hm, mg.w2, Hm, D, Hm, B, 1.f, 0.f};
-    if (mg.w1) jobs[nj++] = GemmJob{w.dZ1[0], Hm, h, E, mg.w1, E, Hm, E, B, 1.f, 0.f};
-    ABCD_TRY((hipError_t)gemm_tn_batch(sw, jobs, nj));
+  if (sw != (hipStream_t)ABCD_DEFER_PARAMS) {
+    ABCD_TRY((hipError_t)stream_fork(s, sw, 1));
+    ABCD_TRY((hipError_t)samp_fused_params(c, h, B, g, w, sw));
   }
   if (d_h)
     ABCD_TRY((hipError_t)gemm(s, B, E, Hm, opKC(w.dZ1[0], Hm, B), opKM(m.w1, E, E), d_h, E, 1.f, 0.f, nullptr,
@@ -1379,8 +1391,10 @@ extern "C" int abcd_sampler_backward_split(const abcd_sampler_cfg* c, const abcd
   SampWS w;
   ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
   hipStream_t s = (hipStream_t)stream;
+  const bool defer = wgrad_stream == ABCD_DEFER_PARAMS;
+  if (defer && !samp_fused_ok(c, d_feats, d_kl)) wgrad_stream = nullptr;  // only the fused path defers
   hipStream_t sw = wgrad_stream ? (hipStream_t)wgrad_stream : s;
-  ABCD_TRY((hipError_t)stream_fork(s, sw, 0));  // d_feats and the forward products
+  if (!defer) ABCD_TRY((hipError_t)stream_fork(s, sw, 0));  // d_feats and the forward products
   const int D = c->feature_dim, K = c->num_categories;
   float* dL = c->plain ? w.dMV + 0 : w.dL;
   int have = 0;
@@ -1391,7 +1405,7 @@ extern "C" int abcd_sampler_backward_split(const abcd_sampler_cfg* c, const abcd
     ABCD_CHECK_LAUNCH();
     dL = w.dL;
     have = 1;
-  } else if (d_feats && d_kl && K <= 1024 && head_bwd_lds(c->mlp_hidden, D, K) <= HEAD_LDS_MAX) {
+  } else if (samp_fused_ok(c, d_feats, d_kl)) {
     return samp_fused_bwd(c, p, h, B, mode, temperature, N, d_feats, d_kl, d_h, g, w, s, sw);
   } else {
     if (d_feats) {
@@ -1410,6 +1424,18 @@ extern "C" int abcd_sampler_backward_split(const abcd_sampler_cfg* c, const abcd
     }
   }
   return samp_fwd_bwd(c, p, h, B, dL, d_h, g, c->plain ? 0 : (d_feats ? 1 : 0), w, s, sw);
+}
+
+extern "C" int abcd_sampler_backward_params(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
+                                            int B, const abcd_sampler_grads* g, void* ws, size_t ws_bytes,
+                                            void* stream) {
+  ABCD_REQUIRE(samp_check(c) == 0 && p && h && g && ws && B > 0);
+  if (c->plain || c->num_categories > 1024 ||
+      head_bwd_lds(c->mlp_hidden, c->feature_dim, c->num_categories) > HEAD_LDS_MAX)
+    return 0;  // the split call ran the unfused path, parameter gradients included
+  SampWS w;
+  ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
+  return samp_fused_params(c, h, B, g, w, (hipStream_t)stream);
 }
 
 extern "C" int abcd_sampler_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h, int B,

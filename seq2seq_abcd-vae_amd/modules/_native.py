@@ -105,6 +105,8 @@ _SIGS = {
     "abcd_sampler_backward_split": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float,
                                             c_double, c_void_p, c_void_p, c_void_p, _P(SamplerGrads), c_void_p,
                                             c_size_t, c_void_p, c_void_p]),
+    "abcd_sampler_backward_params": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, _P(SamplerGrads),
+                                             c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_sample_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_int, c_float, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_kl_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_double, c_void_p, c_int,
@@ -304,6 +306,9 @@ def ptr(t):
 
 def stream():
     return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+DEFER_PARAMS = c_void_p(2 ** 64 - 1)  # abcd_hip.h ABCD_DEFER_PARAMS ((void*)-1)
 
 
 def workspace(nbytes, device):
