@@ -227,14 +227,17 @@ DEV dim3 xcd_tile(bool remap) {
   return dim3(i % gx, (i / gx) % gy, i / (gx * gy));
 }
 
-template <int MR, int NR>
-constexpr int tn_lds_floats() { return 2 * 16 * (32 * MR + 4) + 2 * 16 * (32 * NR + 4); }
+template <int MR, int NR, int BK = 16>
+constexpr int tn_lds_floats() { return 2 * BK * (32 * MR + 4) + 2 * BK * (32 * NR + 4); }
 // one (32 MR) x (32 NR) output tile at (m0, n0) over K range [kb, ke); the
-// result goes to `dst` (ldd) through the epilogue, or raw when `raw` (a split-K slab)
-template <int MR, int NR, bool AKC = false, bool BKC = false>
+// result goes to `dst` (ldd) through the epilogue, or raw when `raw` (a split-K slab).
+// BK: the K depth of one LDS slab (16; 64 for a long K chain on few
+// workgroups: four times the loads in flight per barrier, K-major operands only)
+template <int MR, int NR, bool AKC = false, bool BKC = false, int BK = 16>
 DEV void gemm_tn_tile(float* smab, const float* __restrict__ A, long lda, const float* __restrict__ B, long ldb,
                       int kb, int ke, int m0, int n0, const EpiArgs& e, float* dst, long ldd, bool raw) {
-  constexpr int BM = 32 * MR, BN = 32 * NR, BK = 16, LA = BM + 4, LB = BN + 4;
+  static_assert(BK == 16 || (!AKC && !BKC), "deep slabs for K-major operands only");
+  constexpr int BM = 32 * MR, BN = 32 * NR, LA = BM + 4, LB = BN + 4;
   constexpr int AVT = BK * BM / 4, BVT = BK * BN / 4;   // f4 per slab
   constexpr int AV = (AVT + 255) / 256, BV = (BVT + 255) / 256;
   float* const As = smab;                  // [2][BK * LA]
@@ -302,8 +305,8 @@ DEV void gemm_tn_tile(float* smab, const float* __restrict__ A, long lda, const 
     const float* as = As + cur * BK * LA + wm * 16 * MR + r;
     const float* bs = Bs + cur * BK * LB + wn * 16 * NR + r;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int k = 4 * q + s;
+    for (int s = 0; s < BK / 4; ++s) {
+      const int k = 16 * (s / 4) + 4 * q + (s % 4);
       float a[MR], b[NR];
 #pragma unroll
       for (int i = 0; i < MR; ++i) a[i] = as[k * LA + 16 * i];
@@ -381,15 +384,15 @@ struct GemmBatchArgs {
   int n;
 };
 template <int MR, int NR>
-__global__ __launch_bounds__(256, 2) void gemm_tn_batch_kernel(GemmBatchArgs b) {
-  __shared__ __attribute__((aligned(16))) float smab[tn_lds_floats<MR, NR>()];
+__global__ __launch_bounds__(256) void gemm_tn_batch_kernel(GemmBatchArgs b) {
+  __shared__ __attribute__((aligned(16))) float smab[tn_lds_floats<MR, NR, 64>()];
   int ji = 0;
   while (ji + 1 < b.n && (int)blockIdx.x >= b.tile0[ji + 1]) ++ji;
   const GemmJob J = b.j[ji];
   const int t = (int)blockIdx.x - b.tile0[ji], tn = (J.N + 32 * NR - 1) / (32 * NR);
   const EpiArgs e{J.C, J.ldc, J.M, J.N, J.alpha, J.beta, nullptr, ACT_NONE, nullptr};
-  gemm_tn_tile<MR, NR>(smab, J.A, J.lda, J.B, J.ldb, 0, J.K, (t / tn) * 32 * MR, (t % tn) * 32 * NR, e, J.C, J.ldc,
-                       false);
+  gemm_tn_tile<MR, NR, false, false, 64>(smab, J.A, J.lda, J.B, J.ldb, 0, J.K, (t / tn) * 32 * MR, (t % tn) * 32 * NR,
+                                         e, J.C, J.ldc, false);
 }
 int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
   if (n <= 0) return 0;
