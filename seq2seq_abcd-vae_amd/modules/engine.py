@@ -238,15 +238,18 @@ class FusedStep:
                 "decoder backward")
         d_h = torch.empty(B, self.E, device=dev)
         # the sampler's codebook / W2 / W1 gradients (one batched launch) are
-        # deferred behind the encoder BPTT: in front of it they sat on the d_h ->
-        # enc_bwd chain, beside it (another stream) they delay its residency
+        # deferred behind the encoder's backward: in front of the BPTT they sat
+        # on the d_h -> enc_bwd chain beside the decoder's weight gradients
+        # (59-85 us there, 31-36 us on a quiet chip), and on a stream of their
+        # own or the side stream they delay the BPTT's residency or queue
+        # behind the side stream's tail (DESIGN.md s3 Streams)
         N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
                                                float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
                                                self.samp_g, N.ptr(ws_s), ws_s.numel(), st, N.DEFER_PARAMS),
                 "sampler backward")
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
-                                                 self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
-                                                 N.c_void_p(side.cuda_stream)), "encoder backward")
+                                                 self.enc_g, N.ptr(ws_e), ws_e.numel(), st, side_p),
+                "encoder backward")
         N.check(L_.abcd_sampler_backward_params(self.samp_cfg, self.samp_p, N.ptr(h), B, self.samp_g, N.ptr(ws_s),
                                                 ws_s.numel(), st), "sampler parameter gradients")
         torch.cuda.current_stream(dev).wait_stream(side)
