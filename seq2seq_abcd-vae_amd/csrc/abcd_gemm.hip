@@ -2155,6 +2155,115 @@ int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const 
   return 0;
 }
 
+// colsum_batch: up to COLSUM_BATCH_MAX column sums in one pass-1 and one
+// pass-2 launch (the decoder backward's bias gradients: seven pairs of
+// launches before).  Each job keeps colsum()'s slicing, so its sum is the
+// same, bit for bit.
+struct ColsumBatchArgs {
+  ColsumJob j[COLSUM_BATCH_MAX];
+  int slices[COLSUM_BATCH_MAX], rows_per[COLSUM_BATCH_MAX];
+  long part0[COLSUM_BATCH_MAX];    // offset of the job's partials in `part`
+  int b1[COLSUM_BATCH_MAX + 1];    // first pass-1 block of each job (blocks = column blocks x slices)
+  int b2[COLSUM_BATCH_MAX + 1];    // first pass-2 block (column blocks)
+  int n;
+  float* part;
+};
+__global__ __launch_bounds__(256) void colsum_batch_pass1(ColsumBatchArgs a) {
+  __shared__ float sh[4][64];
+  int ji = 0;
+  while (ji + 1 < a.n && (int)blockIdx.x >= a.b1[ji + 1]) ++ji;
+  const ColsumJob J = a.j[ji];
+  const int cb = (J.ncols + 63) / 64, t = (int)blockIdx.x - a.b1[ji];
+  const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = (t % cb) * 64 + cg, sl = t / cb;
+  const int r0 = sl * a.rows_per[ji], r1 = min(J.nrows, r0 + a.rows_per[ji]);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < J.ncols) {
+    const float* w = J.w;
+    const float* Z = J.Z;
+    const long ldz = J.ldz;
+    int r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      s0 += (w ? w[r] : 1.f) * Z[(long)r * ldz + j];
+      s1 += (w ? w[r + 4] : 1.f) * Z[(long)(r + 4) * ldz + j];
+      s2 += (w ? w[r + 8] : 1.f) * Z[(long)(r + 8) * ldz + j];
+      s3 += (w ? w[r + 12] : 1.f) * Z[(long)(r + 12) * ldz + j];
+    }
+    for (; r < r1; r += 4) s0 += (w ? w[r] : 1.f) * Z[(long)r * ldz + j];
+  }
+  sh[rg][cg] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (rg == 0 && j < J.ncols)
+    a.part[a.part0[ji] + (long)sl * J.ncols + j] = (sh[0][cg] + sh[1][cg]) + (sh[2][cg] + sh[3][cg]);
+}
+__global__ __launch_bounds__(256) void colsum_batch_pass2(ColsumBatchArgs a) {
+  __shared__ float sh[4][64];
+  int ji = 0;
+  while (ji + 1 < a.n && (int)blockIdx.x >= a.b2[ji + 1]) ++ji;
+  const ColsumJob J = a.j[ji];
+  const int cg = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int j = ((int)blockIdx.x - a.b2[ji]) * 64 + cg, nsl = a.slices[ji];
+  const float* part = a.part + a.part0[ji];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < J.ncols) {
+    int z = sg;
+    for (; z + 12 < nsl; z += 16) {
+      s0 += part[(long)z * J.ncols + j];
+      s1 += part[(long)(z + 4) * J.ncols + j];
+      s2 += part[(long)(z + 8) * J.ncols + j];
+      s3 += part[(long)(z + 12) * J.ncols + j];
+    }
+    for (; z < nsl; z += 4) s0 += part[(long)z * J.ncols + j];
+  }
+  sh[sg][cg] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (sg == 0 && j < J.ncols) {
+    const float v = (sh[0][cg] + sh[1][cg]) + (sh[2][cg] + sh[3][cg]);
+    J.out[j] = (J.beta != 0.f ? J.beta * J.out[j] : 0.f) + v;
+    if (J.out2) J.out2[j] = (J.beta != 0.f ? J.beta * J.out2[j] : 0.f) + v;
+  }
+}
+int colsum_batch(hipStream_t s, const ColsumJob* jobs, int n, float* scratch, size_t scratch_floats) {
+  if (n <= 0) return 0;
+  if (n > COLSUM_BATCH_MAX) return (int)hipErrorInvalidValue;
+  ColsumBatchArgs a{};
+  long used = 0;
+  int k = 0, nb1 = 0, nb2 = 0;
+  for (int i = 0; i < n; ++i) {
+    const ColsumJob& J = jobs[i];
+    if (J.ncols <= 0) continue;
+    const int cblocks = cdiv(J.ncols, 64);
+    // colsum()'s slicing, with the scratch shared by the jobs
+    int slices = std::max(1, std::min(cdiv(std::max(J.nrows, 1), 16), std::max(1, 1024 / cblocks)));
+    slices = std::min(slices, 256);
+    const long left = (long)scratch_floats - used;
+    if (left < J.ncols) return (int)hipErrorInvalidValue;
+    slices = (int)std::max<long>(1, std::min<long>(slices, left / J.ncols));
+    const int rows_per = cdiv(std::max(J.nrows, 1), slices);
+    slices = std::max(1, cdiv(std::max(J.nrows, 1), rows_per));
+    a.j[k] = J;
+    a.slices[k] = slices;
+    a.rows_per[k] = rows_per;
+    a.part0[k] = used;
+    a.b1[k] = nb1;
+    a.b2[k] = nb2;
+    used += (long)slices * J.ncols;
+    nb1 += cblocks * slices;
+    nb2 += cblocks;
+    ++k;
+  }
+  if (!k) return 0;
+  a.n = k;
+  a.b1[k] = nb1;
+  a.b2[k] = nb2;
+  a.part = scratch;
+  colsum_batch_pass1<<<nb1, 256, 0, s>>>(a);
+  ABCD_CHECK_LAUNCH();
+  colsum_batch_pass2<<<nb2, 256, 0, s>>>(a);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // layout copies (padding / transposition of weight compute copies)
 // ---------------------------------------------------------------------------

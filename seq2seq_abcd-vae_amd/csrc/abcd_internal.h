@@ -57,6 +57,17 @@ int gemm_slabs(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* 
 
 // out[j] (+)= sum_r w[r] * Z[r*ldz + j]  (w == null -> 1), j < ncols, r < nrows; deterministic.
 // out2 (optional) receives the same sum with the same beta (e.g. b_ih and b_hh of an LSTM).
+// several colsum() jobs in one pass-1 + one pass-2 launch (each job sliced
+// exactly as colsum() slices it: the same sums); scratch holds every job's
+// partials (at most 256 x ncols each)
+constexpr int COLSUM_BATCH_MAX = 8;
+struct ColsumJob {
+  const float* Z; long ldz; int nrows, ncols;
+  const float* w;     // row weights, or null
+  float* out; float beta;
+  float* out2;        // a second destination, or null
+};
+int colsum_batch(hipStream_t s, const ColsumJob* jobs, int n, float* scratch, size_t scratch_floats);
 int colsum(hipStream_t s, const float* Z, long ldz, int nrows, int ncols, const float* w, float* out,
            float beta, float* scratch, size_t scratch_floats, float* out2 = nullptr);
 

@@ -1446,25 +1446,36 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
     if (cg.b_ih) ABCD_TRY((hipError_t)colsum(s, w.dGX, GH, L, GH, nullptr, cg.b_ih, 0.f, sc, scf));
     if (cg.b_hh) ABCD_TRY((hipError_t)colsum(s, w.dGH, GH, L, GH, nullptr, cg.b_hh, 0.f, sc, scf));
   }
+  // the emission MLPs' and the offset head's bias gradients (and the offset
+  // head's w2 = Zo^T dlog) as ONE batched column sum (seven pass-1 / pass-2
+  // pairs before), queued in front of their weight GEMMs so that a GEMM, not a
+  // string of small reductions, ends the side stream's work
   const abcd_mlp_g* em[2] = {&g->mu, &g->lv};
   const float* dout[2] = {w.dMU, w.dLV};
+  const abcd_mlp_g& og = g->offset;
+  {
+    ColsumJob cj[COLSUM_BATCH_MAX];
+    int ncj = 0;
+    for (int k = 0; k < 2; ++k) {
+      if (em[k]->b2) cj[ncj++] = ColsumJob{dout[k], Fp, L, F, nullptr, em[k]->b2, 0.f, nullptr};
+      if (em[k]->b1) cj[ncj++] = ColsumJob{w.dZ + k * Hm, 2 * Hm, L, Hm, nullptr, em[k]->b1, 0.f, nullptr};
+    }
+    if (og.b1) cj[ncj++] = ColsumJob{w.dZo, Hm, L, Hm, nullptr, og.b1, 0.f, nullptr};
+    if (og.w2) cj[ncj++] = ColsumJob{w.Zo, Hm, L, Hm, w.dlog_s, og.w2, 0.f, nullptr};
+    if (og.b2) cj[ncj++] = ColsumJob{w.dlog_s, 1, L, 1, nullptr, og.b2, 0.f, nullptr};
+    ABCD_TRY((hipError_t)colsum_batch(s, cj, ncj, sc, scf));
+  }
   for (int k = 0; k < 2; ++k) {
     const abcd_mlp_g& mg = *em[k];
     if (mg.w2)
       ABCD_TRY((hipError_t)gemm(s, F, Hm, L, opKM(dout[k], Fp, F), opKM(w.Aact + k * Hm, 2 * Hm, Hm), mg.w2, Hm, 1.f,
                                 0.f, nullptr, ACT_NONE, sc, scf));
-    if (mg.b2) ABCD_TRY((hipError_t)colsum(s, dout[k], Fp, L, F, nullptr, mg.b2, 0.f, sc, scf));
     if (mg.w1)
       ABCD_TRY((hipError_t)gemm(s, Hm, H, L, opKM(w.dZ + k * Hm, 2 * Hm, Hm), opKM(w.Hs, H, H), mg.w1, H, 1.f, 0.f,
                                 nullptr, ACT_NONE, sc, scf));
-    if (mg.b1) ABCD_TRY((hipError_t)colsum(s, w.dZ + k * Hm, 2 * Hm, L, Hm, nullptr, mg.b1, 0.f, sc, scf));
   }
-  const abcd_mlp_g& og = g->offset;
   if (og.w1)
     ABCD_TRY((hipError_t)gemm(s, Hm, H, L, opKM(w.dZo, Hm, Hm), opKM(w.Hs, H, H), og.w1, H, 1.f, 0.f, nullptr,
                               ACT_NONE, sc, scf));
-  if (og.b1) ABCD_TRY((hipError_t)colsum(s, w.dZo, Hm, L, Hm, nullptr, og.b1, 0.f, sc, scf));
-  if (og.w2) ABCD_TRY((hipError_t)colsum(s, w.Zo, Hm, L, Hm, w.dlog_s, og.w2, 0.f, sc, scf));
-  if (og.b2) ABCD_TRY((hipError_t)colsum(s, w.dlog_s, 1, L, 1, nullptr, og.b2, 0.f, sc, scf));
   return 0;
 }
