@@ -266,7 +266,9 @@ int abcd_decoder_forward(const abcd_decoder_cfg* cfg, const abcd_decoder_params*
                          float* log_var, float* offset_logits, float* losses, void* ws, size_t ws_bytes,
                          void* stream);
 /* backward w.r.t. losses[0] (scaled by *d_em) and losses[1] (scaled by *d_off);
- * d_em/d_off are device scalars; d_features: B x feature_size (may be NULL). */
+ * d_em/d_off are device scalars; d_features: B x feature_size (may be NULL).
+ * ws must hold the abcd_decoder_forward of the same inputs and parameters
+ * (its stashes and its packed weight layouts, transposed ones included). */
 int abcd_decoder_backward(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
                           const float* features, const int64_t* speakers, const float* gt_offset,
                           const float* d_em, const float* d_off, float* d_features,

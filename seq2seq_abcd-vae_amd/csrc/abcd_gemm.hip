@@ -2289,31 +2289,50 @@ int pack2d(hipStream_t s, const float* src, long lds, int sr, int sc, bool trans
 // several pack2d / add_vec jobs in ONE launch (blockIdx.y = job): the
 // per-step weight re-layouts of a module are ~10 tiny kernels otherwise,
 // each paying a ~5 us launch slot on the step's critical path
+// One launch for a list of pad / transpose copies.  A thread owns 4 adjacent
+// destination columns of a row (one 16-B store where the row is aligned: the
+// frame pad writes L x Fp floats per step); 32-bit index arithmetic (the
+// host checks dr * dc < 2^31).
 __global__ void pack_many_kernel(PackList pl) {
   const PackJob& j = pl.j[blockIdx.y];
-  const long n = (long)j.dr * j.dc;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int r = (int)(i / j.dc), c = (int)(i % j.dc);
-    float v = 0.f;
-    if (r < j.sr && c < j.sc) {
-      const long o = j.trans ? (long)c * j.lds + r : (long)r * j.lds + c;
-      v = j.src[o];
-      if (j.src2) v += j.src2[o];
+  const int cq = (j.dc + 3) >> 2;
+  const int n = j.dr * cq;
+  const bool vec = ((j.ldd & 3) == 0) && ((reinterpret_cast<uintptr_t>(j.dst) & 15) == 0);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = i / cq, c0 = (i - r * cq) * 4;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = c0 + k;
+      v[k] = 0.f;
+      if (r < j.sr && c < j.sc) {
+        const long o = j.trans ? (long)c * j.lds + r : (long)r * j.lds + c;
+        v[k] = j.src[o];
+        if (j.src2) v[k] += j.src2[o];
+      }
     }
-    j.dst[(long)r * j.ldd + c] = v;
+    float* d = j.dst + (long)r * j.ldd + c0;
+    if (vec && c0 + 4 <= j.dc) {
+      *reinterpret_cast<f4*>(d) = f4{v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c0 + k < j.dc) d[k] = v[k];
+    }
   }
 }
 int Packs::add(const float* src, long lds, int sr, int sc, bool trans, float* dst, long ldd, int dr, int dc,
                const float* src2) {
   if ((long)dr * dc <= 0) return 0;
+  if ((long)dr * (dc + 3) >= (1L << 31)) return ABCD_EINVAL;  // the kernel's 32-bit indices
   if (pl.n == ABCD_PACK_MAX) ABCD_TRY((hipError_t)flush());
   pl.j[pl.n++] = PackJob{src, src2, lds, dst, ldd, sr, sc, dr, dc, trans ? 1 : 0};
-  maxn = std::max(maxn, (long)dr * dc);
+  maxn = std::max(maxn, (long)dr * ((dc + 3) / 4));
   return 0;
 }
 int Packs::flush() {
   if (pl.n == 0) return 0;
-  const int gx = (int)std::min<long>(1024, cdiv(maxn, 256));
+  const int gx = (int)std::min<long>(2048, cdiv(maxn, 256));
   pack_many_kernel<<<dim3(gx, pl.n), 256, 0, s>>>(pl);
   ABCD_CHECK_LAUNCH();
   pl.n = 0;

@@ -83,7 +83,7 @@ int mul_vec(hipStream_t s, const float* a, const float* b, float* y, long n);
 
 // A queue of pack2d jobs (optionally dst = src + src2, same layout) issued as
 // one launch by flush() -- or earlier, when the queue is full.
-constexpr int ABCD_PACK_MAX = 12;
+constexpr int ABCD_PACK_MAX = 24;
 struct PackJob {
   const float *src, *src2;
   long lds;

@@ -1920,9 +1920,17 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
 constexpr int W8_ROWS = 32;   // rows per group
 constexpr int W8_M = 8;       // members per group (32 units each)
 constexpr int W8_DTP = 132;   // pitch (floats) of the member's 32 x 4*32 dG tile in LDS
+// The encoder BPTT shares its CUs with the decoder's weight-gradient GEMMs
+// (side stream): its waves win the issue arbitration (s_setprio; the GEMM
+// waves stay at 0).  Same-box A/B at c2: enc_bwd 1.70 -> 1.66 ms, step 8.676
+// -> 8.652 ms (three alternating pairs, each faster).
+#ifndef ABCD_BWD_PRIO
+#define ABCD_BWD_PRIO 3
+#endif
 template <int G>
 __global__ __launch_bounds__(256) void enc_bwd_w8(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  if (ABCD_BWD_PRIO) __builtin_amdgcn_s_setprio(ABCD_BWD_PRIO);
   constexpr int H = 256, GH = G * H, M = W8_M, NSUB = H / 16;
   constexpr int NC = G;                     // 32-deep chunks = gates
   constexpr int NCR = 2, NCL = NC - NCR;    // chunks of the image in registers / in LDS

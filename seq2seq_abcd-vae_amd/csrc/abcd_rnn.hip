@@ -1160,6 +1160,16 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
     ABCD_TRY((hipError_t)pk.add(p->lv.w2, Hm, F, Hm, false, w.W2lp, Hm, Fp, Hm));
     ABCD_TRY((hipError_t)pk.add(p->mu.b2, F, 1, F, false, w.b2mp, Fp, 1, Fp));
     ABCD_TRY((hipError_t)pk.add(p->lv.b2, F, 1, F, false, w.b2lp, Fp, 1, Fp));
+    // the backward's transposed weights, in the same launch (off the
+    // decoder-forward -> decoder-backward chain)
+    ABCD_TRY((hipError_t)pk.add(cw.w_ih, F, F, GH, true, w.WihTp, GH, Fp, GH));  // rows >= F zero
+    ABCD_TRY((hipError_t)pk.add(cw.w_hh, H, H, GH, true, w.WhhT, GH, H, GH));
+    ABCD_TRY((hipError_t)pk.add(p->mu.w2, Hm, Hm, F, true, w.W2mT, Fp, Hm, Fp));
+    ABCD_TRY((hipError_t)pk.add(p->lv.w2, Hm, Hm, F, true, w.W2lT, Fp, Hm, Fp));
+    ABCD_TRY((hipError_t)pk.add(p->mu.w1, H, H, Hm, true, w.W1catT, 2 * Hm, H, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->lv.w1, H, H, Hm, true, w.W1catT + Hm, 2 * Hm, H, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->offset.w1, H, H, Hm, true, w.W1oT, Hm, H, Hm));
+    ABCD_TRY((hipError_t)pk.add(p->f2h_w, DS, DS, Htot, true, w.Wf2hT, Htot, DS, Htot));
     ABCD_TRY((hipError_t)pk.flush());
   }
   // ---- feature2hidden -> initial state ----
@@ -1309,22 +1319,11 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
   const int T = x->T, L = x->L, B = x->B;
   const int64_t* bs = x->batch_sizes;
   const std::vector<int> off = step_offsets(bs, T);
-  const abcd_rnn_w& cw = p->cell;
   float* sc = w.scratch;
   const size_t scf = w.scratch_floats;
-  // ---- derived transposed weights for the backward GEMMs ----
-  {
-    Packs pk(s);
-    ABCD_TRY((hipError_t)pk.add(cw.w_ih, F, F, GH, true, w.WihTp, GH, Fp, GH));  // rows >= F zero
-    ABCD_TRY((hipError_t)pk.add(cw.w_hh, H, H, GH, true, w.WhhT, GH, H, GH));
-    ABCD_TRY((hipError_t)pk.add(p->mu.w2, Hm, Hm, F, true, w.W2mT, Fp, Hm, Fp));
-    ABCD_TRY((hipError_t)pk.add(p->lv.w2, Hm, Hm, F, true, w.W2lT, Fp, Hm, Fp));
-    ABCD_TRY((hipError_t)pk.add(p->mu.w1, H, H, Hm, true, w.W1catT, 2 * Hm, H, Hm));
-    ABCD_TRY((hipError_t)pk.add(p->lv.w1, H, H, Hm, true, w.W1catT + Hm, 2 * Hm, H, Hm));
-    ABCD_TRY((hipError_t)pk.add(p->offset.w1, H, H, Hm, true, w.W1oT, Hm, H, Hm));
-    ABCD_TRY((hipError_t)pk.add(p->f2h_w, DS, DS, Htot, true, w.Wf2hT, Htot, DS, Htot));
-    ABCD_TRY((hipError_t)pk.flush());
-  }
+  // (the transposed weights of the backward GEMMs were packed by the forward
+  // pass, in its one pack launch: the backward reads the forward's stashes
+  // from the same workspace anyway)
   // ---- offset head backward (batched over all frames) ----
   dec_offset_bwd<<<launch_grid((long)L * Hm), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, w.dlog_raw, d_off, w.dZo,
                                                            w.dlog_s);
