@@ -156,8 +156,56 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* slab, int
     }
   }
 }
+// The same sum with the slabs split over ZG thread groups: a workgroup owns
+// 256 / ZG output quads, group g adds the contiguous slab range g of each in
+// slab order, and the ZG partials are added in group order through LDS
+// (deterministic).  For many slabs over a small output (the emission MLPs'
+// dW2: 129 x 256 outputs, 125 slabs) the one-group form ran 33 workgroups,
+// each thread ~16 dependent round trips: 50-55 us for 16.5 MB.
+template <int ZG>
+__global__ __launch_bounds__(256) void slab_reduce_zg_kernel(const float* slab, int Z, EpiArgs e) {
+  constexpr int QB = 256 / ZG;
+  __shared__ f4 part[256];
+  const long n = (long)e.M * e.N, nq = n / 4;
+  const int g = threadIdx.x / QB, ql = threadIdx.x % QB;
+  const long i = (long)blockIdx.x * QB + ql;
+  const int zper = (Z + ZG - 1) / ZG, zb = g * zper, ze = min(Z, zb + zper);
+  f4 s = f4zero();
+  if (i < nq) {
+    for (int z0 = zb; z0 < ze; z0 += SR_DEPTH) {
+      f4 v[SR_DEPTH];
+#pragma unroll
+      for (int k = 0; k < SR_DEPTH; ++k)
+        v[k] = z0 + k < ze ? *reinterpret_cast<const f4*>(slab + (long)(z0 + k) * n + 4 * i) : f4zero();
+#pragma unroll
+      for (int k = 0; k < SR_DEPTH; ++k) s += v[k];
+    }
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (g == 0 && i < nq) {
+#pragma unroll
+    for (int gg = 1; gg < ZG; ++gg) s += part[gg * QB + ql];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const long j = 4 * i + t;
+      const int row = (int)(j / e.N), col = (int)(j % e.N);
+      e.C[(long)row * e.ldc + col] = apply_epi(e, row, col, s[t]);
+    }
+  }
+}
 static int slab_reduce(hipStream_t s, const float* slab, int Z, const EpiArgs& e) {
-  const long n = (long)e.M * e.N;
+  const long n = (long)e.M * e.N, nq = n / 4;
+  if (n % 4 == 0 && ((uintptr_t)slab & 15) == 0 && Z >= 4) {
+    // the fewest thread groups per quad that give >= 512 workgroups (2 per CU)
+    if (nq >= 512 * 64 || Z < 16) {
+      slab_reduce_zg_kernel<4><<<(int)cdiv(nq, 64), 256, 0, s>>>(slab, Z, e);
+    } else {
+      slab_reduce_zg_kernel<16><<<(int)cdiv(nq, 16), 256, 0, s>>>(slab, Z, e);
+    }
+    ABCD_CHECK_LAUNCH();
+    return 0;
+  }
   slab_reduce_kernel<<<(int)std::max<long>(1, std::min<long>(2048, cdiv(n / 4 + 1, 256))), 256, 0, s>>>(slab, Z, e);
   ABCD_CHECK_LAUNCH();
   return 0;
