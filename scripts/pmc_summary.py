@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel PMC summary of scripts/pmc_gemm.sh output: counter totals per
+"""Per-kernel PMC summary of scripts/pmc_step_kernel.sh output: counter totals per
 dispatch of the longest kernel.  usage: pmc_summary.py <outdir>"""
 import csv
 import glob

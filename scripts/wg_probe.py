@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Times abcd_lstm_wgrad (the encoder's layer-0 weight gradients, both
-directions, gemm_wg2 or gemm_wg3 by ABCD_WG3) at the c2 shape (F = 129,
+directions, gemm_wg2 or gemm_wg3b by ABCD_WG3) at the c2 shape (F = 129,
 H = 256, K = 64077 frames) with HIP events: 20 launches after 3 warm-up ones,
 for each ABCD_WG3 value given on the command line (default "0 1")."""
 import ctypes

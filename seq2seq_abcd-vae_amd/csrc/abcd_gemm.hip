@@ -1395,50 +1395,24 @@ __global__ __launch_bounds__(256) void wg2_reduce_kernel(const float* slab, int 
 }
 
 // ---------------------------------------------------------------------------
-// gemm_wg3: gemm_wg2's product with every operand split ONCE, in the staging
-// pass, and no VALU in the MFMA loop.  gemm_wg2 (above) keeps fp32 in LDS and
-// each wave splits the fragments it reads -- the A rows and the B columns
-// twice per workgroup, ~800 VALU per 32-deep chunk per wave against 312 MFMAs
-// whose issue gaps hide ~620 -- so its MFMA pipe idles about half the time
-// (PMC r07).  Here each thread splits the f4s it loaded into three bf16
-// planes stored [plane][k][col] with a k-row pitch that is an odd multiple of
-// 32 B, and the MFMA loop reads its operands with ds_read_b64_tr_b16 (4
-// k-rows x 16 columns per 16-lane group, delivered column-major).  The
-// 16-lane group g of a fragment reads k-rows 4g .. 4g + 3 and 16 + 4g ..
-// 16 + 4g + 3 (one permutation of k for both operands, so the sum is
-// unchanged), which puts the 8 rows of a 32-lane half on 8 distinct 32-B
-// bank slots: conflict-free.
-//   Tile 128 gate rows x one HALF of the NT = N1 + N2 columns (13 blocks of
-// 16; the two halves of a row tile are adjacent workgroups on one XCD, so
-// the second read of the dG tile is an L2 hit), 4 waves as 4 x 1 (32 rows x
-// 13 blocks, 104 accumulator registers).  Two stages of planes (2 x 66 KiB):
-// the next chunk's loads are issued before the MFMAs, split and stored into
-// the other stage between them, one barrier per chunk.
+// gemm_wg3b: gemm_wg2's product with every operand split ONCE, in the
+// staging pass, and no VALU in the MFMA loop.  gemm_wg2 (above) keeps fp32 in
+// LDS and each wave splits the fragments it reads -- the A rows and the B
+// columns twice per workgroup, ~800 VALU per 32-deep chunk per wave against
+// 312 MFMAs whose issue gaps hide ~620 -- so its MFMA pipe idles about half
+// the time (PMC r07).  Here each thread splits the f4s it loaded into three
+// bf16 planes stored [plane][k][col] with a k-row pitch that is an odd
+// multiple of 32 B, and the MFMA loop reads its operands with
+// ds_read_b64_tr_b16 (4 k-rows x 16 columns per 16-lane group, delivered
+// column-major).  The 16-lane group g of a fragment reads k-rows 4g .. 4g + 3
+// and 16 + 4g .. 16 + 4g + 3 (one permutation of k for both operands, so the
+// sum is unchanged), which puts the 8 rows of a 32-lane half on 8 distinct
+// 32-B bank slots: conflict-free.  A tile covers one HALF of the NT = N1 + N2
+// columns (13 blocks of 16; the two halves of a row tile are adjacent
+// workgroups on one XCD, so the second read of the dG tile is an L2 hit).
+// (Round 4 also ran this staging on 128-row tiles, `gemm_wg3`, with 4 or 8
+// waves: 623-691 us alone against wg3b's 572-619; removed in round 5.)
 // ---------------------------------------------------------------------------
-template <int N1, int N2, int W = 4, int WN = 1>
-struct Wg3 {
-  static constexpr int NT = N1 + N2, NB = (NT + 15) / 16, NBH = (NB + 1) / 2, NH = 16 * NBH;  // cols per half
-  // W waves as (W / WN) row groups x WN column groups: RW rows (MI 16-row
-  // blocks) x NB0 column blocks per wave (the last column group NBL)
-  static constexpr int BM = 128, BK = 32, T = 64 * W, WM = W / WN, RW = BM / WM, MI = RW / 16;
-  static constexpr int NB0 = (NBH + WN - 1) / WN, NBL = NBH - (WN - 1) * NB0;
-  static constexpr int odd32(int bytes) { return (((bytes + 31) / 32) | 1) * 32; }
-  static constexpr int RA = odd32(BM * 2), RB = odd32(NH * 2);  // k-row pitch (bytes)
-  static constexpr int PA = BK * RA, PB = BK * RB;               // plane bytes
-  static constexpr int OB = 3 * PA, STG = 3 * (PA + PB);         // B planes' base, stage bytes
-  // f4s per thread: the dG rows, then the half's columns (half 0: X's, then
-  // Hprev's first NH - N1; half 1: Hprev's rest), each v from one source
-  static constexpr int QX = N1 / 4, QH0 = (NH - N1) / 4, QH1 = (NT - NH) / 4;
-  static constexpr int VX = (BK * QX + T - 1) / T, V0 = VX + (BK * QH0 + T - 1) / T, V1 = (BK * QH1 + T - 1) / T;
-  static constexpr int AV = BK * BM / 4 / T, BV = V0 > V1 ? V0 : V1, NV = AV + BV;
-  static constexpr int SP = 16 * NB0 + 4;  // epilogue staging pitch (floats)
-  static constexpr int DUMMY = 2 * STG;                       // 64 lanes x 8 B of discarded stores
-  static constexpr size_t LDS = 2 * (size_t)STG + 512;
-  static_assert(N1 % 4 == 0 && N2 % 4 == 0 && (BK * BM / 4) % T == 0 && RW % 16 == 0 && N1 <= NH, "staging");
-  static_assert(STG % 16 == 0 && LDS <= 160 * 1024 && (size_t)W * 16 * SP * 4 <= LDS, "LDS");
-  static_assert(NV <= NBL && W % WN == 0, "one f4 split per MFMA block");
-};
-
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 
@@ -1456,222 +1430,14 @@ DEV void split4(const f4& x, u2v& h, u2v& m, u2v& l) {
   }
 }
 
-// DIAG (timing probes only, wrong results; ABCD_WG3DIAG): 1 = no splits or
-// plane stores in the loop, 2 = no MFMAs (3 = the loads alone, 4 = no loads:
-// not instantiated)
-template <int N1, int N2, int W, int WN, int DIAG = 0>
-__global__ __launch_bounds__(64 * W, 1) void gemm_wg3_kernel(WgArgs a) {
-  using G = Wg3<N1, N2, W, WN>;
-  constexpr int NT = G::NT, NH = G::NH, BM = G::BM, BK = G::BK, T = G::T, RW = G::RW, MI = G::MI;
-  constexpr int NB0 = G::NB0, NBL = G::NBL, WM = G::WM;
-  constexpr int RA = G::RA, RB = G::RB, PA = G::PA, PB = G::PB, OB = G::OB, STG = G::STG;
-  constexpr int AV = G::AV, NV = G::NV, QX = G::QX, QH0 = G::QH0, QH1 = G::QH1, VX = G::VX;
-  extern __shared__ __attribute__((aligned(16))) float wsm[];
-  char* const lds = reinterpret_cast<char*>(wsm);
-  const dim3 bid = xcd_tile(true);  // both halves of the row tiles of one (direction, K range) on one XCD
-  const int dz = bid.z, d = dz / a.Z, z = dz % a.Z;
-  const int half = bid.x & 1, m0 = (bid.x >> 1) * BM, M = a.M, n0 = half * NH;
-  const int kb = z * a.kps, ke = min(a.K, kb + a.kps);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
-  const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.A[d], (uint32_t)((size_t)ke * a.lda * 4));
-  const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.B1[d], (uint32_t)((size_t)ke * a.ldb1 * 4));
-  const __amdgpu_buffer_rsrc_t r2 = make_rsrc(a.B2[d], (uint32_t)((size_t)ke * a.ldb2 * 4));
-  constexpr uint32_t OOB = 0x80000000u;
-  // this thread's f4s of a chunk: v < AV the dG rows; then the half's
-  // columns, per v from ONE source (a uniform buffer resource -- a per-lane
-  // choice would become a waterfall loop): half 0 = X's N1 columns (VX f4s
-  // per thread) then Hprev's first NH - N1, half 1 = Hprev's rest (zero pad
-  // beyond NT, never stored).  A global element offset at k0 = 0 (-1: read
-  // nothing) and a byte offset in plane 0 of a stage (-1: no store).
-  int gof[NV], lof[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    if (v < AV) {
-      const int x = tid + T * v, k = x / (BM / 4), m = m0 + 4 * (x % (BM / 4));
-      gof[v] = m < M ? k * (int)a.lda + m : -1;
-      lof[v] = k * RA + 8 * (x % (BM / 4));
-      continue;
-    }
-    const int u = v - AV;
-    int k, c, n;  // k-row, local column, column in the source
-    bool in;
-    if (half == 0 && u < VX) {
-      const int x = tid + T * u;
-      in = x < BK * QX, k = x / QX, c = 4 * (x % QX), n = c;
-    } else if (half == 0) {
-      const int x = tid + T * (u - VX);
-      in = x < BK * QH0, k = x / QH0, c = N1 + 4 * (x % QH0), n = c - N1;
-    } else {
-      const int x = tid + T * u;
-      in = x < BK * QH1, k = x / QH1, c = 4 * (x % QH1), n = NH - N1 + c;
-    }
-    const long ld = (half == 0 && u < VX) ? a.ldb1 : a.ldb2;
-    gof[v] = in ? k * (int)ld + n : -1;
-    lof[v] = in ? OB + k * RB + 2 * c : -1;
-  }
-  auto ld4 = [](const __amdgpu_buffer_rsrc_t& rs, uint32_t o) {
-    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
-  };
-  // byte offsets at k0 = 0, OOB (2^31: stays past every buffer's 2^31-byte
-  // bound after adding k0 rows) for nothing to read; the row pitch of each
-  // v's source in bytes (uniform)
-  uint32_t gob[NV];
-  uint32_t rowb[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const bool x1 = v >= AV && half == 0 && v - AV < VX;
-    rowb[v] = 4u * (uint32_t)(v < AV ? a.lda : x1 ? a.ldb1 : a.ldb2);
-    gob[v] = gof[v] < 0 ? OOB : 4u * (uint32_t)gof[v];
-  }
-  auto gload1 = [&](int k0, int v) -> f4 {
-    const bool x1 = v >= AV && half == 0 && v - AV < VX;  // uniform
-    return ld4(v < AV ? rA : x1 ? r1 : r2, gob[v] + (uint32_t)k0 * rowb[v]);
-  };
-  auto gload = [&](int k0, f4 (&raw)[NV]) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) raw[v] = gload1(k0, v);
-  };
-  // split one f4 into the stage's three planes; branch-free (a branch would
-  // cut the MFMA loop into blocks the scheduler cannot interleave): an f4
-  // with no place stores to a per-lane dummy slot past the two stages
-  auto sstore = [&](int stage, int v, const f4& x) {
-    u2v h, m, l;
-    split4(x, h, m, l);
-    const bool ok = lof[v] >= 0;
-    char* base = lds + (ok ? stage * STG + lof[v] : G::DUMMY + 8 * lane);
-    const int pp = ok ? (v < AV ? PA : PB) : 0;
-    *reinterpret_cast<u2v*>(base) = h;
-    *reinterpret_cast<u2v*>(base + pp) = m;
-    *reinterpret_cast<u2v*>(base + 2 * pp) = l;
-  };
-  // lane's transposed-read offset: group q reads k-rows 4q + (r >> 2), columns 4 (r & 3) .. + 3
-  // waves w and w + 4 share a SIMD: one of each column group (wave-uniform:
-  // the column-block guard below must be a scalar branch)
-  const int wu = __builtin_amdgcn_readfirstlane(w), wm = wu % WM, wn = wu / WM;
-  const int nb = wn == WN - 1 ? NBL : NB0;  // this wave's column blocks (wave-uniform)
-  const int offA = (4 * q + (r >> 2)) * RA + 8 * (r & 3) + 2 * (RW * wm);
-  const int offB = OB + (4 * q + (r >> 2)) * RB + 8 * (r & 3) + 2 * 16 * NB0 * wn;
-  typedef __attribute__((address_space(3))) s4v lds_s4;
-  auto trf = [&](int off, int pitch) -> bf8 {  // k-rows at off and 16 further
-    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off));
-    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lds + off + 16 * pitch));
-    return __builtin_bit_cast(bf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  f4 acc[MI][NB0];
-  acc_zero(acc);
-  constexpr int TA[6] = {2, 1, 0, 1, 0, 0}, TB[6] = {0, 1, 2, 0, 1, 0};
-  // the pad columns NT - n0 .. NH of both stages' B planes read as 0 (never stored)
-  for (int e = tid; n0 + NH > NT && e < 2 * 3 * BK * (n0 + NH - NT); e += T) {
-    const int np = n0 + NH - NT, sp = e / (BK * np), x = e % (BK * np);
-    *reinterpret_cast<short*>(lds + (sp / 3) * STG + OB + (sp % 3) * PB + (x / np) * RB + 2 * (NT - n0 + x % np)) = 0;
-  }
-  // raw holds chunk c + 1 while chunk c multiplies; each f4 is reloaded with
-  // chunk c + 2 right after its split, so every load has a whole chunk of
-  // MFMAs to land (loads past the K range read 0; on the last chunks the
-  // splits fill the stage nobody reads again: branch-free)
-  // two register sets of raw f4s, each a chunk ahead of the other: while
-  // chunk c multiplies, one set (chunk c + 1) is split into the other stage
-  // and each f4 reloaded with chunk c + 3 right after its split, so every load
-  // has two chunks of MFMAs to land (loads past the K range read 0; chunks
-  // past it multiply zeros; all branch-free).  The loop runs chunk pairs so
-  // the sets swap roles without register moves.
-  auto chunk = [&](int k0, int cur, f4 (&rw)[NV]) {
-    const int sb = cur * STG;
-    bf8 ap[MI][3];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) ap[i][p] = DIAG == 3 ? bf8{} : trf(sb + p * PA + offA + 2 * 16 * i, RA);
-    auto bload = [&](int j, bf8 (&bp)[3]) {
-#pragma unroll
-      for (int p = 0; p < 3; ++p) bp[p] = DIAG == 3 ? bf8{} : trf(sb + p * PB + offB + 2 * 16 * j, RB);
-    };
-    bf8 bp[3];
-    bload(0, bp);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NB0; ++j) {
-      bf8 bq[3];
-      if (j + 1 < NB0) bload(j + 1, bq);  // (past nb: in-range LDS, never multiplied)
-      if (NB0 == NBL || j < nb) {
-#pragma unroll
-        for (int t = 0; t < 6; ++t)
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-            if (DIAG == 3) {
-            } else if (DIAG != 2) acc[i][j] = mfma_bf(ap[i][TA[t]], bp[TB[t]], acc[i][j]);
-            else acc[i][j][0] += (float)ap[i][TA[t]][0] * (float)bp[TB[t]][1];
-      }
-      // the next chunk's f4s split and stored into the other stage in the
-      // MFMA gaps of the later blocks (blocks every wave has)
-      constexpr int J0 = NBL - NV;
-      const bool sj = j >= J0 && j - J0 < NV;  // (compile time: block j splits f4 j - J0)
-      if (sj) {
-        if (DIAG != 1 && DIAG != 3) sstore(cur ^ 1, j - J0, rw[j - J0]);
-        else acc[0][j][1] += rw[j - J0][0];
-        if (DIAG != 4) rw[j - J0] = gload1(k0 + 3 * BK, j - J0);
-      }
-      // order: the next block's 6 transposed reads first (12 MFMAs before
-      // their use), then each MFMA followed by two of the split's VALU, the
-      // plane stores and the reload last
-      if (j + 1 < NB0) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-#pragma unroll
-      for (int k = 0; k < 6 * MI; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (sj) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-      }
-      if (sj) {
-        __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (j + 1 < NB0) bp[0] = bq[0], bp[1] = bq[1], bp[2] = bq[2];
-    }
-    __syncthreads();
-  };
-  f4 rawA[NV], rawB[NV];
-  gload(kb, rawA);
-#pragma unroll
-  for (int v = 0; v < NV; ++v) sstore(0, v, rawA[v]);
-  gload(kb + BK, rawA);
-  gload(kb + 2 * BK, rawB);
-  __syncthreads();
-  for (int k0 = kb; k0 < ke; k0 += 2 * BK) {
-    chunk(k0, 0, rawA);
-    chunk(k0 + BK, 1, rawB);
-  }
-  // epilogue (gemm_wg2's): per 16-row block, a wave-private LDS transpose,
-  // then whole-row 16-B stores of the half's columns into this K range's slab [M][NT]
-  constexpr int SP = G::SP;
-  float* stg = wsm + w * 16 * SP;
-  float* const out = a.slab + (size_t)dz * M * NT;
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-#pragma unroll
-    for (int j = 0; j < NB0; ++j)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int p = 0; p < NB0; ++p) {  // 16 rows x 4 NB0 quads = 64 NB0 lanes' worth
-      const int e = lane + 64 * p, lr = e / (4 * NB0), c4 = e % (4 * NB0);
-      const int lcol = 16 * NB0 * wn + 4 * c4, gcol = n0 + lcol, grow = m0 + RW * wm + 16 * i + lr;
-      if (grow < M && lcol < NH && gcol < NT)
-        *reinterpret_cast<f4*>(out + (size_t)grow * NT + gcol) = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * c4);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// gemm_wg3b: gemm_wg3 with 256-row tiles (half the B-operand bytes per MFMA:
-// the wg3 loop is bound by its operand traffic).  Two A stages (52 KiB each)
-// but ONE B stage (39 KiB): the next chunk's B columns are split and stored
-// between two barriers at the end of each chunk; the A rows as in wg3, inside
-// the MFMA gaps.  8 waves as 4 row groups (64 rows) x 2 column groups (7 / 6
-// blocks).  Same-box A/B at c2 against the 4 x 2 gemm_wg3: 507 vs ~579 us
-// per launch, step 8.97 / 8.94 -> 8.85 / 8.86 ms.  The default.
+// gemm_wg3b tile: 256 gate rows (half the B-operand bytes per MFMA of a
+// 128-row tile: that loop is bound by its operand traffic).  Two A stages (52
+// KiB each) but ONE B stage (39 KiB): the next chunk's B columns are split and
+// stored between two barriers at the end of each chunk; the A rows inside the
+// MFMA gaps (each loaded f4 split and stored into the other stage, reloaded
+// with the chunk after next).  8 waves as 4 row groups (64 rows) x 2 column
+// groups (7 / 6 blocks).  Same-box A/B at c2 against the 128-row 4 x 2 form:
+// 507 vs ~579 us per launch, step 8.97 / 8.94 -> 8.85 / 8.86 ms.
 template <int N1, int N2>
 struct Wg3b {
   static constexpr int NT = N1 + N2, NB = (NT + 15) / 16, NBH = (NB + 1) / 2, NH = 16 * NBH;
@@ -1867,58 +1633,16 @@ __global__ __launch_bounds__(512, 1) void gemm_wg3b_kernel(WgArgs a) {
   }
 }
 
-template <int N1, int N2, int W, int WN, int DIAG>
-static int wg3_go1(hipStream_t s, const WgArgs& a, dim3 grid) {
-  constexpr size_t lds = Wg3<N1, N2, W, WN>::LDS;
-  static bool attr = false;
-  if (!attr) {
-    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg3_kernel<N1, N2, W, WN, DIAG>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
-  gemm_wg3_kernel<N1, N2, W, WN, DIAG><<<grid, 64 * W, lds, s>>>(a);
-  return 0;
-}
-
-// the DIAG timing probes compute wrong results: they exist only in a
-// diagnostics build (make EXTRA=-DABCD_WG_DIAG); a normal build ignores
-// ABCD_WG3DIAG (with a warning) and always runs the real kernel
-template <int N1, int N2, int W, int WN>
-static int wg3_go(hipStream_t s, const WgArgs& a, dim3 grid, int diag) {
-#ifdef ABCD_WG_DIAG
-  switch (diag) {
-    case 1: return wg3_go1<N1, N2, W, WN, 1>(s, a, grid);
-    case 2: return wg3_go1<N1, N2, W, WN, 2>(s, a, grid);
-    default: break;
-  }
-#else
-  static bool warned = false;
-  if (diag && !warned) {
-    fprintf(stderr, "libabcd_hip: ABCD_WG3DIAG ignored (timing probes exist only in a -DABCD_WG_DIAG build)\n");
-    warned = true;
-  }
-#endif
-  return wg3_go1<N1, N2, W, WN, 0>(s, a, grid);
-}
-
 template <int N1, int N2, bool W3>
 static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F, float* scratch,
                             size_t scratch_floats) {
-  using G = Wg2<N1, N2>;  // tile and slab geometry (gemm_wg3 shares it)
-  static_assert(Wg3<N1, N2>::BM == G::BM && Wg3<N1, N2>::NT == G::NT, "same slab geometry");
-  const int mt = cdiv(M, G::BM);
-  // one workgroup per CU: about 256 / (nd x mt) K ranges, the grid a multiple of 8
-  // gemm_wg3b (256-row tiles) by default; ABCD_WG3W = 2 / 8 / 4: gemm_wg3's
-  // 4 x 2, 8 x 1 or 4-wave forms (128-row tiles)
-  const char* wv0 = getenv("ABCD_WG3W");
-  const bool w3b = W3 && !(wv0 && (wv0[0] == '2' || wv0[0] == '8' || wv0[0] == '4'));
-  const int mtb = w3b ? cdiv(M, 256) : mt;
-  const int tw = W3 ? 2 * mtb : mt;  // workgroups per (direction, K range)
+  using G = Wg2<N1, N2>;  // slab geometry (gemm_wg3b writes the same [M][NT] slabs)
+  static_assert(Wg3b<N1, N2>::NT == G::NT, "same slab geometry");
+  const int tw = W3 ? 2 * cdiv(M, 256) : cdiv(M, G::BM);  // workgroups per (direction, K range)
   int Z = std::max(1, 256 / (nd * tw));
   while ((nd * tw * Z) % 8) ++Z;
   Z = (int)std::min<long>(Z, (long)(scratch_floats / ((size_t)nd * M * G::NT)));
   if (Z < 1) return -1;
-  // gemm_wg3 runs chunk pairs: K ranges of whole pairs
   const int kq = W3 ? 64 : 32, kps = ((cdiv(K, Z) + kq - 1) / kq) * kq;
   Z = cdiv(K, kps);
   WgArgs a{};
@@ -1928,41 +1652,22 @@ static int wgrad_wg2_launch(hipStream_t s, int nd, const WgDir* dirs, int M, int
     o.w_ih[d] = dirs[d].w_ih; o.b_ih[d] = dirs[d].b_ih; o.b_hh[d] = dirs[d].b_hh; o.w_hh[d] = dirs[d].w_hh;
   }
   a.lda = M; a.ldb1 = N1; a.ldb2 = N2; a.M = M; a.K = K; a.kps = kps; a.Z = Z; a.slab = scratch;
-  if (!W3) {
+  if (W3) {
+    static bool attr_b = false;
+    if (!attr_b) {
+      ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg3b_kernel<N1, N2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)Wg3b<N1, N2>::LDS));
+      attr_b = true;
+    }
+    gemm_wg3b_kernel<N1, N2><<<dim3(tw, 1, nd * Z), 512, Wg3b<N1, N2>::LDS, s>>>(a);
+  } else {
     static bool attr = false;
     if (!attr) {
       ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg2_kernel<N1, N2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)G::LDS));
       attr = true;
     }
-    gemm_wg2_kernel<N1, N2><<<dim3(mt, 1, nd * Z), 256, G::LDS, s>>>(a);
-  } else {
-    // the two column halves of a row tile in adjacent x; ABCD_WG3W = 4 or 8
-    // waves; ABCD_WG3DIAG: the timing probes (wrong results)
-    if (w3b) {
-      static bool attr_b = false;
-      if (!attr_b) {
-        ABCD_TRY(hipFuncSetAttribute((const void*)gemm_wg3b_kernel<N1, N2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)Wg3b<N1, N2>::LDS));
-        attr_b = true;
-      }
-      gemm_wg3b_kernel<N1, N2><<<dim3(2 * mtb, 1, nd * Z), 512, Wg3b<N1, N2>::LDS, s>>>(a);
-      ABCD_CHECK_LAUNCH();
-      const long nqb = (long)nd * M * G::NT / 4;
-      wg2_reduce_kernel<<<(int)std::min<long>(2048, cdiv(nqb, 256)), 256, 0, s>>>(scratch, nd, Z, M, G::NT, N1, F, N2, o);
-      ABCD_CHECK_LAUNCH();
-      return 0;
-    }
-    const char* dg = getenv("ABCD_WG3DIAG");
-    const char* wv = getenv("ABCD_WG3W");
-    const int diag = dg ? atoi(dg) : 0;
-    const dim3 gr(2 * mt, 1, nd * Z);
-    // ABCD_WG3W: 8x1 (8 waves of 16 rows x 13 column blocks), 4x2 (the default:
-    // 8 waves of 32 rows x 7 / 6 blocks, half the transposed B reads), 4 (4 x 1)
-    const int form = !wv ? 1 : wv[0] == '8' ? 0 : wv[0] == '4' && wv[1] == 0 ? 2 : 1;
-    ABCD_TRY((hipError_t)(form == 0   ? wg3_go<N1, N2, 8, 1>(s, a, gr, diag)
-                          : form == 1 ? wg3_go<N1, N2, 8, 2>(s, a, gr, diag)
-                                      : wg3_go<N1, N2, 4, 1>(s, a, gr, diag)));
+    gemm_wg2_kernel<N1, N2><<<dim3(tw, 1, nd * Z), 256, G::LDS, s>>>(a);
   }
   ABCD_CHECK_LAUNCH();
   const long nq = (long)nd * M * G::NT / 4;
@@ -1995,12 +1700,7 @@ bool wg3_on() {
   return !(v && v[0] == '0');
 }
 // the dispatch record's name of the form wgrad_lstm_l0 runs (printf format, Fp, H, nd)
-const char* wg_dispatch_fmt() {
-  if (!wg3_on()) return "gemm_wg2<%d,%d> x%d";
-  const char* wv = getenv("ABCD_WG3W");
-  const bool w3b = !(wv && (wv[0] == '2' || wv[0] == '8' || wv[0] == '4'));
-  return w3b ? "gemm_wg3b<%d,%d> x%d" : "gemm_wg3<%d,%d> x%d";
-}
+const char* wg_dispatch_fmt() { return wg3_on() ? "gemm_wg3b<%d,%d> x%d" : "gemm_wg2<%d,%d> x%d"; }
 
 template <int MR, int NR, bool AKC, bool BKC>
 static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,

@@ -43,9 +43,8 @@ KERNELS = {
     "LSTM": ("enc_fwd_persist<4,16,8>", "enc_bwd_w8<4>", "dec_fwd_x6<13,8,8,LSTM>", "dec_bwd_w16<9,LSTM>"),
     "GRU": ("enc_fwd_persist<3,16,8>", "enc_bwd_w8<3>", "dec_fwd_x6<13,8,8,GRU>", "dec_bwd_w16<9,GRU>"),
 }
-# the encoder weight-gradient form (ABCD_WG3=0: gemm_wg2; ABCD_WG3W=2/8/4: gemm_wg3; default gemm_wg3b)
-WG_FORM = ("gemm_wg2" if os.environ.get("ABCD_WG3", "") == "0"
-           else "gemm_wg3" if os.environ.get("ABCD_WG3W", "")[:1] in ("2", "8", "4") else "gemm_wg3b")
+# the encoder weight-gradient form (ABCD_WG3=0: gemm_wg2; default gemm_wg3b)
+WG_FORM = "gemm_wg2" if os.environ.get("ABCD_WG3", "") == "0" else "gemm_wg3b"
 
 
 # (bench config, batch, seed of the synthetic batch)

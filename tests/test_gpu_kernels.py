@@ -30,20 +30,18 @@ def test_gemm_nt_vs_torch(M, N, K):
     assert err <= 1e-5 * K ** 0.5 * 4 + 1e-5, err
 
 
-@pytest.mark.parametrize("wg", ["3", "2", "3w8", "3w2"])
+@pytest.mark.parametrize("wg", ["3", "2"])
 @pytest.mark.parametrize("nd,F,H,K", [(2, 129, 256, 65583), (1, 129, 256, 3001), (2, 130, 256, 777), (2, 33, 48, 500),
                                        (1, 20, 24, 64), (2, 129, 256, 31), (1, 143, 256, 100003)])
 def test_lstm_wgrad_vs_torch(nd, F, H, K, wg, monkeypatch):
     """abcd_lstm_wgrad (the LSTM layer's w_ih, b_ih, b_hh, w_hh gradients from
-    the gate gradients, model.py:53,60-66): gemm_wg3 (default) or gemm_wg2
+    the gate gradients, model.py:53,60-66): gemm_wg3b (default) or gemm_wg2
     (ABCD_WG3=0) at F <= 143, H = 256 (the c2 shape first, both directions;
     a K below one chunk; the widest F with a K range that is not a multiple
     of 32), the split-GEMM route elsewhere -- against float64 torch."""
-    # "3": the default (gemm_wg3b, 256-row tiles); "3w2" / "3w8": gemm_wg3's 4 x 2 / 8 x 1 forms
+    # "3": the default (gemm_wg3b, 256-row tiles)
     monkeypatch.setenv("ABCD_WG3", "0" if wg == "2" else "1")
-    if wg in ("3w8", "3w2"):
-        monkeypatch.setenv("ABCD_WG3W", wg[2])
-    wg = {"3": "3b", "2": "2"}.get(wg, "3")
+    wg = {"3": "3b", "2": "2"}[wg]
     import ctypes
     from modules import _native as Nn
     g = torch.Generator(device="cuda").manual_seed(nd * 7 + F + H + K)

@@ -134,3 +134,43 @@ def test_fused_head_repeatable():
         outs.append([lg, ft, kl, pp, dh] + [g[k] for k in sorted(g)])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("K", [128, 1024])
+def test_deferred_parameter_gradients_identical(K):
+    """abcd_sampler_backward_split with ABCD_DEFER_PARAMS, then
+    abcd_sampler_backward_params (the engine's order: the codebook / W2 / W1
+    gradients after the encoder's backward) gives the same bits as the
+    one-call backward: the same batched GEMM launch on the same workspace
+    stash, only later in stream order.  d_h is complete after the first call."""
+    from modules import model as M, _native as N
+    L = N.lib()
+    dev = torch.device("cuda")
+    torch.manual_seed(11 + K)
+    B, E, Hm, D = 512, 1024, 256, 256
+    samp = M.ABCDSampler(E, Hm, K, D).to(dev)
+    cfg, par = samp._scfg(), samp._sparams()
+    h = torch.randn(B, E, device=dev)
+    d_feats = torch.randn(B, D, device=dev) / B
+    d_kl = torch.full((), 1.0 / B, device=dev)
+    ws = N.workspace(L.abcd_sampler_workspace_bytes(cfg, B), dev)
+    st = N.stream()
+    outs = []
+    for defer in (False, True):
+        lg, ft, kl = torch.empty(B, K, device=dev), torch.empty(B, D, device=dev), torch.empty(1, device=dev)
+        _ck(L.abcd_sampler_forward_fused(cfg, par, N.ptr(h), B, N.SAMPLE_GUMBEL, 0.5, None, 5, 0, 1e4,
+                                         N.ptr(lg), N.ptr(ft), N.ptr(kl), None, N.ptr(ws), ws.numel(), st))
+        g, gs = _grads(samp, dev)
+        dh = torch.empty(B, E, device=dev)
+        _ck(L.abcd_sampler_backward_split(cfg, par, N.ptr(h), B, N.SAMPLE_GUMBEL, 0.5, 1e4, N.ptr(d_feats),
+                                          N.ptr(d_kl), N.ptr(dh), gs, N.ptr(ws), ws.numel(), st,
+                                          N.DEFER_PARAMS if defer else None))
+        if defer:
+            torch.cuda.synchronize()
+            assert all(float(g[k].abs().max()) == 0.0 for k in ("codebook", "mlp0.w1", "mlp0.w2")), \
+                "parameter gradients written before abcd_sampler_backward_params"
+            _ck(L.abcd_sampler_backward_params(cfg, par, N.ptr(h), B, gs, N.ptr(ws), ws.numel(), st))
+        torch.cuda.synchronize()
+        outs.append([dh] + [g[k] for k in sorted(g)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
