@@ -114,7 +114,7 @@ int abcd_encoder_backward_dropout(const abcd_encoder_cfg* cfg, const abcd_encode
  * stride ldx), Hprev[d]: K x H (stride H; the hidden state each frame's step
  * consumed, zero where it had no predecessor).  b_hh[d] may be NULL.  The
  * encoder backward runs this after its BPTT (layer 0); at F <= 143 with
- * roundup16(F) = 144 and H = 256 it is one gemm_wg2 launch + one slab reduction. */
+ * roundup16(F) = 144 and H = 256 it is one gemm_wg3b launch + one slab reduction. */
 size_t abcd_lstm_wgrad_workspace_bytes(int nd, int F, int H, int K);
 int abcd_lstm_wgrad(int nd, int F, int H, int K, const float* const* dG, const float* X, long ldx,
                     const float* const* Hprev, float* const* w_ih, float* const* b_ih, float* const* b_hh,
@@ -204,11 +204,16 @@ int abcd_sampler_backward_split(const abcd_sampler_cfg* cfg, const abcd_sampler_
                                 const float* d_kl, float* d_h, const abcd_sampler_grads* g, void* ws,
                                 size_t ws_bytes, void* stream, void* wgrad_stream);
 /* the deferred codebook / W2 / W1 gradients of a preceding
- * abcd_sampler_backward_split(..., ABCD_DEFER_PARAMS): one batched launch
- * (dC = [d_feats; U]^T [Y; dL / sqrt(D)], dW2 = dU^T Z1, dW1 = dZ1^T h) on
- * `stream`; returns 0 without work when that call took another path. */
+ * abcd_sampler_backward_split(..., ABCD_DEFER_PARAMS) on `stream`: one
+ * batched launch (dC = [d_feats; U]^T [Y; dL / sqrt(D)], dW2 = dU^T Z1,
+ * dW1 = dZ1^T h); returns 0 without work when that call took another path.
+ * wgrad_stream (NULL or == stream: on `stream`): the launch goes there behind
+ * an event on `stream`, in a tiling that co-resides with the encoder's
+ * persistent BPTT (the training step queues it on its side stream behind the
+ * decoder's weight gradients); the caller joins before reading them. */
 int abcd_sampler_backward_params(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
-                                 const abcd_sampler_grads* g, void* ws, size_t ws_bytes, void* stream);
+                                 const abcd_sampler_grads* g, void* ws, size_t ws_bytes, void* stream,
+                                 void* wgrad_stream);
 /* The same backward split the way autograd sees the three reference methods:
  * sample_backward:  d_feats -> d_logits (written), d_codebook (written, may be NULL)
  *                   (plain: d_feats -> d[mean | log_var])

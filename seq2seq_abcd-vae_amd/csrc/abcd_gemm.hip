@@ -431,15 +431,15 @@ struct GemmBatchArgs {
   int tile0[GEMM_BATCH_MAX + 1];  // first tile of each job; tile0[n] = total
   int n;
 };
-template <int MR, int NR>
+template <int MR, int NR, int BK>
 __global__ __launch_bounds__(256) void gemm_tn_batch_kernel(GemmBatchArgs b) {
-  __shared__ __attribute__((aligned(16))) float smab[tn_lds_floats<MR, NR, 64>()];
+  __shared__ __attribute__((aligned(16))) float smab[tn_lds_floats<MR, NR, BK>()];
   int ji = 0;
   while (ji + 1 < b.n && (int)blockIdx.x >= b.tile0[ji + 1]) ++ji;
   const GemmJob J = b.j[ji];
   const int t = (int)blockIdx.x - b.tile0[ji], tn = (J.N + 32 * NR - 1) / (32 * NR);
   const EpiArgs e{J.C, J.ldc, J.M, J.N, J.alpha, J.beta, nullptr, ACT_NONE, nullptr};
-  gemm_tn_tile<MR, NR, false, false, 64>(smab, J.A, J.lda, J.B, J.ldb, 0, J.K, (t / tn) * 32 * MR, (t % tn) * 32 * NR,
+  gemm_tn_tile<MR, NR, false, false, BK>(smab, J.A, J.lda, J.B, J.ldb, 0, J.K, (t / tn) * 32 * MR, (t % tn) * 32 * NR,
                                          e, J.C, J.ldc, false);
 }
 int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
@@ -461,7 +461,10 @@ int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
   b.n = k;
   b.tile0[k] = tiles;
   if (!tiles) return 0;
-  gemm_tn_batch_kernel<2, 2><<<tiles, 256, 0, s>>>(b);
+  // 64-deep LDS slabs (70 KB) on a quiet chip; 16-deep ones (17 KB) beside a
+  // persistent kernel (side mode), whose LDS image leaves ~40 KB per CU
+  if (tl_side) gemm_tn_batch_kernel<2, 2, 16><<<tiles, 256, 0, s>>>(b);
+  else gemm_tn_batch_kernel<2, 2, 64><<<tiles, 256, 0, s>>>(b);
   ABCD_CHECK_LAUNCH();
   return 0;
 }
@@ -501,7 +504,10 @@ static int gemm_tn_launch(hipStream_t s, int M, int N, int K, const float* A, lo
 // ops of the splits: the f32-MFMA form of the same chunk costs 8 MR NR
 // MFMAs of 32 cycles.
 // ---------------------------------------------------------------------------
-template <int MR, int NR, bool AKC, bool BKC>
+// ONE: a single operand stage (34 KB at 128 x 128, so the workgroup fits
+// beside a persistent kernel's LDS image): the next chunk's loads still go
+// out before the MFMAs, their LDS stores wait for a barrier after them.
+template <int MR, int NR, bool AKC, bool BKC, bool ONE = false>
 __global__ __launch_bounds__(256, 2) void gemm_x6s_kernel(const float* __restrict__ A, long lda,
                                                        const float* __restrict__ B, long ldb, int K, int kps,
                                                        EpiArgs e, int remap) {
@@ -513,9 +519,10 @@ __global__ __launch_bounds__(256, 2) void gemm_x6s_kernel(const float* __restric
   constexpr int SA = BK * LA + 16 * (BK / 8), SB = BK * LB + 16 * (BK / 8);  // one stage
   constexpr int AVT = BK * BM / 4, BVT = BK * BN / 4;  // f4 per slab
   constexpr int AV = (AVT + 255) / 256, BV = (BVT + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float smab[2 * SA + 2 * SB];
+  constexpr int NS = ONE ? 1 : 2;  // operand stages
+  __shared__ __attribute__((aligned(16))) float smab[NS * SA + NS * SB];
   float* const As = smab;
-  float* const Bs = smab + 2 * SA;
+  float* const Bs = smab + NS * SA;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, q = lane >> 4;
   const int wm = w >> 1, wn = w & 1;
   const int m0 = bid.y * BM, n0 = bid.x * BN;
@@ -613,9 +620,16 @@ __global__ __launch_bounds__(256, 2) void gemm_x6s_kernel(const float* __restric
     const bool more = k0 + BK < ke;
     if (more) gload(k0 + BK, ra, rb);
     compute(cur);
-    if (more) lstore(cur ^ 1, ra, rb);
+    if constexpr (ONE) {
+      if (more) {
+        __syncthreads();
+        lstore(0, ra, rb);
+      }
+    } else {
+      if (more) lstore(cur ^ 1, ra, rb);
+      cur ^= 1;
+    }
     __syncthreads();
-    cur ^= 1;
   }
   // epilogue: wave-private LDS transpose, whole-row 16-B stores (as gemm_tn_kernel)
   constexpr int SW = 16 * NR, SP = SW + 4;
@@ -1702,7 +1716,7 @@ bool wg3_on() {
 // the dispatch record's name of the form wgrad_lstm_l0 runs (printf format, Fp, H, nd)
 const char* wg_dispatch_fmt() { return wg3_on() ? "gemm_wg3b<%d,%d> x%d" : "gemm_wg2<%d,%d> x%d"; }
 
-template <int MR, int NR, bool AKC, bool BKC>
+template <int MR, int NR, bool AKC, bool BKC, bool ONE = false>
 static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
                            EpiArgs e, float* scratch, size_t scratch_floats) {
   const int BM = 32 * MR, BN = 32 * NR;
@@ -1715,8 +1729,8 @@ static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, l
   Z = cdiv(K, kps);
   EpiArgs ek = e;
   if (Z > 1) ek.slab = scratch;
-  gemm_x6s_kernel<MR, NR, AKC, BKC><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps, ek,
-                                                                                     1);
+  gemm_x6s_kernel<MR, NR, AKC, BKC, ONE><<<dim3(cdiv(N, BN), cdiv(M, BM), Z), 256, 0, s>>>(A, lda, B, ldb, K, kps,
+                                                                                          ek, 1);
   ABCD_CHECK_LAUNCH();
   if (Z > 1) {
     ABCD_TRY((hipError_t)slab_reduce(s, scratch, Z, e));
@@ -1744,6 +1758,14 @@ static int gemm_tn(hipStream_t s, int M, int N, int K, const Operand& A, const O
     default: return gemm_tn_launch<4, 8>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
   }
 #undef TN_CASE
+}
+// ABCD_SIDE_X6=0: the side-stream frame reductions on gemm_tn (fp32 MFMA)
+static bool side_x6() {
+  static const bool on = [] {
+    const char* v = getenv("ABCD_SIDE_X6");
+    return !(v && v[0] == '0');
+  }();
+  return on;
 }
 static bool tn_ok(const Operand& o, int rows) {
   return o.kmajor && o.ld % 4 == 0 && ((uintptr_t)o.p % 16) == 0 && o.ld >= ((rows + 3) & ~3);
@@ -1799,6 +1821,15 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
       if ((size_t)K * A.ld * 4 < (1ull << 31) && (size_t)K * B.ld * 4 < (1ull << 31))
         return gemm_x6t_launch<4, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
       return gemm_x6s_launch<4, 4, false, false>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+    }
+    // beside the encoder BPTT (side mode): split-fp32 on one operand stage
+    // (34 KB, 204 VGPRs: fits beside enc_bwd_w8's 120 KB / 256 registers)
+    if (side_x6()) {
+      if (N > 128 && N <= 160)
+        return gemm_x6s_launch<4, 5, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+      if (M > 128 && M <= 160)
+        return gemm_x6s_launch<5, 4, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+      return gemm_x6s_launch<4, 4, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
     }
     return gemm_tn(s, M, N, K, A, B, e, scratch, scratch_floats);
   }

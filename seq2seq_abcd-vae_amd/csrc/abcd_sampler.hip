@@ -1336,6 +1336,7 @@ static int samp_fused_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* 
   note_dispatch(TK_SAMP_BWD, "samp_head_bwd grid %d + d_h gemm", grid);
   if (sw != (hipStream_t)ABCD_DEFER_PARAMS) {
     ABCD_TRY((hipError_t)stream_fork(s, sw, 1));
+    GemmSideScope side(sw != s);
     ABCD_TRY((hipError_t)samp_fused_params(c, h, B, g, w, sw));
   }
   if (d_h)
@@ -1428,14 +1429,21 @@ extern "C" int abcd_sampler_backward_split(const abcd_sampler_cfg* c, const abcd
 
 extern "C" int abcd_sampler_backward_params(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
                                             int B, const abcd_sampler_grads* g, void* ws, size_t ws_bytes,
-                                            void* stream) {
+                                            void* stream, void* wgrad_stream) {
   ABCD_REQUIRE(samp_check(c) == 0 && p && h && g && ws && B > 0);
   if (c->plain || c->num_categories > 1024 ||
       head_bwd_lds(c->mlp_hidden, c->feature_dim, c->num_categories) > HEAD_LDS_MAX)
     return 0;  // the split call ran the unfused path, parameter gradients included
   SampWS w;
   ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
-  return samp_fused_params(c, h, B, g, w, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  hipStream_t sw = wgrad_stream ? (hipStream_t)wgrad_stream : s;
+  if (sw == s) return samp_fused_params(c, h, B, g, w, s);
+  // on the caller's side stream, behind an event on `stream` (the head
+  // kernel's stash), in the tiling that co-resides with a persistent kernel
+  ABCD_TRY((hipError_t)stream_fork(s, sw, 1));
+  GemmSideScope side(true);
+  return samp_fused_params(c, h, B, g, w, sw);
 }
 
 extern "C" int abcd_sampler_backward(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h, int B,

@@ -106,7 +106,7 @@ _SIGS = {
                                             c_double, c_void_p, c_void_p, c_void_p, _P(SamplerGrads), c_void_p,
                                             c_size_t, c_void_p, c_void_p]),
     "abcd_sampler_backward_params": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, _P(SamplerGrads),
-                                             c_void_p, c_size_t, c_void_p]),
+                                             c_void_p, c_size_t, c_void_p, c_void_p]),
     "abcd_sampler_sample_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_int, c_float, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_kl_backward": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_double, c_void_p, c_int,

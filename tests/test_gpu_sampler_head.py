@@ -137,12 +137,15 @@ def test_fused_head_repeatable():
 
 
 @pytest.mark.parametrize("K", [128, 1024])
-def test_deferred_parameter_gradients_identical(K):
+@pytest.mark.parametrize("on_side", [False, True])
+def test_deferred_parameter_gradients_identical(K, on_side):
     """abcd_sampler_backward_split with ABCD_DEFER_PARAMS, then
     abcd_sampler_backward_params (the engine's order: the codebook / W2 / W1
     gradients after the encoder's backward) gives the same bits as the
     one-call backward: the same batched GEMM launch on the same workspace
-    stash, only later in stream order.  d_h is complete after the first call."""
+    stash, only later in stream order -- on `stream` or on a side stream (the
+    engine's form: side tiling, 16-deep LDS slabs, the same sums in the same
+    order).  d_h is complete after the first call."""
     from modules import model as M, _native as N
     L = N.lib()
     dev = torch.device("cuda")
@@ -155,6 +158,7 @@ def test_deferred_parameter_gradients_identical(K):
     d_kl = torch.full((), 1.0 / B, device=dev)
     ws = N.workspace(L.abcd_sampler_workspace_bytes(cfg, B), dev)
     st = N.stream()
+    side = torch.cuda.Stream() if on_side else None
     outs = []
     for defer in (False, True):
         lg, ft, kl = torch.empty(B, K, device=dev), torch.empty(B, D, device=dev), torch.empty(1, device=dev)
@@ -169,8 +173,9 @@ def test_deferred_parameter_gradients_identical(K):
             torch.cuda.synchronize()
             assert all(float(g[k].abs().max()) == 0.0 for k in ("codebook", "mlp0.w1", "mlp0.w2")), \
                 "parameter gradients written before abcd_sampler_backward_params"
-            _ck(L.abcd_sampler_backward_params(cfg, par, N.ptr(h), B, gs, N.ptr(ws), ws.numel(), st))
-        torch.cuda.synchronize()
+            _ck(L.abcd_sampler_backward_params(cfg, par, N.ptr(h), B, gs, N.ptr(ws), ws.numel(), st,
+                                               side.cuda_stream if side is not None else None))
+        torch.cuda.synchronize()  # joins the side stream too
         outs.append([dh] + [g[k] for k in sorted(g)])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
