@@ -1430,7 +1430,7 @@ extern "C" int abcd_sampler_backward_split(const abcd_sampler_cfg* c, const abcd
 extern "C" int abcd_sampler_backward_params(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
                                             int B, const abcd_sampler_grads* g, void* ws, size_t ws_bytes,
                                             void* stream, void* wgrad_stream) {
-  ABCD_REQUIRE(samp_check(c) == 0 && p && h && g && ws && B > 0);
+  ABCD_REQUIRE(samp_check(c) == 0 && p && h && g && ws && B > 0 && wgrad_stream != ABCD_DEFER_PARAMS);
   if (c->plain || c->num_categories > 1024 ||
       head_bwd_lds(c->mlp_hidden, c->feature_dim, c->num_categories) > HEAD_LDS_MAX)
     return 0;  // the split call ran the unfused path, parameter gradients included
