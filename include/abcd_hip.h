@@ -398,12 +398,22 @@ void abcd_dispatch_reset(void);
 /* diagnostics (scripts/, not part of the reference's interface):
  * abcd_debug_persist_prof -- the persistent kernels of the roles in `mask`
  * (1 enc fwd, 2 enc bwd, 4 dec fwd, 8 dec bwd) stamp s_memrealtime at their
- * phase boundaries into dev_buf (blocks x T x 8 u64; null: off);
+ * phase boundaries into dev_buf (blocks x T x 8 u64; null: off); 16 / 32:
+ * the sampler-head forward / backward kernels (tiles x 8 u64);
  * abcd_debug_xcc_map -- launches `blocks` one-per-CU workgroups that record
  * their (XCC id, HW_ID) pair into dev_out[2 * block], dev_out[2 * block + 1]
  * (dev_out holds 2 * blocks u32; the placement the persistent kernels' group
  * roles rely on).  Returns 0 / a HIP error. */
 void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask);
+/* Side-stream gate (process-wide switch, default off): the weight-gradient
+ * work abcd_decoder_backward_overlap queues on its wgrad_stream first waits,
+ * on the device and bounded (tens of ms, then it proceeds), until the NEXT
+ * encoder BPTT launch of this process has every workgroup resident -- for a
+ * caller that queues abcd_encoder_backward* right after the decoder and
+ * sampler backward, as the training step does.  Without it the side GEMMs can
+ * take a CU's room before a BPTT member is placed there.  Read when that
+ * call is made (the training step sets it around its decoder backward). */
+void abcd_side_gate_enable(int on);
 int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream);
 /* 0 if no persistent recurrent kernel has timed out waiting for its group
  * since the last call (a timeout means the grid was not co-resident; the

@@ -74,6 +74,11 @@ def main():
         first = s[:, 0, 0][ok[:, 0]].min()
         last = s[:, -1, nst - 1][ok[:, -1]].max()
         print(f"   span first->last stamp {float(last - first):.0f} ns")
+        # start skew: when each workgroup stamped its first step (a late one was
+        # placed late, e.g. behind side-stream work holding its CU)
+        s00 = s[:, 0, 0][ok[:, 0]] - first
+        q = torch.quantile(s00, torch.tensor([0.5, 0.9, 1.0], dtype=s00.dtype))
+        print(f"   start skew over workgroups: median {float(q[0]):.0f}  p90 {float(q[1]):.0f}  max {float(q[2]):.0f} ns")
         if w.numel():
             print(f"   step wall median {float(w.median()):.0f} ns, mean {float(w.mean()):.0f} ns")
         # first 40 steps (full batch)

@@ -141,6 +141,9 @@ int wgrad_lstm_l0(hipStream_t s, int nd, const WgDir* dirs, int M, int K, int F,
 
 // While alive (on this host thread), GEMMs use the co-residency-friendly
 // "side stream" tiling: see abcd_gemm.hip.
+// diagnostics (abcd_debug_persist_prof): the stamp buffer when `bit` is set in its mask, else null
+unsigned long long* debug_prof_buf(int bit);
+
 struct GemmSideScope {
   int prev;
   explicit GemmSideScope(bool on);

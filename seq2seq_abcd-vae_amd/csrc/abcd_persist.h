@@ -49,6 +49,7 @@ struct PBwdArgs {
   unsigned* sync;
   unsigned long long* prof;
   float* part;       // split-K partials: 2 parity slots x groups x H/16 consumers x 4 waves x H/16 producers x 256
+  unsigned* started; // residency count (a zeroed registry line): the last workgroup to start bumps g_bptt_epoch
 };
 
 // Decoder forward (self-feedback LSTM, model.py:147-196): one launch for the
@@ -129,5 +130,13 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
 
 // ABCD_PERSIST=0 disables the persistent path (parity/timing comparisons).
 bool persist_enabled();
+
+// Side-stream gate (abcd_side_gate_enable): a one-wave kernel on the side
+// stream that waits, bounded, until the NEXT encoder BPTT launch has every
+// workgroup resident, so side work queued behind it cannot take that
+// launch's CUs first (two side GEMM workgroups on a CU leave no room for a
+// BPTT member, which then starts only when one of them retires).
+bool side_gate_enabled();
+int side_gate(hipStream_t sw);
 
 }  // namespace abcd

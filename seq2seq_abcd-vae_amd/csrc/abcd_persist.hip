@@ -26,6 +26,7 @@
 // progress, so the launcher checks grid <= CUs x occupancy and otherwise
 // declines (the caller runs the per-step kernels).  Spins are bounded; a
 // timeout sets abcd_device_status() and lets the grid drain.
+#include <atomic>
 #include <mutex>
 #include <vector>
 #include <cstdlib>
@@ -41,6 +42,7 @@ __device__ unsigned g_persist_status = 0;
 __device__ unsigned g_persist_sticky = 0;       // OR of every status abcd_step_status folded (abcd_device_status)
 __device__ unsigned g_persist_abort = 0;        // a wait of the CURRENT launch timed out (zeroed by persist_reset)
 __device__ unsigned g_spin_limit = 1u << 22;    // polls before a hand-off wait gives up (ABCD_SPIN_LIMIT, tests)
+__device__ unsigned g_bptt_epoch = 0;           // encoder BPTT launches whose every workgroup has started
 
 // ---------------------------------------------------------------------------
 // hand-off primitives
@@ -228,6 +230,26 @@ struct GSync {
   }
 };
 
+// residency: each workgroup of an encoder BPTT launch counts itself in on
+// start; the last one bumps the device epoch the side-stream gate waits for
+DEV void bptt_resident(unsigned* started) {
+  if (started && threadIdx.x == 0) {
+    const unsigned n = __hip_atomic_fetch_add(started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n + 1 == gridDim.x) __hip_atomic_fetch_add(&g_bptt_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// the gate: one wave polls until the epoch reaches `target` (bounded: 2^17
+// polls of ~0.2-0.5 us, i.e. tens of ms; a timeout just lets the side work
+// go -- no error)
+__global__ void side_gate_kernel(unsigned target) {
+  if (threadIdx.x == 0) {
+    for (unsigned spins = 0; spins < (1u << 17); ++spins) {
+      if (__hip_atomic_load(&g_bptt_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+}
+
 // diagnostics: thread 0 stamps s_memrealtime (100 MHz, one clock for the whole
 // device, so stamps of different workgroups compare) at the phase boundaries of step i
 #define PSTAMP(k)                                                                                   \
@@ -413,6 +435,7 @@ __global__ __launch_bounds__(256) void enc_fwd_persist(PFwdArgs a) {
 template <int G, int PD>
 __global__ __launch_bounds__(256) void enc_bwd_persist(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  bptt_resident(a.started);
   const int H = a.H, GH = G * H, nut = H / 16, nchg = GH / 16, T = a.T;
   const Role role = assign_role(a.nd * a.nrt, nut);
   const int grp = role.grp, mem = role.mem;
@@ -546,6 +569,7 @@ constexpr int SK_PITCH = 68;  // floats per row of the wave-private dG transpose
 template <int G, int NSUB>
 __global__ __launch_bounds__(256) void enc_bwd_sk(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  bptt_resident(a.started);
   constexpr int H = NSUB * 16, GH = G * H, nut = NSUB;
   const int T = a.T, ng = a.nd * a.nrt;
   const Role role = assign_role(ng, nut);
@@ -1930,6 +1954,7 @@ constexpr int W8_DTP = 132;   // pitch (floats) of the member's 32 x 4*32 dG til
 template <int G>
 __global__ __launch_bounds__(256) void enc_bwd_w8(PBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) f4 smem[];
+  bptt_resident(a.started);
   if (ABCD_BWD_PRIO) __builtin_amdgcn_s_setprio(ABCD_BWD_PRIO);
   constexpr int H = 256, GH = G * H, M = W8_M, NSUB = H / 16;
   constexpr int NC = G;                     // 32-deep chunks = gates
@@ -2348,6 +2373,33 @@ static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
   return (hipError_t)zero_sync_impl(s, sync, ngroups);
 }
 
+// the side-stream gate's bookkeeping: encoder BPTT launches per device (the
+// device counts the same launches once all their workgroups have started)
+static unsigned h_bptt_launches[64];
+static std::atomic<bool> g_side_gate{false};
+static int cur_dev() {
+  int dev = 0;
+  return hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 ? dev : 0;
+}
+// an encoder BPTT launch: its residency line (the first registry line, zeroed
+// by the reset in front of it) and the host launch count
+static void bptt_launch(PBwdArgs& b, int ngroups) {
+  b.started = b.sync + (size_t)2 * ngroups * PERSIST_SYNC_STRIDE;
+  ++h_bptt_launches[cur_dev()];
+}
+// ABCD_SIDE_GATE=0 keeps it off whatever the switch says (same-box A/B)
+bool side_gate_enabled() {
+  static const bool env_off = [] {
+    const char* v = getenv("ABCD_SIDE_GATE");
+    return v && v[0] == '0';
+  }();
+  return g_side_gate.load() && !env_off;
+}
+int side_gate(hipStream_t sw) {
+  side_gate_kernel<<<1, 64, 0, sw>>>(h_bptt_launches[cur_dev()] + 1);
+  return (int)hipGetLastError();
+}
+
 
 // ring depth: the largest of 16 / 4 / 1 dividing the chunk count
 static int ring_depth(int nch) { return nch % 16 == 0 ? 16 : (nch % 4 == 0 ? 4 : 1); }
@@ -2386,6 +2438,7 @@ static int launch_bwd(hipStream_t s, const PBwdArgs& a, bool* launched) {
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_ENC_BWD);
+    bptt_launch(b, a.nd * a.nrt);
     enc_bwd_persist<G, PD><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_ENC_BWD, "enc_bwd_persist<%d,%d> grid %d", G, PD, grid);
@@ -2428,6 +2481,7 @@ static int launch_bwd_sk(hipStream_t s, const PBwdArgs& a, bool* launched) {
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_ENC_BWD);
+    bptt_launch(b, a.nd * a.nrt);
     enc_bwd_sk<G, NSUB><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_ENC_BWD, "enc_bwd_sk<%d,%d> grid %d", G, NSUB, grid);
@@ -2457,6 +2511,7 @@ static int launch_bwd_w8(hipStream_t s, const PBwdArgs& a, bool* launched) {
   b.prof = (g_prof_mask & 2) ? g_prof : nullptr;
   {
     TimedScope ts(s, TK_ENC_BWD);
+    bptt_launch(b, a.nd * nrt);
     enc_bwd_w8<G><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_ENC_BWD, "enc_bwd_w8<%d> grid %d", G, grid);
@@ -2663,10 +2718,15 @@ extern "C" int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream) {
 
 // diagnostics (abcd_hip.h: abcd_debug_persist_prof): stamp buffer for the
 // persistent kernels selected by mask, grid x T x 8 u64, or null to disable
+extern "C" void abcd_side_gate_enable(int on) { abcd::g_side_gate.store(on != 0); }
+
 extern "C" void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask) {
   abcd::g_prof = dev_buf;
   abcd::g_prof_mask = mask;
 }
+namespace abcd {
+unsigned long long* debug_prof_buf(int bit) { return (g_prof_mask & bit) ? g_prof : nullptr; }
+}  // namespace abcd
 
 namespace abcd {
 // stream-ordered: out[0] = the timeout status raised since the last fold

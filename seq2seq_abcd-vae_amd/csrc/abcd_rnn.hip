@@ -1407,6 +1407,10 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
     ABCD_TRY(hipEventRecord(ev, s));
     s = (hipStream_t)wgrad_stream;
     ABCD_TRY(hipStreamWaitEvent(s, ev, 0));
+    // abcd_side_gate_enable: hold the side work until the encoder BPTT that
+    // follows is resident (its members would otherwise wait for CUs the
+    // side GEMMs took first: up to 150 us of start skew measured)
+    if (side_gate_enabled()) ABCD_TRY((hipError_t)side_gate(s));
   }
   GemmSideScope side_tiles(side);
   if (g->f2h_w)

@@ -329,6 +329,11 @@ __global__ void plain_dparams(const float* MV, const float* EPS, int B, int f, c
 // side stream.
 // ---------------------------------------------------------------------------
 constexpr int HEAD_ROWS = 16;
+// diagnostics: thread 0 of each tile stamps s_memrealtime (100 MHz, device-wide) at phase k
+#define HSTAMP(k)                                                                              \
+  do {                                                                                         \
+    if (a.prof && threadIdx.x == 0) a.prof[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 // "last workgroup" tickets (self-resetting): [0] forward KL, [1] backward
 // column sums.  Launches on one device are serialised on the engine's stream.
 __device__ unsigned g_head_ticket[2];
@@ -370,11 +375,11 @@ DEV BKM bkm(const float* p, int ld, int nk) { return BKM{make_rsrc(p, (uint32_t)
 // lda floats).  Wave w takes the 16-column subtiles w*NR.., (w+4)*NR..;
 // epi(c0, acc): lane (r, q) holds rows 4q+g of column c0 + r.  PD chunks of
 // A and B fragments in flight per wave, branch-free.
-template <int NR, int PD, class OB, class Epi>
+template <int NR, int PD, int NW, class OB, class Epi>
 DEV void tile_mma(const float* Al, int lda, int nk, const OB& B, int ncols, int w, int lane, Epi&& epi) {
   const int r = lane & 15, q = lane >> 4;
   const int nsub = ncols >> 4, nch = nk >> 4;
-  for (int j0 = w * NR; j0 < nsub; j0 += 4 * NR) {
+  for (int j0 = w * NR; j0 < nsub; j0 += NW * NR) {
     f4 acc[NR];
     int bn[NR];
     bool bok[NR];
@@ -409,9 +414,9 @@ DEV void tile_mma(const float* Al, int lda, int nk, const OB& B, int ncols, int 
       if (j0 + j < nsub) epi((j0 + j) * 16, acc[j]);
   }
 }
-template <class OB, class Epi>
+template <int NW, class OB, class Epi>
 DEV void tile_mma_any(const float* Al, int lda, int nk, const OB& B, int ncols, int w, int lane, Epi&& epi) {
-  tile_mma<2, 4>(Al, lda, nk, B, ncols, w, lane, epi);
+  tile_mma<2, 4, NW>(Al, lda, nk, B, ncols, w, lane, epi);
 }
 // sum over the 16 rows a lane group holds (rows 4q+g): every lane of the
 // column gets the column's tile sum
@@ -460,6 +465,7 @@ struct HeadFwdArgs {
   float* ppl;        // [exp(mean row entropy of Q), exp(entropy of the batch-mean Q)]
   double* entpart;   // per-tile sum of row entropies
   float* qcolpart;   // tiles x K column sums of Q
+  unsigned long long* prof;  // diagnostics: per-tile phase stamps (tiles x 8), or null
 };
 inline size_t head_fwd_lds(int Hm, int D, int K) {
   return ((size_t)HEAD_ROWS * (std::max(Hm, K) + 4) + (size_t)HEAD_ROWS * (std::max(D, K) + 4) + 2 * (size_t)K) * 4 +
@@ -467,8 +473,9 @@ inline size_t head_fwd_lds(int Hm, int D, int K) {
 }
 
 // KPL: categories per lane, ceil(K / 64) rounded up to a power of two
-template <int KPL>
-__global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
+template <int KPL, int NT>
+__global__ __launch_bounds__(NT) void samp_head_fwd(HeadFwdArgs a) {
+  constexpr int NW = NT / 64, RPW = HEAD_ROWS / NW;  // waves, softmax rows per wave
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   const int Hm = a.Hm, D = a.D, K = a.K;
   const int ld1 = max(Hm, K) + 4, ld2 = max(D, K) + 4;
@@ -480,6 +487,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
   int* flag = reinterpret_cast<int*>(sh + 16);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
   const int row0 = blockIdx.x * HEAD_ROWS, nr = min(HEAD_ROWS, a.B - row0);
+  HSTAMP(0);
   // Prologue, one memory round trip per iteration: (a) this tile's slice of
   // the transposed codebook / W2 (the backward's K-contiguous operands):
   // CT[k][d] = C[d][k], W2T[j][d] = W2[d][j]; (b) Z1 = tanh(sum of the
@@ -495,12 +503,12 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     const __amdgpu_buffer_rsrc_t rB = make_rsrc(a.b1, (uint32_t)Hm * 4u);
     const int h4 = Hm >> 2, nZ = HEAD_ROWS * h4;
     constexpr int UT = 8, UZ = 2;
-    const int itT = (t1 - t0 + 256 * UT - 1) / (256 * UT), itZ = (nZ + 256 * UZ - 1) / (256 * UZ);
+    const int itT = (t1 - t0 + NT * UT - 1) / (NT * UT), itZ = (nZ + NT * UZ - 1) / (NT * UZ);
     for (int it = 0; it < max(itT, itZ); ++it) {
       float tv[UT];
 #pragma unroll
       for (int u = 0; u < UT; ++u) {
-        const int e = t0 + (it * UT + u) * 256 + tid;
+        const int e = t0 + (it * UT + u) * NT + tid;
         const bool inC = e < nC;
         const int k = e / D, d = e - k * D, f = e - nC, jj = f / D, dd = f - jj * D;
         const uint32_t oc = (e < t1 && inC) ? ((uint32_t)d * K + k) * 4u : 0x80000000u;
@@ -510,7 +518,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
       f4 v[UZ][HEAD_MAX_SLABS + 1];  // [.][HEAD_MAX_SLABS]: b1
 #pragma unroll
       for (int u = 0; u < UZ; ++u) {
-        const int e = (it * UZ + u) * 256 + tid, rr = e / h4, c = (e - rr * h4) * 4;
+        const int e = (it * UZ + u) * NT + tid, rr = e / h4, c = (e - rr * h4) * 4;
         const bool ok = e < nZ && rr < nr;
         const uint32_t o = ok ? ((uint32_t)(row0 + rr) * Hm + c) * 4u : 0x80000000u;
 #pragma unroll
@@ -520,12 +528,12 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < UT; ++u) {
-        const int e = t0 + (it * UT + u) * 256 + tid;
+        const int e = t0 + (it * UT + u) * NT + tid;
         if (e < t1) { if (e < nC) a.CT[e] = tv[u]; else a.W2T[e - nC] = tv[u]; }
       }
 #pragma unroll
       for (int u = 0; u < UZ; ++u) {
-        const int e = (it * UZ + u) * 256 + tid, rr = e / h4, c = (e - rr * h4) * 4;
+        const int e = (it * UZ + u) * NT + tid, rr = e / h4, c = (e - rr * h4) * 4;
         if (e >= nZ) continue;
         f4 z = f4zero();
         if (rr < nr) {
@@ -541,8 +549,9 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     }
   }
   __syncthreads();
+  HSTAMP(1);
   // U = Z1 W2^T + b2
-  tile_mma_any(R1, ld1, Hm, bkc(a.W2, Hm, D), D, w, lane, [&](int c0, f4 acc) {
+  tile_mma_any<NW>(R1, ld1, Hm, bkc(a.W2, Hm, D), D, w, lane, [&](int c0, f4 acc) {
     const int col = c0 + r;
     const float bb = a.b2[col];
 #pragma unroll
@@ -554,10 +563,11 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     }
   });
   __syncthreads();
+  HSTAMP(2);
   // logits = U C / sqrt(D)   (C: D x K, the K-major operand; D the model's feature dim)
   const float rs = a.rsD;
   const int Kv = a.Kv;
-  tile_mma_any(R2, ld2, D, bkm(a.C, K, D), K, w, lane, [&](int c0, f4 acc) {
+  tile_mma_any<NW>(R2, ld2, D, bkm(a.C, K, D), K, w, lane, [&](int c0, f4 acc) {
     const int col = c0 + r;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -567,9 +577,11 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
       if (row < nr) a.logits[(long)(row0 + row) * K + col] = v;
     }
   });
+  HSTAMP(3);
   // Dirichlet posterior: elog for the row terms (every tile), the stash once
   prior_block(a.psl, K, Kv, a.N, a.a0, alphaL, elogL, sh, blockIdx.x == 0, a.p, a.alpha, a.elog, a.tri,
               a.kl_small);
+  HSTAMP(4);
   // rows: KL row term v_b = sum_k Q (log Q - elog) (kl_rows) and the sample
   // Y = softmax((logits + g) / tau) (sample_softmax_rows), one wave per row,
   // the row's KPL logits per lane in registers
@@ -578,8 +590,8 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
   float qcol[KPL];
 #pragma unroll
   for (int u = 0; u < KPL; ++u) qcol[u] = 0.f;
-  for (int rr = 0; rr < HEAD_ROWS / 4; ++rr) {
-    const int row = w * (HEAD_ROWS / 4) + rr;
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = w * RPW + rr;
     float* y = R2 + row * ld2;
     if (row >= nr) {
       for (int k = lane; k < K; k += 64) y[k] = 0.f;
@@ -654,7 +666,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
   }
   if (lane == 0) {
     sh[w] = klsum;
-    sh[4 + w] = entsum;
+    sh[NW + w] = entsum;
   }
   __syncthreads();
   if (a.ppl) {  // the waves' Q column sums into the (now free) logits region
@@ -662,8 +674,9 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     for (int u = 0; u < KPL; ++u)
       if (lane + 64 * u < K) R1[w * K + lane + 64 * u] = qcol[u];
   }
+  HSTAMP(5);
   // feats = Y C^T
-  tile_mma_any(R2, ld2, K, bkc(a.C, K, D), D, w, lane, [&](int c0, f4 acc) {
+  tile_mma_any<NW>(R2, ld2, K, bkc(a.C, K, D), D, w, lane, [&](int c0, f4 acc) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int row = 4 * q + g;
@@ -673,13 +686,21 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
   if (!a.kl_out && !a.ppl) return;
   if (a.ppl) {
     __syncthreads();
-    for (int k = tid; k < K; k += 256)
-      st_agent(a.qcolpart + (long)blockIdx.x * K + k, (R1[k] + R1[K + k]) + (R1[2 * K + k] + R1[3 * K + k]));
+    for (int k = tid; k < K; k += NT) {
+      float c = 0.f;  // wave order
+#pragma unroll
+      for (int v = 0; v < NW; ++v) c += R1[v * K + k];
+      st_agent(a.qcolpart + (long)blockIdx.x * K + k, c);
+    }
   }
   if (tid == 0) {
-    st_agent(a.klpart + blockIdx.x, (sh[0] + sh[1]) + (sh[2] + sh[3]));
-    st_agent(a.entpart + blockIdx.x, (sh[4] + sh[5]) + (sh[6] + sh[7]));
+    double kls = 0.0, ens = 0.0;  // wave order
+#pragma unroll
+    for (int v = 0; v < NW; ++v) kls += sh[v], ens += sh[NW + v];
+    st_agent(a.klpart + blockIdx.x, kls);
+    st_agent(a.entpart + blockIdx.x, ens);
   }
+  HSTAMP(6);
   if (!last_workgroup(&g_head_ticket[0], flag)) return;
   const int nt = gridDim.x;
   if (a.kl_out && w == 0) {
@@ -692,18 +713,18 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
   // perplexities (perplex_kernel's formulas): exp(sum of row entropies / B),
   // exp(entropy of the column sums normalised by their total)
   double te = 0.0;
-  for (int i = tid; i < nt; i += 256) te += a.entpart[i];
+  for (int i = tid; i < nt; i += NT) te += a.entpart[i];
   te = block_sum_dd(te, sh);
   double tot = 0.0;
-  for (int k = tid; k < K; k += 256) {
-    float c = 0.f;  // tile order, 8 tiles' loads in flight
+  for (int k = tid; k < K; k += NT) {
+    float c = 0.f;  // tile order, 32 tiles' loads in flight
     int i = 0;
-    for (; i + 8 <= nt; i += 8) {
-      float v8[8];
+    for (; i + 32 <= nt; i += 32) {
+      float v8[32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v8[u] = a.qcolpart[(long)(i + u) * K + k];
+      for (int u = 0; u < 32; ++u) v8[u] = a.qcolpart[(long)(i + u) * K + k];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) c += v8[u];
+      for (int u = 0; u < 32; ++u) c += v8[u];
     }
     for (; i < nt; ++i) c += a.qcolpart[(long)i * K + k];
     R1[k] = c;
@@ -711,7 +732,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
   }
   tot = block_sum_dd(tot, sh);
   double be = 0.0;
-  for (int k = tid; k < K; k += 256) {
+  for (int k = tid; k < K; k += NT) {
     const double bm = R1[k] / tot;
     if (bm > 0) be += -bm * log(bm);
   }
@@ -720,6 +741,7 @@ __global__ __launch_bounds__(256) void samp_head_fwd(HeadFwdArgs a) {
     a.ppl[0] = (float)exp(te / a.B);
     a.ppl[1] = (float)exp(be);
   }
+  HSTAMP(7);
 }
 
 struct HeadBwdArgs {
@@ -732,9 +754,12 @@ struct HeadBwdArgs {
   float* colpart;                          // tiles x (D + Hm + K)
   float *db2, *db1, *dpsl;                 // last workgroup's outputs (each may be null)
   const float *CT, *W2T;                   // transposed copies written by the forward head
+  unsigned long long* prof;                // diagnostics: per-tile phase stamps (tiles x 8), or null
 };
+constexpr int HEAD_THREADS = 512;  // 8 waves per 16-row tile (4: the U / dZ1 products ran two column passes per wave)
 inline size_t head_bwd_lds(int Hm, int D, int K) {
-  return ((size_t)HEAD_ROWS * (K + 4) + (size_t)HEAD_ROWS * (D + 4) + (size_t)HEAD_ROWS * (Hm + 4) + 6 * (size_t)K) *
+  return ((size_t)HEAD_ROWS * (K + 4) + (size_t)HEAD_ROWS * (D + 4) + (size_t)HEAD_ROWS * (Hm + 4) +
+          (size_t)(HEAD_THREADS / 64 + 2) * K) *
              4 + 16 * sizeof(double) + 16;
 }
 
@@ -757,22 +782,24 @@ DEV HeadRow<KPL> head_row_load(const HeadBwdArgs& a, int brow, bool valid, int l
   return h;
 }
 
-template <int KPL>
-__global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
+template <int KPL, int NT>
+__global__ __launch_bounds__(NT) void samp_head_bwd(HeadBwdArgs a) {
+  constexpr int NW = NT / 64, RPW = HEAD_ROWS / NW;  // waves, rows per wave
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   const int Hm = a.Hm, D = a.D, K = a.K;
   const int ld1 = K + 4, ld2 = D + 4, ldz = Hm + 4;
   float* R1 = hsm;                    // dY, then dL
   float* R2 = R1 + HEAD_ROWS * ld1;   // d_feats, then dU
   float* ZL = R2 + HEAD_ROWS * ld2;   // Z1 tile
-  float* QcL = ZL + HEAD_ROWS * ldz;  // per-wave Q column sums (4 x K); the last workgroup's Qsum
-  float* elogL = QcL + 4 * K;
+  float* QcL = ZL + HEAD_ROWS * ldz;  // per-wave Q column sums (NW x K); the last workgroup's Qsum
+  float* elogL = QcL + NW * K;
   double* sh = reinterpret_cast<double*>(elogL + K);
   int* flag = reinterpret_cast<int*>(sh + 16);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, q = lane >> 4;
   const int row0 = blockIdx.x * HEAD_ROWS, nr = min(HEAD_ROWS, a.B - row0);
   const int NC = D + Hm + K;
   float* part = a.colpart + (long)blockIdx.x * NC;
+  HSTAMP(0);
   // stage d_feats, Z1 and elog; zero the Q column sums
   {  // one round trip per iteration: d_feats, Z1 and elog loads all in flight
     const __amdgpu_buffer_rsrc_t rF = make_rsrc(a.dfeat + (long)row0 * D, (uint32_t)nr * D * 4u);
@@ -781,11 +808,11 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
     const int nF = HEAD_ROWS * D / 4, nZ = HEAD_ROWS * Hm / 4, nE = K / 4;
     const int nAll = nF + nZ + nE;
     constexpr int U = 4;
-    for (int e0 = tid; e0 < nAll; e0 += 256 * U) {
+    for (int e0 = tid; e0 < nAll; e0 += NT * U) {
       f4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = e0 + 256 * u;
+        const int e = e0 + NT * u;
         const int ez = e - nF, ee = ez - nZ;
         // rows >= nr lie beyond the d_feats / Z1 resources and read 0
         const uint32_t o = e < nF ? (uint32_t)e * 16u : ez < nZ ? (uint32_t)ez * 16u : ee < nE ? (uint32_t)ee * 16u : 0x80000000u;
@@ -793,7 +820,7 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = e0 + 256 * u;
+        const int e = e0 + NT * u;
         if (e < nF) {
           const int rr = e / (D / 4), c = (e - rr * (D / 4)) * 4;
           *reinterpret_cast<f4*>(R2 + rr * ld2 + c) = v[u];
@@ -806,33 +833,35 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
       }
     }
   }
-  for (int k = tid; k < 4 * K; k += 256) QcL[k] = 0.f;
+  for (int k = tid; k < NW * K; k += NT) QcL[k] = 0.f;
   __syncthreads();
   if (a.dfeat_copy) {
     const int d4 = D >> 2;
-    for (int e = tid; e < nr * d4; e += 256) {
+    for (int e = tid; e < nr * d4; e += NT) {
       const int rr = e / d4, c = (e - rr * d4) * 4;
       *reinterpret_cast<f4*>(a.dfeat_copy + (long)(row0 + rr) * D + c) = *reinterpret_cast<const f4*>(R2 + rr * ld2 + c);
     }
   }
+  HSTAMP(1);
   // dY = d_feats C
-  tile_mma_any(R2, ld2, D, bkc(a.CT, D, K), K, w, lane, [&](int c0, f4 acc) {
+  tile_mma_any<NW>(R2, ld2, D, bkc(a.CT, D, K), K, w, lane, [&](int c0, f4 acc) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) R1[(4 * q + g) * ld1 + c0 + r] = acc[g];
   });
   __syncthreads();
+  HSTAMP(2);
   // dL = Y (dY - sum Y dY) / tau  +  s Q ((log Q - elog) - v_b)
   // (sample_softmax_bwd + kl_rows_bwd), one wave per row; the next row's
   // Y / Q / v_b loads are in flight while this row is reduced
   const float s = *a.dkl, rs = a.rsD;
   {
-    const int rbase = w * (HEAD_ROWS / 4);
+    const int rbase = w * RPW;
     float* qc = QcL + w * K;
     HeadRow<KPL> cur = head_row_load<KPL>(a, row0 + rbase, rbase < nr, lane);
-    for (int rr = 0; rr < HEAD_ROWS / 4; ++rr) {
+    for (int rr = 0; rr < RPW; ++rr) {
       const int row = rbase + rr;
       HeadRow<KPL> nxt = cur;
-      if (rr + 1 < HEAD_ROWS / 4) nxt = head_row_load<KPL>(a, row0 + row + 1, row + 1 < nr, lane);
+      if (rr + 1 < RPW) nxt = head_row_load<KPL>(a, row0 + row + 1, row + 1 < nr, lane);
       float* d = R1 + row * ld1;
       if (row < nr) {
         const long g0 = (long)(row0 + row) * K;
@@ -862,9 +891,15 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
   }
   __syncthreads();
   // Qsum partial of this tile (the prior gradient's column sums)
-  for (int k = tid; k < K; k += 256) st_agent(part + D + Hm + k, (QcL[k] + QcL[K + k]) + (QcL[2 * K + k] + QcL[3 * K + k]));
+  for (int k = tid; k < K; k += NT) {
+    float c = 0.f;  // wave order
+#pragma unroll
+    for (int v = 0; v < NW; ++v) c += QcL[v * K + k];
+    st_agent(part + D + Hm + k, c);
+  }
+  HSTAMP(3);
   // dU = dL C^T / sqrt(D)  (+ the db2 partial)
-  tile_mma_any(R1, ld1, K, bkc(a.C, K, D), D, w, lane, [&](int c0, f4 acc) {
+  tile_mma_any<NW>(R1, ld1, K, bkc(a.C, K, D), D, w, lane, [&](int c0, f4 acc) {
     const int col = c0 + r;
     f4 v;
 #pragma unroll
@@ -878,8 +913,9 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
     if (q == 0) st_agent(part + col, cs);
   });
   __syncthreads();
+  HSTAMP(4);
   // dZ1 = (dU W2) (1 - Z1^2)  (+ the db1 partial)
-  tile_mma_any(R2, ld2, D, bkc(a.W2T, D, Hm), Hm, w, lane, [&](int c0, f4 acc) {
+  tile_mma_any<NW>(R2, ld2, D, bkc(a.W2T, D, Hm), Hm, w, lane, [&](int c0, f4 acc) {
     const int col = c0 + r;
     f4 v;
 #pragma unroll
@@ -892,19 +928,20 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
     const float cs = tile_colsum(v);
     if (q == 0) st_agent(part + D + col, cs);
   });
+  HSTAMP(5);
   if (!last_workgroup(&g_head_ticket[1], flag)) return;
   // last workgroup: column sums over the tiles (tile order) -> db2, db1,
   // Qsum; then the Dirichlet prior's gradient
   const int nt = gridDim.x;
-  for (int c = tid; c < NC; c += 256) {
-    float t = 0.f;  // tile order; 8 tiles' loads in flight
+  for (int c = tid; c < NC; c += NT) {
+    float t = 0.f;  // tile order; 32 tiles' loads in flight (8: 12 us for 640 columns x 32 tiles)
     int i = 0;
-    for (; i + 8 <= nt; i += 8) {
-      float v[8];
+    for (; i + 32 <= nt; i += 32) {
+      float v[32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = a.colpart[(long)(i + u) * NC + c];
+      for (int u = 0; u < 32; ++u) v[u] = a.colpart[(long)(i + u) * NC + c];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t += v[u];
+      for (int u = 0; u < 32; ++u) t += v[u];
     }
     for (; i < nt; ++i) t += a.colpart[(long)i * NC + c];
     if (c < D) { if (a.db2) a.db2[c] = t; }
@@ -912,7 +949,9 @@ __global__ __launch_bounds__(256) void samp_head_bwd(HeadBwdArgs a) {
     else QcL[c - D - Hm] = t;
   }
   __syncthreads();
+  HSTAMP(6);
   if (a.dpsl) prior_bwd_block(a.p, a.alpha, a.tri, a.kl_small, QcL, a.Kv, a.B, a.N, a.a0, s, a.dpsl, sh);
+  HSTAMP(7);
 }
 
 // KPL dispatch: K <= 64 * KPL
@@ -940,8 +979,8 @@ static int head_lds_attr(const void* fn, size_t lds) {  // once per kernel insta
 template <int KPL>
 struct HeadFwdLaunch {
   static int run(const HeadFwdArgs& a, int grid, size_t lds, hipStream_t s) {
-    ABCD_TRY((hipError_t)head_lds_attr((const void*)samp_head_fwd<KPL>, lds));
-    samp_head_fwd<KPL><<<grid, 256, lds, s>>>(a);
+    ABCD_TRY((hipError_t)head_lds_attr((const void*)samp_head_fwd<KPL, HEAD_THREADS>, lds));
+    samp_head_fwd<KPL, HEAD_THREADS><<<grid, HEAD_THREADS, lds, s>>>(a);
     ABCD_CHECK_LAUNCH();
     return 0;
   }
@@ -949,8 +988,8 @@ struct HeadFwdLaunch {
 template <int KPL>
 struct HeadBwdLaunch {
   static int run(const HeadBwdArgs& a, int grid, size_t lds, hipStream_t s) {
-    ABCD_TRY((hipError_t)head_lds_attr((const void*)samp_head_bwd<KPL>, lds));
-    samp_head_bwd<KPL><<<grid, 256, lds, s>>>(a);
+    ABCD_TRY((hipError_t)head_lds_attr((const void*)samp_head_bwd<KPL, HEAD_THREADS>, lds));
+    samp_head_bwd<KPL, HEAD_THREADS><<<grid, HEAD_THREADS, lds, s>>>(a);
     ABCD_CHECK_LAUNCH();
     return 0;
   }
@@ -1159,6 +1198,7 @@ extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_
   a.klpart = w.klpart; a.kl_out = kl_out;
   a.CT = w.CT; a.W2T = w.W2T[0];
   a.ppl = ppl_out; a.entpart = w.entpart; a.qcolpart = w.qcolpart;
+  a.prof = debug_prof_buf(16);
   const int grid = cdiv(B, HEAD_ROWS);
   ABCD_TRY((hipError_t)head_dispatch<HeadFwdLaunch>(K, a, grid, lds, s));
   note_dispatch(TK_SAMP_FWD, "gemm_slabs[%d] + samp_head_fwd grid %d", Z, grid);
@@ -1330,6 +1370,7 @@ static int samp_fused_bwd(const abcd_sampler_cfg* c, const abcd_sampler_params* 
   a.dLs = w.YdL + (size_t)B * K; a.dU = w.dU; a.dZ1 = w.dZ1[0];
   a.colpart = w.colpart; a.db2 = mg.b2; a.db1 = mg.b1; a.dpsl = g->posterior_shape_logits;
   a.CT = w.CT; a.W2T = w.W2T[0];
+  a.prof = debug_prof_buf(32);
   const size_t lds = head_bwd_lds(Hm, D, K);
   const int grid = cdiv(B, HEAD_ROWS);
   ABCD_TRY((hipError_t)head_dispatch<HeadBwdLaunch>(K, a, grid, lds, s));

@@ -164,6 +164,7 @@ _SIGS = {
     "abcd_dispatch_count": (c_long, [c_int]),
     "abcd_dispatch_reset": (None, []),
     "abcd_debug_persist_prof": (None, [c_void_p, c_int]),
+    "abcd_side_gate_enable": (None, [c_int]),
     "abcd_debug_xcc_map": (c_int, [c_void_p, c_int, c_void_p]),
     "abcd_fill_normal": (c_int, [c_void_p, c_long, c_uint64, c_uint64, c_void_p]),
     "abcd_fill_dropout": (c_int, [c_void_p, c_long, c_float, c_uint64, c_uint64, c_void_p]),

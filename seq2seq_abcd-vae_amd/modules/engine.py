@@ -232,10 +232,16 @@ class FusedStep:
         # the decoder's weight-gradient reductions run on a side stream beside
         # the sampler + encoder backward (joined below, before clip + SGD):
         # measured at c2 ~0.5 ms/step shorter than serial (DESIGN.md §3 Streams)
-        N.check(L_.abcd_decoder_backward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
-                                                 N.ptr(xmask), N.ptr(inv), N.ptr(inv), N.ptr(d_feats), self.dec_g,
-                                                 N.ptr(ws_d), ws_d.numel(), st, side_p),
-                "decoder backward")
+        # (the side work waits on the device until the encoder BPTT queued below
+        # is resident on every CU: abcd_side_gate_enable, read at this call)
+        L_.abcd_side_gate_enable(1)
+        try:
+            N.check(L_.abcd_decoder_backward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
+                                                     N.ptr(xmask), N.ptr(inv), N.ptr(inv), N.ptr(d_feats),
+                                                     self.dec_g, N.ptr(ws_d), ws_d.numel(), st, side_p),
+                    "decoder backward")
+        finally:
+            L_.abcd_side_gate_enable(0)
         d_h = torch.empty(B, self.E, device=dev)
         # the sampler's codebook / W2 / W1 gradients (one batched launch) are
         # taken off the d_h -> enc_bwd chain (59-85 us there beside the
