@@ -176,6 +176,16 @@ int abcd_sampler_kl(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, c
  * perplexities of abcd_perplexities on these logits (reduced by the same
  * last tile); ppl_out[2] is left to abcd_shape_perplexity (it reads
  * posterior_shape_logits after the SGD step, learning.py:171-178). */
+/* The Dirichlet prior's per-category terms of ABCDSampler.kl_divergence
+ * (model.py:608-639: alpha = softmax(posterior_shape_logits) * N + a0, its
+ * digamma / trigamma / lgamma terms) into the workspace stash -- they depend
+ * on the parameters only, not on the batch, so a training step can run this
+ * one-workgroup kernel on a side stream early and pass
+ * mode | ABCD_SAMPLE_PRIOR_READY to abcd_sampler_forward_fused (same ws and
+ * B, same entire_data_size, the side stream joined first).  plain: no-op. */
+#define ABCD_SAMPLE_PRIOR_READY 0x100
+int abcd_sampler_prior(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, int B, double entire_data_size,
+                       void* ws, size_t ws_bytes, void* stream);
 int abcd_sampler_forward_fused(const abcd_sampler_cfg* cfg, const abcd_sampler_params* p, const float* h, int B,
                                int mode, float temperature, const float* noise, uint64_t seed, uint64_t offset,
                                double entire_data_size, float* logits, float* feats, float* kl_out, float* ppl_out,

@@ -456,6 +456,7 @@ struct HeadFwdArgs {
   const float *slab, *b1, *W2, *b2, *C, *psl;  // slab: nslab x B x Hm raw partials of h W1^T
   double N; float a0;
   int gumbel; float tau; const float* noise; uint64_t seed, offset;
+  int prior_ready;  // the prior stash (p, alpha, elog, tri, kl_small) filled by abcd_sampler_prior
   float *Z1, *U, *logits, *Y, *Q, *v, *feats;
   float *p, *alpha, *elog, *tri; double* kl_small;  // prior stash (written by workgroup 0)
   double* klpart;                                   // per-tile sum_b v_b
@@ -579,8 +580,14 @@ __global__ __launch_bounds__(NT) void samp_head_fwd(HeadFwdArgs a) {
   });
   HSTAMP(3);
   // Dirichlet posterior: elog for the row terms (every tile), the stash once
-  prior_block(a.psl, K, Kv, a.N, a.a0, alphaL, elogL, sh, blockIdx.x == 0, a.p, a.alpha, a.elog, a.tri,
-              a.kl_small);
+  // -- or, with the stash filled ahead by abcd_sampler_prior, elog read from it
+  if (a.prior_ready) {
+    for (int k = tid; k < K; k += NT) elogL[k] = a.elog[k];
+    __syncthreads();
+  } else {
+    prior_block(a.psl, K, Kv, a.N, a.a0, alphaL, elogL, sh, blockIdx.x == 0, a.p, a.alpha, a.elog, a.tri,
+                a.kl_small);
+  }
   HSTAMP(4);
   // rows: KL row term v_b = sum_k Q (log Q - elog) (kl_rows) and the sample
   // Y = softmax((logits + g) / tau) (sample_softmax_rows), one wave per row,
@@ -1156,11 +1163,26 @@ extern "C" int abcd_sampler_kl(const abcd_sampler_cfg* c, const abcd_sampler_par
 // ---- the fused training-step forward: forward + sample + kl in two launches ----
 constexpr size_t HEAD_LDS_MAX = 160 * 1024;
 
+extern "C" int abcd_sampler_prior(const abcd_sampler_cfg* c, const abcd_sampler_params* p, int B, double N,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  ABCD_REQUIRE(samp_check(c) == 0 && p && ws && B > 0 && N > 0);
+  if (c->plain) return 0;
+  Arena A(ws, ws_bytes);
+  SampWS w = carve_sampler(A, c, B);
+  ABCD_REQUIRE(A.ok);
+  kl_prior<<<1, 256, 0, (hipStream_t)stream>>>(p->posterior_shape_logits, c->num_categories, kvalid(c), N,
+                                               p->prior_concentration, w.p, w.alpha, w.elog, w.tri, w.kl_small);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_sampler_params* p, const float* h,
                                           int B, int mode, float temperature, const float* noise, uint64_t seed,
                                           uint64_t offset, double N, float* logits, float* feats, float* kl_out,
                                           float* ppl_out, void* ws, size_t ws_bytes, void* stream) {
   ABCD_REQUIRE(samp_check(c) == 0 && p && h && logits && feats && ws && B > 0);
+  const bool prior_ready = (mode & ABCD_SAMPLE_PRIOR_READY) != 0;
+  mode &= ~ABCD_SAMPLE_PRIOR_READY;
   const int E = c->input_size, Hm = c->mlp_hidden, D = c->feature_dim, K = c->num_categories;
   const size_t lds = c->plain ? 0 : head_fwd_lds(Hm, D, K);
   if (c->plain || lds > HEAD_LDS_MAX || K > 1024) {  // the three reference methods in turn
@@ -1193,6 +1215,7 @@ extern "C" int abcd_sampler_forward_fused(const abcd_sampler_cfg* c, const abcd_
   a.N = N > 0 ? N : 1.0; a.a0 = p->prior_concentration;
   a.gumbel = mode == ABCD_SAMPLE_GUMBEL; a.tau = a.gumbel ? temperature : 1.f;
   a.noise = noise; a.seed = seed; a.offset = offset;
+  a.prior_ready = prior_ready ? 1 : 0;
   a.Z1 = w.Z1[0]; a.U = w.U; a.logits = logits; a.Y = w.Y; a.Q = w.Q; a.v = w.v; a.feats = feats;
   a.p = w.p; a.alpha = w.alpha; a.elog = w.elog; a.tri = w.tri; a.kl_small = w.kl_small;
   a.klpart = w.klpart; a.kl_out = kl_out;

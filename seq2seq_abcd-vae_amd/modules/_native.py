@@ -97,6 +97,7 @@ _SIGS = {
                                     c_uint64, c_uint64, c_void_p, c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_kl": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_double, c_void_p, c_void_p,
                                 c_size_t, c_void_p]),
+    "abcd_sampler_prior": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_int, c_double, c_void_p, c_size_t, c_void_p]),
     "abcd_sampler_forward_fused": (c_int, [_P(SamplerCfg), _P(SamplerParams), c_void_p, c_int, c_int, c_float,
                                            c_void_p, c_uint64, c_uint64, c_double, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -309,6 +310,7 @@ def stream():
     return c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+SAMPLE_PRIOR_READY = 0x100  # abcd_hip.h ABCD_SAMPLE_PRIOR_READY
 DEFER_PARAMS = c_void_p(2 ** 64 - 1)  # abcd_hip.h ABCD_DEFER_PARAMS ((void*)-1)
 
 

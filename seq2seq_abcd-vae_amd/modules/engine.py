@@ -191,11 +191,18 @@ class FusedStep:
         pdrop = self.decoder._input_dropout_p() if train else 0.0
         eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
         side = self._side_stream()
+        side.wait_stream(torch.cuda.current_stream(dev))  # the previous step (parameters, eps) is queued before
         if eps is None:  # Philox mode: eps[row, f] = philox_normal(eseed, eoff + row * F + f)
             eps = self._workspace("eps", L * F * 4)[:L * F * 4].view(torch.float32)
-            side.wait_stream(torch.cuda.current_stream(dev))  # eps is free (the previous step is queued before)
             N.check(L_.abcd_fill_normal(N.ptr(eps), L * F, eseed, eoff, N.c_void_p(side.cuda_stream)),
                     "decoder noise")
+        # the Dirichlet prior's per-category terms depend on the parameters
+        # only: one small kernel on the side stream now instead of in every
+        # sampler-head tile on the sampler's chain (abcd_sampler_prior)
+        prior = not self.plain
+        if prior:
+            N.check(L_.abcd_sampler_prior(self.samp_cfg, self.samp_p, B, float(entire_data_size), N.ptr(ws_s),
+                                          ws_s.numel(), N.c_void_p(side.cuda_stream)), "sampler prior")
         N.check(L_.abcd_encoder_forward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(h),
                                                 N.ptr(ws_e), ws_e.numel(), st), "encoder forward")
         logits = torch.empty(B, W, device=dev)
@@ -204,7 +211,10 @@ class FusedStep:
         # feature_sampler(h) -> .sample(logits) -> .kl_divergence(logits, N)
         # (learning.py:149-153): ABCD = the split-K MLP GEMM + one row-tiled
         # sampler-head kernel (logits, Gumbel-softmax, y C^T, KL) per step
-        N.check(L_.abcd_sampler_forward_fused(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau, N.ptr(nt), seed,
+        if prior:
+            torch.cuda.current_stream(dev).wait_stream(side)  # the prior stash (and the decoder noise)
+        N.check(L_.abcd_sampler_forward_fused(self.samp_cfg, self.samp_p, N.ptr(h), B,
+                                              mode | (N.SAMPLE_PRIOR_READY if prior else 0), tau, N.ptr(nt), seed,
                                               off, float(entire_data_size), N.ptr(logits), N.ptr(feats),
                                               N.ptr(sc[KL:KL + 1]),
                                               None if self.plain else N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 2]),
