@@ -255,19 +255,18 @@ class FusedStep:
         d_h = torch.empty(B, self.E, device=dev)
         # the sampler's codebook / W2 / W1 gradients (one batched launch) are
         # taken off the d_h -> enc_bwd chain (59-85 us there beside the
-        # decoder's weight gradients; 31-38 us after gemm_wg3b, on the tail)
+        # decoder's weight gradients) and queued after the encoder's backward
+        # (31-38 us on a quiet chip; on the side stream behind the decoder's
+        # weight gradients they ran beside gemm_wg3b and slowed it ~45 us)
         N.check(L_.abcd_sampler_backward_split(self.samp_cfg, self.samp_p, N.ptr(h), B, mode, tau,
                                                float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
                                                self.samp_g, N.ptr(ws_s), ws_s.numel(), st, N.DEFER_PARAMS),
                 "sampler backward")
-        # ... queued on the side stream behind the decoder's weight gradients
-        # (which end before the encoder BPTT does), in the tiling that shares
-        # the CUs with the BPTT: off the step's tail
-        N.check(L_.abcd_sampler_backward_params(self.samp_cfg, self.samp_p, N.ptr(h), B, self.samp_g, N.ptr(ws_s),
-                                                ws_s.numel(), st, side_p), "sampler parameter gradients")
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
                                                  self.enc_g, N.ptr(ws_e), ws_e.numel(), st, side_p),
                 "encoder backward")
+        N.check(L_.abcd_sampler_backward_params(self.samp_cfg, self.samp_p, N.ptr(h), B, self.samp_g, N.ptr(ws_s),
+                                                ws_s.numel(), st, None), "sampler parameter gradients")
         torch.cuda.current_stream(dev).wait_stream(side)
         if self.pad is not None:  # the real positions of the twin's gradients
             torch.index_select(self.kflat.grad, 0, self.pad_index, out=self.flat.grad)
