@@ -213,24 +213,17 @@ class FusedStep:
         # sampler-head kernel (logits, Gumbel-softmax, y C^T, KL) per step
         if prior:
             torch.cuda.current_stream(dev).wait_stream(side)  # the prior stash (and the decoder noise)
-        # the cluster / batch perplexities (learning.py:171-178, reported only)
-        # from the logits on the side stream, off the sampler -> decoder chain
-        # (the head kernel's last tile spent ~7 us on them); the zero-padded
-        # twin keeps the in-kernel form (it knows the valid categories)
-        ppl_side = not self.plain and self.pad is None
+        # (the cluster / batch perplexities stay in the head kernel's last
+        # tile: a separate perplexity kernel on the side stream, placed before
+        # dec_fwd or dec_bwd, held a CU one of their members then waited for --
+        # 12-27 us of start skew -- for the ~5 us it saved here)
         N.check(L_.abcd_sampler_forward_fused(self.samp_cfg, self.samp_p, N.ptr(h), B,
                                               mode | (N.SAMPLE_PRIOR_READY if prior else 0), tau, N.ptr(nt), seed,
                                               off, float(entire_data_size), N.ptr(logits), N.ptr(feats),
                                               N.ptr(sc[KL:KL + 1]),
-                                              None if (self.plain or ppl_side) else
-                                              N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 2]),
+                                              None if self.plain else N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 2]),
                                               N.ptr(ws_s), ws_s.numel(), st), "sampler")
-        torch.cuda.current_stream(dev).wait_stream(side)  # the decoder noise (before the perplexities join it)
-        if ppl_side:  # out[2] (the shape perplexity) is rewritten after the SGD step
-            side.wait_stream(torch.cuda.current_stream(dev))
-            N.check(L_.abcd_perplexities(N.ptr(logits), B, W, N.ptr(self.sampler.posterior_shape_logits),
-                                         N.ptr(sc[PPL_CLUSTER:PPL_SHAPE + 1]), N.c_void_p(side.cuda_stream)),
-                    "perplexities")
+        torch.cuda.current_stream(dev).wait_stream(side)  # the decoder noise
         spk = None
         if kdec.embed_speaker is not None:
             spk = speakers.to(dev, torch.int64).contiguous()
