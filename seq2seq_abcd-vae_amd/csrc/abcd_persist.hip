@@ -2393,7 +2393,7 @@ bool side_gate_enabled() {
     const char* v = getenv("ABCD_SIDE_GATE");
     return v && v[0] == '0';
   }();
-  return g_side_gate.load() && !env_off;
+  return g_side_gate.load() && !env_off && persist_enabled();  // (no persistent BPTT: nothing to wait for)
 }
 int side_gate(hipStream_t sw) {
   side_gate_kernel<<<1, 64, 0, sw>>>(h_bptt_launches[cur_dev()] + 1);
