@@ -147,9 +147,11 @@ DEV void prior_block(const float* psl, int K, int Kv, double N, float a0, float*
     acc = block_sum_dd(acc, sh);
     if (tid == 0) {
       const double a0d = a0;
-      kl_small[0] = lgamma(S) + acc - (lgamma(a0d * K) - K * lgamma(a0d));
-      kl_small[1] = trigamma_d(S);
-      kl_small[2] = S;
+      // write-through: the forward head's last workgroup reads [0] in this launch
+      __hip_atomic_store(kl_small, lgamma(S) + acc - (lgamma(a0d * K) - K * lgamma(a0d)), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(kl_small + 1, trigamma_d(S), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(kl_small + 2, S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
@@ -426,22 +428,23 @@ DEV float tile_colsum(f4 v) {
   c += __shfl_xor(c, 32, 64);
   return c;
 }
-// true in every thread of the last workgroup to call it (after this
-// workgroup's global stores); that workgroup then reads the others' partials
-// with agent-scope loads
+// true in every thread of the last workgroup to call it.  The hand-over is
+// write-through (MI355X_MICROARCH.md visibility table, R1): every partial the
+// last workgroup reads was stored by st_agent (sc1) and drained by its wave
+// (vmcnt(0)) before the barrier and the relaxed ticket add, and is read back
+// with ld_agent (sc1) -- no L2 write-back / invalidate (__threadfence: ~3.5
+// us per call, twice on the last workgroup's path)
 DEV bool last_workgroup(unsigned* ticket, int* flag_sh) {
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned n = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned n = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool last = n == gridDim.x - 1;
     if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag_sh = last;
   }
   __syncthreads();
-  const bool last = *flag_sh != 0;
-  if (last) __threadfence();
-  return last;
+  return *flag_sh != 0;
 }
 template <class T>
 DEV T ld_agent(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -712,15 +715,15 @@ __global__ __launch_bounds__(NT) void samp_head_fwd(HeadFwdArgs a) {
   const int nt = gridDim.x;
   if (a.kl_out && w == 0) {
     double t = 0.0;  // lane-strided partial sums, then a fixed shuffle tree: deterministic
-    for (int i = lane; i < nt; i += 64) t += a.klpart[i];
+    for (int i = lane; i < nt; i += 64) t += ld_agent(a.klpart + i);
     t = wave_sum_d(t);
-    if (lane == 0) *a.kl_out = (float)(a.kl_small[0] * ((double)a.B / a.N) + t);
+    if (lane == 0) *a.kl_out = (float)(ld_agent(a.kl_small) * ((double)a.B / a.N) + t);
   }
   if (!a.ppl) return;
   // perplexities (perplex_kernel's formulas): exp(sum of row entropies / B),
   // exp(entropy of the column sums normalised by their total)
   double te = 0.0;
-  for (int i = tid; i < nt; i += NT) te += a.entpart[i];
+  for (int i = tid; i < nt; i += NT) te += ld_agent(a.entpart + i);
   te = block_sum_dd(te, sh);
   double tot = 0.0;
   for (int k = tid; k < K; k += NT) {
@@ -729,11 +732,11 @@ __global__ __launch_bounds__(NT) void samp_head_fwd(HeadFwdArgs a) {
     for (; i + 32 <= nt; i += 32) {
       float v8[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) v8[u] = a.qcolpart[(long)(i + u) * K + k];
+      for (int u = 0; u < 32; ++u) v8[u] = ld_agent(a.qcolpart + (long)(i + u) * K + k);
 #pragma unroll
       for (int u = 0; u < 32; ++u) c += v8[u];
     }
-    for (; i < nt; ++i) c += a.qcolpart[(long)i * K + k];
+    for (; i < nt; ++i) c += ld_agent(a.qcolpart + (long)i * K + k);
     R1[k] = c;
     tot += c;
   }
@@ -946,11 +949,11 @@ __global__ __launch_bounds__(NT) void samp_head_bwd(HeadBwdArgs a) {
     for (; i + 32 <= nt; i += 32) {
       float v[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) v[u] = a.colpart[(long)(i + u) * NC + c];
+      for (int u = 0; u < 32; ++u) v[u] = ld_agent(a.colpart + (long)(i + u) * NC + c);
 #pragma unroll
       for (int u = 0; u < 32; ++u) t += v[u];
     }
-    for (; i < nt; ++i) t += a.colpart[(long)i * NC + c];
+    for (; i < nt; ++i) t += ld_agent(a.colpart + (long)i * NC + c);
     if (c < D) { if (a.db2) a.db2[c] = t; }
     else if (c < D + Hm) { if (a.db1) a.db1[c - D] = t; }
     else QcL[c - D - Hm] = t;
