@@ -1009,6 +1009,178 @@ static int gemm_x6r_launch(hipStream_t s, int M, int N, int K, const float* A, l
   return 0;
 }
 
+// gemm_x6r8: gemm_x6r with EIGHT waves (two per SIMD) sharing the resident B
+// slice.  With one wave per SIMD every A-load wait, split, B-plane read and
+// epilogue store of gemm_x6r sits between its MFMAs (36 % MFMA busy at the
+// input projection); a second wave issues its MFMAs in those gaps.  The
+// register budget halves (256 per wave), so the look-ahead is a rolling one
+// in the same registers: as soon as chunk c of a block is split, the next
+// block's chunk c is loaded into the fragment registers it came from.  The
+// epilogue stages HR rows per wave (HR = 8 where 16 rows of the slice width
+// would not fit beside the B planes).
+template <int NC, int BN, int MR, int HR>
+__global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restrict__ A, long lda,
+                                                        const float* __restrict__ B, long ldb, int K, EpiArgs e,
+                                                        int nslices, int rows_per) {
+  extern __shared__ __attribute__((aligned(16))) f4 rsm[];
+  constexpr int NR = BN / 16, SP = BN + 4, NW = 8, NPP = HR * BN / 256;
+  static_assert(HR == 8 || HR == 16, "staging rows");
+  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3;  // grid = 8 * per
+  const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int slice = lin % nslices, part = lin / nslices;
+  const int n0 = slice * BN, M = e.M, N = e.N;
+  {  // B slice -> LDS planes [j][c][plane][lane] (as gemm_x6r)
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (size_t)n0 * ldb, (uint32_t)(std::max(0, std::min(BN, N - n0)) * ldb * 4));
+    for (int x = threadIdx.x; x < NR * NC * 64; x += 64 * NW) {
+      const int j = x / (NC * 64), c = (x / 64) % NC, ln = x & 63;
+      const int row = 16 * j + (ln & 15), kk = 32 * c + 8 * (ln >> 4);
+      const uint32_t o = kk < K ? (uint32_t)(row * ldb + kk) * 4u : 0x80000000u;
+      const f4 lo = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, o, 0, 0));
+      const f4 hi = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, kk < K ? o + 16u : o, 0, 0));
+      bf8 h, m, l;
+      split8(lo, hi, h, m, l);
+      f4* d = rsm + ((j * NC + c) * 3) * 64 + ln;
+      d[0] = __builtin_bit_cast(f4, h);
+      d[64] = __builtin_bit_cast(f4, m);
+      d[128] = __builtin_bit_cast(f4, l);
+    }
+  }
+  float* stg = reinterpret_cast<float*>(rsm + NR * NC * 3 * 64) + w * HR * SP;
+  __syncthreads();
+  const int r0 = part * rows_per, r1 = std::min(M, r0 + rows_per);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A, (uint32_t)((size_t)M * lda * 4));
+  // the lane's A fragments of chunk c of the block at row b: rows b + 16 i + r, k = 32 c + 8 q + 0..7
+  auto aload = [&](int b, int c, f4 (&v)[MR][NC][2]) {
+    const int kk = 32 * c + 8 * q;
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const uint32_t o = kk < K ? (uint32_t)((b + 16 * i + r) * lda + kk) * 4u : 0x80000000u;
+      v[i][c][0] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, o, 0, 0));
+      v[i][c][1] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, kk < K ? o + 16u : o, 0, 0));
+    }
+  };
+  constexpr int RB = 16 * MR;
+  const int ec = n0 + 4 * (lane % (BN / 4));
+  f4 bq = f4zero();
+  if (e.bias) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bq[t] = ec + t < N ? e.bias[ec + t] : 0.f;
+  }
+  f4 va[MR][NC][2];
+  int b = r0 + w * RB;
+  if (b < r1) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) aload(b, c, va);
+  }
+  for (; b < r1; b += NW * RB) {
+    const int bn = b + NW * RB;  // the next block (rows past M read 0; past r1 a wasted read)
+    f4 acc[MR][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) acc[i][j] = f4zero();
+    auto bread = [&](int c, int j, f4 (&bb)[3]) {
+      const f4* bp = rsm + ((j * NC + c) * 3) * 64 + lane;
+      bb[0] = bp[0], bb[1] = bp[64], bb[2] = bp[128];
+    };
+    f4 bcur[3];
+    bread(0, 0, bcur);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      bf8 as[MR][3];
+#pragma unroll
+      for (int i = 0; i < MR; ++i) split8(va[i][c][0], va[i][c][1], as[i][0], as[i][1], as[i][2]);
+      // the rolling look-ahead, unconditional: a conditional load makes the
+      // compiler copy the fragments at the loop latch behind a vmcnt(0)
+      aload(bn, c, va);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        f4 bnxt[3];
+        const bool nx = j + 1 < NR || c + 1 < NC;
+        if (nx) bread(j + 1 < NR ? c : c + 1, j + 1 < NR ? j + 1 : 0, bnxt);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+          acc[i][j] = mma_x6(acc[i][j], as[i][0], as[i][1], as[i][2], __builtin_bit_cast(bf8, bcur[0]),
+                             __builtin_bit_cast(bf8, bcur[1]), __builtin_bit_cast(bf8, bcur[2]));
+        __builtin_amdgcn_sched_barrier(0);
+        if (nx) bcur[0] = bnxt[0], bcur[1] = bnxt[1], bcur[2] = bnxt[2];
+      }
+    }
+    // epilogue: HR rows x BN at a time through the wave's LDS tile
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+#pragma unroll
+      for (int h = 0; h < 16 / HR; ++h) {
+        __builtin_amdgcn_wave_barrier();
+        if (HR == 16 || (q >> 1) == h) {
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) stg[(4 * q + g - HR * h) * SP + 16 * j + r] = acc[i][j][g];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int pp = 0; pp < NPP; ++pp) {
+          const int lr = (lane + 64 * pp) / (BN / 4), col = ec;
+          const int row = b + 16 * i + HR * h + lr;
+          f4 val = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * (lane % (BN / 4)));
+          if (row < r1 && col < N) {
+            float* d = e.C + (long)row * e.ldc + col;
+            val = val * e.alpha + bq;
+            if (e.beta != 0.f) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+                if (col + t < N) val[t] += e.beta * d[t];
+            }
+            if (e.act == ACT_TANH) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t) val[t] = tanhf(val[t]);
+            }
+            if (col + 4 <= N) *reinterpret_cast<f4*>(d) = val;
+            else
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+                if (col + t < N) d[t] = val[t];
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int NC, int BN, int MR, int HR>
+static int gemm_x6r8_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
+                            EpiArgs e) {
+  const int nslices = cdiv(N, BN);
+  const int step = 8 / std::gcd(nslices, 8);  // as gemm_x6r_launch, one workgroup per CU
+  const int nparts = std::max(step, (256 / nslices) / step * step);
+  const int grid = nslices * nparts;
+  const int rows_per = ((cdiv(M, nparts) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
+  const size_t lds = (size_t)(BN / 16) * NC * 3 * 64 * 16 + (size_t)8 * HR * (BN + 4) * 4;
+  static bool attr = false;
+  if (!attr) {
+    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_x6r8_kernel<NC, BN, MR, HR>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  gemm_x6r8_kernel<NC, BN, MR, HR><<<grid, 512, lds, s>>>(A, lda, B, ldb, K, e, nslices, rows_per);
+  ABCD_CHECK_LAUNCH();
+  return 0;
+}
+// ABCD_X6R8=0: the four-wave gemm_x6r (same-box A/B)
+static bool x6r8_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("ABCD_X6R8");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 // ---------------------------------------------------------------------------
 // gemm_x6t: gemm_x6f for two K-major operands (element (row, k) at
 // P[k * ld + row]: the weight gradients dW = dG^T X over all packed frames).
@@ -1792,8 +1964,12 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
         // fragment-staged form (one split per workgroup) when both operands fit a buffer resource
         if (K % 8 == 0 && (size_t)M * A.ld * 4 < (1ull << 31) && (size_t)N * B.ld * 4 < (1ull << 31)) {
           // short K: B slice resident, frames streamed (gemm_x6r)
-          if (K <= 160) return gemm_x6r_launch<5, 128, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
-          if (K <= 256) return gemm_x6r_launch<8, 64, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
+          if (K <= 160)
+            return x6r8_enabled() ? gemm_x6r8_launch<5, 128, 2, 8>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
+                                  : gemm_x6r_launch<5, 128, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
+          if (K <= 256)
+            return x6r8_enabled() ? gemm_x6r8_launch<8, 64, 2, 16>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
+                                  : gemm_x6r_launch<8, 64, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
           return gemm_x6f_launch<4, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
         }
         return gemm_x6s_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
