@@ -1017,7 +1017,12 @@ static int gemm_x6r_launch(hipStream_t s, int M, int N, int K, const float* A, l
 // in the same registers: as soon as chunk c of a block is split, the next
 // block's chunk c is loaded into the fragment registers it came from.  The
 // epilogue stages HR rows per wave (HR = 8 where 16 rows of the slice width
-// would not fit beside the B planes).
+// would not fit beside the B planes).  MI355X, scripts/gemm_bench.py, same
+// box: input projection 64044 x 2048 x 144 268-279 us against gemm_x6r's
+// 304-311, offset head 64044 x 256 x 256 57-60 against 70-71 (PMC: MFMA busy
+// 51 % at the ~1.7 GHz the chip holds under this load).  Measured slower: the
+// epilogue straight from the accumulators (64-B row segments, no LDS
+// transpose): 342-347 / 69-70 us.
 template <int NC, int BN, int MR, int HR>
 __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restrict__ A, long lda,
                                                         const float* __restrict__ B, long ldb, int K, EpiArgs e,
