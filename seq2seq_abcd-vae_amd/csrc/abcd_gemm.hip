@@ -1023,13 +1023,24 @@ static int gemm_x6r_launch(hipStream_t s, int M, int N, int K, const float* A, l
 // 51 % at the ~1.7 GHz the chip holds under this load).  Measured slower: the
 // epilogue straight from the accumulators (64-B row segments, no LDS
 // transpose): 342-347 / 69-70 us.
-template <int NC, int BN, int MR, int HR>
+// MODE 1 / 2: the offset head's forward / backward (abcd_internal.h,
+// gemm_offset_fwd / gemm_offset_bwd; BN = 64)
+struct OffArgs {
+  const float* w2;        // K (mode 2) / N (mode 1) floats
+  float* part;            // mode 1: partial logits [M][nslices]
+  const float* dlog_raw;  // mode 2
+  const float* s;         // mode 2: device scalar
+  float* dZo;             // mode 2: M x K, ld = lda
+  float* dlog_s;          // mode 2
+};
+template <int NC, int BN, int MR, int HR, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restrict__ A, long lda,
                                                         const float* __restrict__ B, long ldb, int K, EpiArgs e,
-                                                        int nslices, int rows_per) {
+                                                        int nslices, int rows_per, OffArgs oa) {
   extern __shared__ __attribute__((aligned(16))) f4 rsm[];
   constexpr int NR = BN / 16, SP = BN + 4, NW = 8, NPP = HR * BN / 256;
   static_assert(HR == 8 || HR == 16, "staging rows");
+  static_assert(MODE == 0 || BN == 64, "offset-head modes: 64-column slices");
   const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int per = gridDim.x >> 3;  // grid = 8 * per
@@ -1053,8 +1064,21 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
     }
   }
   float* stg = reinterpret_cast<float*>(rsm + NR * NC * 3 * 64) + w * HR * SP;
-  __syncthreads();
   const int r0 = part * rows_per, r1 = std::min(M, r0 + rows_per);
+  // mode 2: w2 (zero past K) and the row range's s dlog_raw, after the staging tiles
+  float* w2s = reinterpret_cast<float*>(rsm + NR * NC * 3 * 64) + NW * HR * SP;
+  float* dls = w2s + 32 * NC;
+  if constexpr (MODE == 2) {
+    const float sc = *oa.s;
+    for (int k = threadIdx.x; k < 32 * NC; k += 64 * NW) w2s[k] = k < K ? oa.w2[k] : 0.f;
+    for (int x = threadIdx.x; x < rows_per; x += 64 * NW) {
+      const int row = r0 + x;
+      const float dl = row < r1 ? sc * oa.dlog_raw[row] : 0.f;
+      dls[x] = dl;
+      if (slice == 0 && row < r1) oa.dlog_s[row] = dl;
+    }
+  }
+  __syncthreads();
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(A, (uint32_t)((size_t)M * lda * 4));
   // the lane's A fragments of chunk c of the block at row b: rows b + 16 i + r, k = 32 c + 8 q + 0..7
   auto aload = [&](int b, int c, f4 (&v)[MR][NC][2]) {
@@ -1068,10 +1092,14 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
   };
   constexpr int RB = 16 * MR;
   const int ec = n0 + 4 * (lane % (BN / 4));
-  f4 bq = f4zero();
+  f4 bq = f4zero(), w2q = f4zero();
   if (e.bias) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) bq[t] = ec + t < N ? e.bias[ec + t] : 0.f;
+  }
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) w2q[t] = ec + t < N ? oa.w2[ec + t] : 0.f;
   }
   f4 va[MR][NC][2];
   int b = r0 + w * RB;
@@ -1095,6 +1123,26 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       bf8 as[MR][3];
+      if constexpr (MODE == 2) {  // Zo -> dZo = s dlog (1 - Zo^2) w2; this slice stores chunks c = slice mod nslices
+        const int kk = 32 * c + 8 * q;
+        const f4 wl = *reinterpret_cast<const f4*>(w2s + kk), wh = *reinterpret_cast<const f4*>(w2s + kk + 4);
+#pragma unroll
+        for (int i = 0; i < MR; ++i) {
+          const int rl = b + 16 * i + r - r0;
+          const float dl = dls[rl < rows_per ? rl : 0];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const float z0 = va[i][c][0][t], z1 = va[i][c][1][t];
+            va[i][c][0][t] = dl * wl[t] * (1.f - z0 * z0);
+            va[i][c][1][t] = dl * wh[t] * (1.f - z1 * z1);
+          }
+          if (c % nslices == slice && b + 16 * i + r < r1 && kk < K) {
+            float* d = oa.dZo + (long)(b + 16 * i + r) * lda + kk;
+            *reinterpret_cast<f4*>(d) = va[i][c][0];
+            *reinterpret_cast<f4*>(d + 4) = va[i][c][1];
+          }
+        }
+      }
 #pragma unroll
       for (int i = 0; i < MR; ++i) split8(va[i][c][0], va[i][c][1], as[i][0], as[i][1], as[i][2]);
       // the rolling look-ahead, unconditional: a conditional load makes the
@@ -1134,6 +1182,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
           const int lr = (lane + 64 * pp) / (BN / 4), col = ec;
           const int row = b + 16 * i + HR * h + lr;
           f4 val = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * (lane % (BN / 4)));
+          float pl = 0.f;  // mode 1: this quad's share of the row's logit
           if (row < r1 && col < N) {
             float* d = e.C + (long)row * e.ldc + col;
             val = val * e.alpha + bq;
@@ -1146,11 +1195,19 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
 #pragma unroll
               for (int t = 0; t < 4; ++t) val[t] = tanhf(val[t]);
             }
+            if constexpr (MODE == 1) pl = val[0] * w2q[0] + val[1] * w2q[1] + val[2] * w2q[2] + val[3] * w2q[3];
             if (col + 4 <= N) *reinterpret_cast<f4*>(d) = val;
             else
 #pragma unroll
               for (int t = 0; t < 4; ++t)
                 if (col + t < N) d[t] = val[t];
+          }
+          if constexpr (MODE == 1) {  // the 16 quads of a row: lanes 16 k .. 16 k + 15, fixed order
+            pl += __shfl_xor(pl, 1, 64);
+            pl += __shfl_xor(pl, 2, 64);
+            pl += __shfl_xor(pl, 4, 64);
+            pl += __shfl_xor(pl, 8, 64);
+            if ((lane & 15) == 0 && row < r1) oa.part[(long)row * nslices + slice] = pl;
           }
         }
       }
@@ -1158,22 +1215,30 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
   }
 }
 
-template <int NC, int BN, int MR, int HR>
+template <int NC, int BN, int MR>
+struct X6r8Grid {
+  int nslices, grid, rows_per;
+  X6r8Grid(int M, int N) {
+    nslices = cdiv(N, BN);
+    const int step = 8 / std::gcd(nslices, 8);  // as gemm_x6r_launch, one workgroup per CU
+    const int nparts = std::max(step, (256 / nslices) / step * step);
+    grid = nslices * nparts;
+    rows_per = ((cdiv(M, nparts) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
+  }
+};
+template <int NC, int BN, int MR, int HR, int MODE = 0>
 static int gemm_x6r8_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
-                            EpiArgs e) {
-  const int nslices = cdiv(N, BN);
-  const int step = 8 / std::gcd(nslices, 8);  // as gemm_x6r_launch, one workgroup per CU
-  const int nparts = std::max(step, (256 / nslices) / step * step);
-  const int grid = nslices * nparts;
-  const int rows_per = ((cdiv(M, nparts) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
-  const size_t lds = (size_t)(BN / 16) * NC * 3 * 64 * 16 + (size_t)8 * HR * (BN + 4) * 4;
+                            EpiArgs e, OffArgs oa = OffArgs{}) {
+  const X6r8Grid<NC, BN, MR> gr(M, N);
+  size_t lds = (size_t)(BN / 16) * NC * 3 * 64 * 16 + (size_t)8 * HR * (BN + 4) * 4;
+  if (MODE == 2) lds += (size_t)(32 * NC + gr.rows_per) * 4;
   static bool attr = false;
   if (!attr) {
-    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_x6r8_kernel<NC, BN, MR, HR>,
+    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_x6r8_kernel<NC, BN, MR, HR, MODE>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  gemm_x6r8_kernel<NC, BN, MR, HR><<<grid, 512, lds, s>>>(A, lda, B, ldb, K, e, nslices, rows_per);
+  gemm_x6r8_kernel<NC, BN, MR, HR, MODE><<<gr.grid, 512, lds, s>>>(A, lda, B, ldb, K, e, gr.nslices, gr.rows_per, oa);
   ABCD_CHECK_LAUNCH();
   return 0;
 }
@@ -1184,6 +1249,55 @@ static bool x6r8_enabled() {
     return !(v && v[0] == '0');
   }();
   return on;
+}
+
+// the offset head's GEMMs (abcd_internal.h); ABCD_OFFSET_FUSED=0 keeps the
+// separate head kernels (same-box A/B)
+static bool offset_fused_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("ABCD_OFFSET_FUSED");
+    return !(v && v[0] == '0');
+  }();
+  return on && x6r8_enabled();
+}
+static bool offset_fused_ok(int M, int N, int K, long lda, const void* A, const void* B, long ldb) {
+  return offset_fused_enabled() && M > 0 && N > 0 && K > 0 && K <= 256 && K % 8 == 0 && lda % 4 == 0 &&
+         ldb % 4 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 &&
+         (size_t)M * lda * 4 < (1ull << 31) && (size_t)N * ldb * 4 < (1ull << 31);
+}
+int offset_head_slices(int N) { return cdiv(N, 64); }
+int gemm_offset_fwd(hipStream_t s, int M, int N, int K, const float* Hs, long ldh, const float* W1o,
+                    const float* b1o, float* Zo, const float* w2, float* part, bool* done) {
+  *done = false;
+  if (!offset_fused_ok(M, N, K, ldh, Hs, W1o, K) || (N % 4) != 0 || ((uintptr_t)Zo % 16) != 0) return 0;
+  EpiArgs e{Zo, N, M, N, 1.f, 0.f, b1o, ACT_TANH, nullptr};
+  OffArgs oa{};
+  oa.w2 = w2;
+  oa.part = part;
+  ABCD_TRY((hipError_t)(gemm_x6r8_launch<8, 64, 2, 16, 1>(s, M, N, K, Hs, ldh, W1o, K, e, oa)));
+  *done = true;
+  return 0;
+}
+int gemm_offset_bwd(hipStream_t s, int M, int N, int K, const float* Zo, const float* W1oT, float* DHO,
+                    const float* w2, const float* dlog_raw, const float* s_off, float* dZo, float* dlog_s,
+                    bool* done) {
+  *done = false;
+  if (!offset_fused_ok(M, N, K, K, Zo, W1oT, K) || (N % 4) != 0 || ((uintptr_t)DHO % 16) != 0 ||
+      ((uintptr_t)dZo % 16) != 0)
+    return 0;
+  const X6r8Grid<8, 64, 2> gr(M, N);
+  const size_t lds = (size_t)4 * 8 * 3 * 64 * 16 + (size_t)8 * 16 * 68 * 4 + (size_t)(256 + gr.rows_per) * 4;
+  if (lds > 160 * 1024) return 0;
+  EpiArgs e{DHO, N, M, N, 1.f, 0.f, nullptr, ACT_NONE, nullptr};
+  OffArgs oa{};
+  oa.w2 = w2;
+  oa.dlog_raw = dlog_raw;
+  oa.s = s_off;
+  oa.dZo = dZo;
+  oa.dlog_s = dlog_s;
+  ABCD_TRY((hipError_t)(gemm_x6r8_launch<8, 64, 2, 16, 2>(s, M, N, K, Zo, K, W1oT, K, e, oa)));
+  *done = true;
+  return 0;
 }
 
 // ---------------------------------------------------------------------------

@@ -52,6 +52,22 @@ int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n);
 int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, long ldc, float alpha,
          float beta, const float* bias, int act, float* scratch, size_t scratch_floats);
 
+// The decoder's offset head (model.py:121-122,191,195) folded into its two
+// frame-parallel GEMMs (gemm_x6r8, 64-column slices):
+//   forward:  Zo = tanh(Hs W1o^T + b1o) (M x N, K = H) and part[m * nsl + slice]
+//             = the slice's share of Zo . w2 (nsl = offset_head_slices(N));
+//   backward: DHO = dZo W1o with dZo = s dlog_raw (1 - Zo^2) w2 formed from Zo
+//             while its fragments load (M x N, K = Hm); dZo (ld = K) and
+//             dlog_s = s dlog_raw are stored on the way.
+// Both return 0 with *done = false where the fused form does not apply (the
+// caller then runs the separate kernels).
+int offset_head_slices(int N);
+int gemm_offset_fwd(hipStream_t s, int M, int N, int K, const float* Hs, long ldh, const float* W1o,
+                    const float* b1o, float* Zo, const float* w2, float* part, bool* done);
+int gemm_offset_bwd(hipStream_t s, int M, int N, int K, const float* Zo, const float* W1oT, float* DHO,
+                    const float* w2, const float* dlog_raw, const float* s_off, float* dZo, float* dlog_s,
+                    bool* done);
+
 // A B^T (both K-contiguous) as raw split-K slabs slab[z][m*N + n], z < *zout.
 int gemm_slabs(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* slab, size_t slab_floats, int* zout);
 

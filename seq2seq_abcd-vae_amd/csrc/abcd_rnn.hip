@@ -859,6 +859,22 @@ __global__ void dec_offset_head(const float* Zo, int L, int Hm, const float* w2,
     }
   }
 }
+// the same from the fused forward GEMM's per-slice partial dot products
+// (gemm_offset_fwd), summed in slice order
+__global__ void dec_offset_logit(const float* part, int nsl, int L, const float* b2, const float* tgt, float* logit,
+                                 float* dlog_raw, float* bce) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= L) return;
+  float s = 0.f;
+  for (int k = 0; k < nsl; ++k) s += part[(long)row * nsl + k];
+  const float x = s + b2[0];
+  logit[row] = x;
+  if (tgt) {
+    const float y = tgt[row];
+    bce[row] = fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
+    dlog_raw[row] = 1.f / (1.f + __expf(-x)) - y;
+  }
+}
 // emission NLL partial sums: 0.5*(log 2pi + lv + (y-mu)^2 e^{-lv}) over L x F
 __global__ void dec_emission_nll(const float* MU, const float* LV, int Fp, const float* Y, int F, long L,
                                  double* part) {
@@ -956,6 +972,7 @@ struct DecWS {
   float *WihTp, *WhhT, *W2mT, *W2lT, *W1catT, *W1oT, *Wf2hT;
   // forward stash
   float *FS, *Hinit, *Xin, *Hprev, *Cprev, *Gst, *Cst, *Hs, *Aact, *MU, *LV, *OUT, *Zo, *offlog, *dlog_raw, *bce;
+  float* offpart;  // the fused offset head's partial logits (L x offset_head_slices(Hm))
   float* EPS;  // the Philox decoder noise, rows x F (philox_normal_fill)
   float* dWb;  // [dW_ih | db] of the cell (bias column folded into the GEMM)
   double* part;
@@ -998,6 +1015,7 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
   w.MU = A.f((size_t)L * Fp); w.LV = A.f((size_t)L * Fp); w.OUT = A.f((size_t)L * Fp);
   w.EPS = A.f((size_t)L * F);
   w.Zo = A.f((size_t)L * Hm); w.offlog = A.f(L); w.dlog_raw = A.f(L); w.bce = A.f(L);
+  w.offpart = A.f((size_t)L * offset_head_slices(Hm));
   w.part = A.d(2048);
   w.dGX = A.f((size_t)L * GH);
   w.dGH = G == 4 ? w.dGX : A.f((size_t)L * GH);
@@ -1251,11 +1269,20 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
     sum_partials<<<1, 256, 0, sl>>>(w.part, nbk, losses);
     ABCD_CHECK_LAUNCH();
   }
-  // ---- offset head over all frames (off the recurrent critical path) ----
-  ABCD_TRY((hipError_t)gemm(s, L, Hm, H, opKC(w.Hs, H, L), opKC(p->offset.w1, H, Hm), w.Zo, Hm, 1.f, 0.f,
-                            p->offset.b1, ACT_TANH, w.scratch, w.scratch_floats));
-  dec_offset_head<<<cdiv(L, 4), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, p->offset.b2, gt_offset, w.offlog,
-                                             w.dlog_raw, w.bce);
+  // ---- offset head over all frames (off the recurrent critical path): the
+  // logit's dot product folded into the Zo GEMM's epilogue where it applies ----
+  bool fused = false;
+  ABCD_TRY((hipError_t)gemm_offset_fwd(s, L, Hm, H, w.Hs, H, p->offset.w1, p->offset.b1, w.Zo, p->offset.w2,
+                                       w.offpart, &fused));
+  if (fused) {
+    dec_offset_logit<<<cdiv(L, 256), 256, 0, s>>>(w.offpart, offset_head_slices(Hm), L, p->offset.b2, gt_offset,
+                                                  w.offlog, w.dlog_raw, w.bce);
+  } else {
+    ABCD_TRY((hipError_t)gemm(s, L, Hm, H, opKC(w.Hs, H, L), opKC(p->offset.w1, H, Hm), w.Zo, Hm, 1.f, 0.f,
+                              p->offset.b1, ACT_TANH, w.scratch, w.scratch_floats));
+    dec_offset_head<<<cdiv(L, 4), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, p->offset.b2, gt_offset, w.offlog,
+                                               w.dlog_raw, w.bce);
+  }
   ABCD_CHECK_LAUNCH();
   if (losses && gt_offset) {
     ABCD_TRY((hipError_t)stream_fork(s, sl, 5));  // bce
@@ -1324,12 +1351,18 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
   // (the transposed weights of the backward GEMMs were packed by the forward
   // pass, in its one pack launch: the backward reads the forward's stashes
   // from the same workspace anyway)
-  // ---- offset head backward (batched over all frames) ----
-  dec_offset_bwd<<<launch_grid((long)L * Hm), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, w.dlog_raw, d_off, w.dZo,
-                                                           w.dlog_s);
-  ABCD_CHECK_LAUNCH();
-  ABCD_TRY((hipError_t)gemm(s, L, H, Hm, opKC(w.dZo, Hm, L), opKC(w.W1oT, Hm, H), w.DHO, H, 1.f, 0.f, nullptr,
-                            ACT_NONE, sc, scf));
+  // ---- offset head backward (batched over all frames): dZo formed from Zo
+  // inside the DHO GEMM where it applies ----
+  bool fused = false;
+  ABCD_TRY((hipError_t)gemm_offset_bwd(s, L, H, Hm, w.Zo, w.W1oT, w.DHO, p->offset.w2, w.dlog_raw, d_off, w.dZo,
+                                       w.dlog_s, &fused));
+  if (!fused) {
+    dec_offset_bwd<<<launch_grid((long)L * Hm), 256, 0, s>>>(w.Zo, L, Hm, p->offset.w2, w.dlog_raw, d_off, w.dZo,
+                                                             w.dlog_s);
+    ABCD_CHECK_LAUNCH();
+    ABCD_TRY((hipError_t)gemm(s, L, H, Hm, opKC(w.dZo, Hm, L), opKC(w.W1oT, Hm, H), w.DHO, H, 1.f, 0.f, nullptr,
+                              ACT_NONE, sc, scf));
+  }
   // ---- BPTT: one persistent launch, or three launches per step ----
   bool done = false;
   {
