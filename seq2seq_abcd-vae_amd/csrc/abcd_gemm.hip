@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float* __restrict
                                  e.slab ? (long)e.N : e.ldc, e.slab != nullptr);
 }
 
-// gemm_tn_batch: gemm_tn's LDS-staged tile (64 x 64, fp32 MFMA) over the
+// gemm_tn_batch: gemm_tn's LDS-staged tile (32 x 32, fp32 MFMA) over the
 // whole K for every tile of every job of the batch, one launch (the sampler's and the decoder
 // initial state's weight gradients: four GEMMs, each 8-128 tiles at K = 512 /
 // 1024, were four split-K launches + four slab reductions).  The job table
@@ -442,9 +442,20 @@ __global__ __launch_bounds__(256) void gemm_tn_batch_kernel(GemmBatchArgs b) {
   gemm_tn_tile<MR, NR, false, false, BK>(smab, J.A, J.lda, J.B, J.ldb, 0, J.K, (t / tn) * 32 * MR, (t % tn) * 32 * NR,
                                          e, J.C, J.ldc, false);
 }
+// 32 x 32 tiles on a quiet chip: four times the workgroups at the same K
+// depth (the sampler's parameter gradients, 88 -> 352 workgroups; same-box
+// A/B at c2: step 8.51 / 8.52 -> 8.47 / 8.48 ms); ABCD_TNB=2: the 64 x 64 form
+static int tnb_tile() {
+  static const int t = [] {
+    const char* v = getenv("ABCD_TNB");
+    return (v && v[0] == '2') ? 64 : 32;
+  }();
+  return t;
+}
 int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
   if (n <= 0) return 0;
   if (n > GEMM_BATCH_MAX) return (int)hipErrorInvalidValue;
+  const int tb = tl_side ? 64 : tnb_tile();
   GemmBatchArgs b{};
   int tiles = 0, k = 0;
   for (int i = 0; i < n; ++i) {
@@ -455,7 +466,7 @@ int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
       return ABCD_EINVAL;
     b.j[k] = jobs[i];
     b.tile0[k] = tiles;
-    tiles += cdiv(jobs[i].M, 64) * cdiv(jobs[i].N, 64);
+    tiles += cdiv(jobs[i].M, tb) * cdiv(jobs[i].N, tb);
     ++k;
   }
   b.n = k;
@@ -464,6 +475,7 @@ int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
   // 64-deep LDS slabs (70 KB) on a quiet chip; 16-deep ones (17 KB) beside a
   // persistent kernel (side mode), whose LDS image leaves ~40 KB per CU
   if (tl_side) gemm_tn_batch_kernel<2, 2, 16><<<tiles, 256, 0, s>>>(b);
+  else if (tb == 32) gemm_tn_batch_kernel<1, 1, 64><<<tiles, 256, 0, s>>>(b);
   else gemm_tn_batch_kernel<2, 2, 64><<<tiles, 256, 0, s>>>(b);
   ABCD_CHECK_LAUNCH();
   return 0;
