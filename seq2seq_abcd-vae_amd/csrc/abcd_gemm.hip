@@ -2395,6 +2395,8 @@ __global__ void pack_many_kernel(PackList pl) {
         const long o = j.trans ? (long)c * j.lds + r : (long)r * j.lds + c;
         v[k] = j.src[o];
         if (j.src2) v[k] += j.src2[o];
+      } else if (j.ones && r < j.sr && c == j.sc) {
+        v[k] = 1.f;
       }
     }
     float* d = j.dst + (long)r * j.ldd + c0;
@@ -2408,11 +2410,11 @@ __global__ void pack_many_kernel(PackList pl) {
   }
 }
 int Packs::add(const float* src, long lds, int sr, int sc, bool trans, float* dst, long ldd, int dr, int dc,
-               const float* src2) {
+               const float* src2, bool ones) {
   if ((long)dr * dc <= 0) return 0;
   if ((long)dr * (dc + 3) >= (1L << 31)) return ABCD_EINVAL;  // the kernel's 32-bit indices
   if (pl.n == ABCD_PACK_MAX) ABCD_TRY((hipError_t)flush());
-  pl.j[pl.n++] = PackJob{src, src2, lds, dst, ldd, sr, sc, dr, dc, trans ? 1 : 0};
+  pl.j[pl.n++] = PackJob{src, src2, lds, dst, ldd, sr, sc, dr, dc, trans ? 1 : 0, ones ? 1 : 0};
   maxn = std::max(maxn, (long)dr * ((dc + 3) / 4));
   return 0;
 }

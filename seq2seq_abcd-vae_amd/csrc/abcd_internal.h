@@ -98,14 +98,15 @@ int add_vec(hipStream_t s, const float* a, const float* b, float* y, int n);
 int mul_vec(hipStream_t s, const float* a, const float* b, float* y, long n);
 
 // A queue of pack2d jobs (optionally dst = src + src2, same layout) issued as
-// one launch by flush() -- or earlier, when the queue is full.
+// one launch by flush() -- or earlier, when the queue is full.  ones: column sc
+// of rows < sr is 1 instead of 0 (the encoder's [X | 1] frame copy).
 constexpr int ABCD_PACK_MAX = 24;
 struct PackJob {
   const float *src, *src2;
   long lds;
   float* dst;
   long ldd;
-  int sr, sc, dr, dc, trans;
+  int sr, sc, dr, dc, trans, ones;
 };
 struct PackList {
   PackJob j[ABCD_PACK_MAX];
@@ -117,7 +118,7 @@ struct Packs {
   long maxn;
   explicit Packs(hipStream_t st) : s(st), pl{}, maxn(0) {}
   int add(const float* src, long lds, int sr, int sc, bool trans, float* dst, long ldd, int dr, int dc,
-          const float* src2 = nullptr);
+          const float* src2 = nullptr, bool ones = false);
   int flush();
 };
 

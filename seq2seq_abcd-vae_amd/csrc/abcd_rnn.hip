@@ -277,8 +277,9 @@ static int bwd_tn(int H) { return (H / 16) % 4 == 0 ? 64 : ((H / 16) % 2 == 0 ? 
 // ENCODER
 // ===========================================================================
 // Bias gradients folded into the input weight-gradient GEMM (layer 0 with a
-// padded input, Fp > F): column F of the padded frame copy Xp is set to 1 after
-// the forward has used it, so the GEMM dG^T [X | 1] of width F + 1 yields
+// padded input, Fp > F): column F of the padded frame copy Xp is 1 (written by
+// the forward's pack; W_ih's packed pad columns are 0, so the input projection
+// is unchanged), so the GEMM dG^T [X | 1] of width F + 1 yields
 // dW_ih and, in its last column, sum_r dG[r] = the bias gradient -- one
 // colsum pass over the L x G*H gate gradients fewer per direction.
 __global__ __launch_bounds__(256) void set_col_kernel(float* X, long ld, long rows, int col, float v) {
@@ -405,7 +406,9 @@ extern "C" int abcd_encoder_forward_dropout(const abcd_encoder_cfg* c, const abc
   const std::vector<int> off = step_offsets(x->batch_sizes, T);
   const int64_t* bs = x->batch_sizes;
   Packs pk(s);
-  ABCD_TRY((hipError_t)pk.add(x->data, F, L, F, false, w.Xp, Fp, L, Fp));
+  // [X | 1 | 0]: the ones column (F < Fp) feeds the backward's bias-gradient
+  // column and meets W_ih's zero padding in the input projection
+  ABCD_TRY((hipError_t)pk.add(x->data, F, L, F, false, w.Xp, Fp, L, Fp, nullptr, F < Fp));
   for (int l = 0; l < c->layers; ++l) {
     const int In = l == 0 ? F : D * H, Inp = l == 0 ? Fp : D * H;
     for (int d = 0; d < D; ++d) {
@@ -629,10 +632,7 @@ extern "C" int abcd_encoder_backward_dropout(const abcd_encoder_cfg* c, const ab
       if (gr.b_hh) ABCD_TRY((hipError_t)colsum(st, dGH, GH, K, GH, nullptr, gr.b_hh, beta, scratch, scf));
       return 0;
     };
-    if (ones_col) {
-      set_col_kernel<<<std::max(1, std::min(1024, cdiv(L, 256))), 256, 0, s>>>(w.Xp, Fp, L, F, 1.f);
-      ABCD_CHECK_LAUNCH();
-    }
+    // (the ones column of Xp was written by the forward's pack)
     int wg2 = -1;  // 0: gemm_wg2 produced every gradient of this layer
     if (ones_col && G == 4) {
       WgDir dirs[2] = {};
