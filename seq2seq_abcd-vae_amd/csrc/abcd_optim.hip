@@ -11,8 +11,14 @@
 
 namespace abcd {
 
-__global__ void sq_pass1(const float* g, long n, double* part) {
+// global norm in one launch: each block's partial sum of squares (fp64) is
+// stored write-through and the last block to finish (last_workgroup) sums
+// them in a fixed order (thread-strided, shuffle tree, waves): deterministic.
+// state[0] = norm, state[1] = clip coefficient
+__device__ unsigned g_norm_ticket;
+__global__ void sq_norm(const float* g, long n, double* part, float max_norm, float* state, float* out_norm) {
   __shared__ double sh[16];
+  __shared__ int last;
   double v = 0.0;
   const long n4 = n / 4;
   const f4* g4 = reinterpret_cast<const f4*>(g);
@@ -28,24 +34,21 @@ __global__ void sq_pass1(const float* g, long n, double* part) {
   if (threadIdx.x == 0) {
     double t = 0;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
-    part[blockIdx.x] = t;
+    st_agent(&part[blockIdx.x], t);
   }
-}
-// state[0] = norm, state[1] = clip coefficient
-__global__ void norm_pass2(const double* part, int np, float max_norm, float* state, float* out_norm) {
-  __shared__ double sh[16];
-  double v = 0.0;
-  for (int i = threadIdx.x; i < np; i += blockDim.x) v += part[i];
+  if (!last_workgroup(&g_norm_ticket, &last)) return;
+  v = 0.0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) v += ld_agent(&part[i]);
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  __syncthreads();
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
     const float norm = (float)sqrt(t);
-    const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);
     state[0] = norm;
-    state[1] = coef;
+    state[1] = fminf(max_norm / (norm + 1e-6f), 1.0f);
     if (out_norm) *out_norm = norm;
   }
 }
@@ -89,9 +92,7 @@ extern "C" int abcd_grad_norm(const float* g, long n, float* out_norm, void* ws,
   hipStream_t s = (hipStream_t)stream;
   double* part = (double*)ws;
   float* state = (float*)(part + kNormBlocks);
-  sq_pass1<<<kNormBlocks, 256, 0, s>>>(g, n, part);
-  ABCD_CHECK_LAUNCH();
-  norm_pass2<<<1, 256, 0, s>>>(part, kNormBlocks, 1.f, state, out_norm);
+  sq_norm<<<kNormBlocks, 256, 0, s>>>(g, n, part, 1.f, state, out_norm);
   ABCD_CHECK_LAUNCH();
   return 0;
 }
@@ -104,9 +105,7 @@ extern "C" int abcd_clip_sgd(float* p, float* g, float* momentum_buf, long n, fl
   hipStream_t s = (hipStream_t)stream;
   double* part = (double*)ws;
   float* state = (float*)(part + kNormBlocks);
-  sq_pass1<<<kNormBlocks, 256, 0, s>>>(g, n, part);
-  ABCD_CHECK_LAUNCH();
-  norm_pass2<<<1, 256, 0, s>>>(part, kNormBlocks, max_norm, state, out_norm);
+  sq_norm<<<kNormBlocks, 256, 0, s>>>(g, n, part, max_norm, state, out_norm);
   ABCD_CHECK_LAUNCH();
   const int nb = (int)std::min<long>(4096, (n + 255) / 256);
   sgd_update<<<nb, 256, 0, s>>>(p, g, momentum != 0.f ? momentum_buf : nullptr, n, state, lr, momentum,

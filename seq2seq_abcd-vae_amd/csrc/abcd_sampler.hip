@@ -428,29 +428,6 @@ DEV float tile_colsum(f4 v) {
   c += __shfl_xor(c, 32, 64);
   return c;
 }
-// true in every thread of the last workgroup to call it.  The hand-over is
-// write-through (MI355X_MICROARCH.md visibility table, R1): every partial the
-// last workgroup reads was stored by st_agent (sc1) and drained by its wave
-// (vmcnt(0)) before the barrier and the relaxed ticket add, and is read back
-// with ld_agent (sc1) -- no L2 write-back / invalidate (__threadfence: ~3.5
-// us per call, twice on the last workgroup's path)
-DEV bool last_workgroup(unsigned* ticket, int* flag_sh) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned n = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = n == gridDim.x - 1;
-    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag_sh = last;
-  }
-  __syncthreads();
-  return *flag_sh != 0;
-}
-template <class T>
-DEV T ld_agent(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-template <class T>
-DEV void st_agent(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
 constexpr int HEAD_MAX_SLABS = 8;  // split-K slabs the forward head sums (gemm_slabs' cap)
 
 struct HeadFwdArgs {
