@@ -80,7 +80,10 @@ __global__ void fill_normal_kernel(float* out, long n, uint64_t seed, uint64_t o
 
 using namespace abcd;
 
+// partial slots; sq_norm runs kSqBlocks of them (its hand-over ticket is one
+// word: ~12 ns per serialized add, so 1024 blocks cost ~12 us, 256 ~3 us)
 static const int kNormBlocks = 1024;
+static const int kSqBlocks = 256;
 
 extern "C" size_t abcd_optim_workspace_bytes(long n) {
   (void)n;
@@ -92,7 +95,7 @@ extern "C" int abcd_grad_norm(const float* g, long n, float* out_norm, void* ws,
   hipStream_t s = (hipStream_t)stream;
   double* part = (double*)ws;
   float* state = (float*)(part + kNormBlocks);
-  sq_norm<<<kNormBlocks, 256, 0, s>>>(g, n, part, 1.f, state, out_norm);
+  sq_norm<<<kSqBlocks, 256, 0, s>>>(g, n, part, 1.f, state, out_norm);
   ABCD_CHECK_LAUNCH();
   return 0;
 }
@@ -105,7 +108,7 @@ extern "C" int abcd_clip_sgd(float* p, float* g, float* momentum_buf, long n, fl
   hipStream_t s = (hipStream_t)stream;
   double* part = (double*)ws;
   float* state = (float*)(part + kNormBlocks);
-  sq_norm<<<kNormBlocks, 256, 0, s>>>(g, n, part, max_norm, state, out_norm);
+  sq_norm<<<kSqBlocks, 256, 0, s>>>(g, n, part, max_norm, state, out_norm);
   ABCD_CHECK_LAUNCH();
   const int nb = (int)std::min<long>(4096, (n + 255) / 256);
   sgd_update<<<nb, 256, 0, s>>>(p, g, momentum != 0.f ? momentum_buf : nullptr, n, state, lr, momentum,
