@@ -446,11 +446,8 @@ __global__ __launch_bounds__(256) void gemm_tn_batch_kernel(GemmBatchArgs b) {
 // depth (the sampler's parameter gradients, 88 -> 352 workgroups; same-box
 // A/B at c2: step 8.51 / 8.52 -> 8.47 / 8.48 ms); ABCD_TNB=2: the 64 x 64 form
 static int tnb_tile() {
-  static const int t = [] {
-    const char* v = getenv("ABCD_TNB");
-    return (v && v[0] == '2') ? 64 : 32;
-  }();
-  return t;
+  const char* v = getenv("ABCD_TNB");
+  return (v && v[0] == '2') ? 64 : 32;
 }
 int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
   if (n <= 0) return 0;
@@ -1254,23 +1251,18 @@ static int gemm_x6r8_launch(hipStream_t s, int M, int N, int K, const float* A, 
   ABCD_CHECK_LAUNCH();
   return 0;
 }
-// ABCD_X6R8=0: the four-wave gemm_x6r (same-box A/B)
+// ABCD_X6R8=0: the four-wave gemm_x6r (same-box A/B; read per call, as the
+// other form switches, so one test process covers both forms)
 static bool x6r8_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("ABCD_X6R8");
-    return !(v && v[0] == '0');
-  }();
-  return on;
+  const char* v = getenv("ABCD_X6R8");
+  return !(v && v[0] == '0');
 }
 
 // the offset head's GEMMs (abcd_internal.h); ABCD_OFFSET_FUSED=0 keeps the
 // separate head kernels (same-box A/B)
 static bool offset_fused_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("ABCD_OFFSET_FUSED");
-    return !(v && v[0] == '0');
-  }();
-  return on && x6r8_enabled();
+  const char* v = getenv("ABCD_OFFSET_FUSED");
+  return !(v && v[0] == '0') && x6r8_enabled();
 }
 static bool offset_fused_ok(int M, int N, int K, long lda, const void* A, const void* B, long ldb) {
   return offset_fused_enabled() && M > 0 && N > 0 && K > 0 && K <= 256 && K % 8 == 0 && lda % 4 == 0 &&

@@ -30,6 +30,14 @@ def test_gemm_nt_vs_torch(M, N, K):
     assert err <= 1e-5 * K ** 0.5 * 4 + 1e-5, err
 
 
+@pytest.mark.parametrize("M,N,K", [(64044, 2048, 144), (9000, 300, 136), (30001, 384, 256)])
+def test_gemm_nt_x6r_four_wave_form(M, N, K, monkeypatch):
+    """ABCD_X6R8=0: the four-wave gemm_x6r that gemm_x6r8 replaced, at the
+    frame-streaming shapes of test_gemm_nt_vs_torch."""
+    monkeypatch.setenv("ABCD_X6R8", "0")
+    test_gemm_nt_vs_torch(M, N, K)
+
+
 @pytest.mark.parametrize("wg", ["3", "2"])
 @pytest.mark.parametrize("nd,F,H,K", [(2, 129, 256, 65583), (1, 129, 256, 3001), (2, 130, 256, 777), (2, 33, 48, 500),
                                        (1, 20, 24, 64), (2, 129, 256, 31), (1, 143, 256, 100003)])

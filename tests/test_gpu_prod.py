@@ -92,6 +92,17 @@ def test_fused_step_prod_vs_reference(name):
         assert abs(float(delta.sum()) - ref_s) <= GRAD_TOL * ref_n * delta.numel() ** 0.5 + 1e-9, k
 
 
+@pytest.mark.parametrize("env", ["ABCD_OFFSET_FUSED=0", "ABCD_X6R8=0", "ABCD_TNB=2"])
+def test_fused_step_prod_replaced_forms(env, monkeypatch):
+    """The forms round 5's defaults replaced, still selected by switch (and,
+    for the offset head, by shapes the fused GEMM modes do not take): the
+    separate offset-head kernels beside plain GEMMs, the four-wave gemm_x6r,
+    64 x 64 gemm_tn_batch tiles -- the same reference checks as the default."""
+    k, v = env.split("=")
+    monkeypatch.setenv(k, v)
+    test_fused_step_prod_vs_reference("lstm_k128")
+
+
 @pytest.mark.parametrize("name", ["lstm_k128", "gru_k1024_spk", "plain_lstm"])
 def test_module_surface_prod_vs_reference(name):
     """encoder(packed) -> sampler -> sample -> kl -> decoder on the nn.Module
