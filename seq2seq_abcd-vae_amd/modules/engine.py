@@ -223,7 +223,9 @@ class FusedStep:
                                               N.ptr(sc[KL:KL + 1]),
                                               None if self.plain else N.ptr(sc[PPL_CLUSTER:PPL_CLUSTER + 2]),
                                               N.ptr(ws_s), ws_s.numel(), st), "sampler")
-        torch.cuda.current_stream(dev).wait_stream(side)  # the decoder noise
+        if not prior:  # (with the prior, the join in front of the sampler covered the noise:
+            # a second, already-satisfied wait still cost a ~6 us barrier in front of the decoder)
+            torch.cuda.current_stream(dev).wait_stream(side)  # the decoder noise
         spk = None
         if kdec.embed_speaker is not None:
             spk = speakers.to(dev, torch.int64).contiguous()
