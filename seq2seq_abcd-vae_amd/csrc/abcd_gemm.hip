@@ -1042,7 +1042,9 @@ struct OffArgs {
   float* dZo;             // mode 2: M x K, ld = lda
   float* dlog_s;          // mode 2
 };
-template <int NC, int BN, int MR, int HR, int MODE = 0>
+// T16: the last chunk holds at most 16 valid k (K <= 32 (NC - 1) + 16) and
+// runs 16-deep (mma_x6_16): its B planes and A fragments in that layout
+template <int NC, int BN, int MR, int HR, int MODE = 0, bool T16 = false>
 __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restrict__ A, long lda,
                                                         const float* __restrict__ B, long ldb, int K, EpiArgs e,
                                                         int nslices, int rows_per, OffArgs oa) {
@@ -1060,13 +1062,26 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
     const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (size_t)n0 * ldb, (uint32_t)(std::max(0, std::min(BN, N - n0)) * ldb * 4));
     for (int x = threadIdx.x; x < NR * NC * 64; x += 64 * NW) {
       const int j = x / (NC * 64), c = (x / 64) % NC, ln = x & 63;
+      f4* d = rsm + ((j * NC + c) * 3) * 64 + ln;
+      if (T16 && c == NC - 1) {  // k = 32c + 4 (ln >> 4) + 0..3
+        const int row = 16 * j + (ln & 15), kk = 32 * c + 4 * (ln >> 4);
+        const uint32_t o = kk < K ? (uint32_t)(row * ldb + kk) * 4u : 0x80000000u;
+        const f4 v = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, o, 0, 0));
+        s4 h, m, l;
+        split4(v, h, m, l);
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v hh = __builtin_bit_cast(f2v, h), mm = __builtin_bit_cast(f2v, m), ll = __builtin_bit_cast(f2v, l);
+        d[0] = f4{hh[0], hh[1], 0.f, 0.f};
+        d[64] = f4{mm[0], mm[1], 0.f, 0.f};
+        d[128] = f4{ll[0], ll[1], 0.f, 0.f};
+        continue;
+      }
       const int row = 16 * j + (ln & 15), kk = 32 * c + 8 * (ln >> 4);
       const uint32_t o = kk < K ? (uint32_t)(row * ldb + kk) * 4u : 0x80000000u;
       const f4 lo = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, o, 0, 0));
       const f4 hi = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, kk < K ? o + 16u : o, 0, 0));
       bf8 h, m, l;
       split8(lo, hi, h, m, l);
-      f4* d = rsm + ((j * NC + c) * 3) * 64 + ln;
       d[0] = __builtin_bit_cast(f4, h);
       d[64] = __builtin_bit_cast(f4, m);
       d[128] = __builtin_bit_cast(f4, l);
@@ -1091,12 +1106,13 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(A, (uint32_t)((size_t)M * lda * 4));
   // the lane's A fragments of chunk c of the block at row b: rows b + 16 i + r, k = 32 c + 8 q + 0..7
   auto aload = [&](int b, int c, f4 (&v)[MR][NC][2]) {
-    const int kk = 32 * c + 8 * q;
+    const bool t16 = T16 && c == NC - 1;
+    const int kk = 32 * c + (t16 ? 4 : 8) * q;
 #pragma unroll
     for (int i = 0; i < MR; ++i) {
       const uint32_t o = kk < K ? (uint32_t)((b + 16 * i + r) * lda + kk) * 4u : 0x80000000u;
       v[i][c][0] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, o, 0, 0));
-      v[i][c][1] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, kk < K ? o + 16u : o, 0, 0));
+      if (!t16) v[i][c][1] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, kk < K ? o + 16u : o, 0, 0));
     }
   };
   constexpr int RB = 16 * MR;
@@ -1131,6 +1147,26 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
     bread(0, 0, bcur);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
+      if (T16 && c == NC - 1) {  // the 16-deep last chunk (MODE 0 only)
+        s4 at[MR][3];
+#pragma unroll
+        for (int i = 0; i < MR; ++i) split4(va[i][c][0], at[i][0], at[i][1], at[i][2]);
+        aload(bn, c, va);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          f4 bnxt[3];
+          const bool nx = j + 1 < NR;
+          if (nx) bread(c, j + 1, bnxt);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < MR; ++i)
+            acc[i][j] = mma_x6_16(acc[i][j], at[i][0], at[i][1], at[i][2], lo_s4(bcur[0]), lo_s4(bcur[1]), lo_s4(bcur[2]));
+          __builtin_amdgcn_sched_barrier(0);
+          if (nx) bcur[0] = bnxt[0], bcur[1] = bnxt[1], bcur[2] = bnxt[2];
+        }
+        continue;
+      }
       bf8 as[MR][3];
       if constexpr (MODE == 2) {  // Zo -> dZo = s dlog (1 - Zo^2) w2; this slice stores chunks c = slice mod nslices
         const int kk = 32 * c + 8 * q;
@@ -1235,7 +1271,7 @@ struct X6r8Grid {
     rows_per = ((cdiv(M, nparts) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
   }
 };
-template <int NC, int BN, int MR, int HR, int MODE = 0>
+template <int NC, int BN, int MR, int HR, int MODE = 0, bool T16 = false>
 static int gemm_x6r8_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
                             EpiArgs e, OffArgs oa = OffArgs{}) {
   const X6r8Grid<NC, BN, MR> gr(M, N);
@@ -1243,11 +1279,11 @@ static int gemm_x6r8_launch(hipStream_t s, int M, int N, int K, const float* A, 
   if (MODE == 2) lds += (size_t)(32 * NC + gr.rows_per) * 4;
   static bool attr = false;
   if (!attr) {
-    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_x6r8_kernel<NC, BN, MR, HR, MODE>,
+    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_x6r8_kernel<NC, BN, MR, HR, MODE, T16>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  gemm_x6r8_kernel<NC, BN, MR, HR, MODE><<<gr.grid, 512, lds, s>>>(A, lda, B, ldb, K, e, gr.nslices, gr.rows_per, oa);
+  gemm_x6r8_kernel<NC, BN, MR, HR, MODE, T16><<<gr.grid, 512, lds, s>>>(A, lda, B, ldb, K, e, gr.nslices, gr.rows_per, oa);
   ABCD_CHECK_LAUNCH();
   return 0;
 }
@@ -1255,6 +1291,12 @@ static int gemm_x6r8_launch(hipStream_t s, int M, int N, int K, const float* A, 
 // other form switches, so one test process covers both forms)
 static bool x6r8_enabled() {
   const char* v = getenv("ABCD_X6R8");
+  return !(v && v[0] == '0');
+}
+
+// ABCD_X6R8_T16=0: the K in (128, 144] last chunk zero-padded to 32-deep
+static bool x6r8_t16() {
+  const char* v = getenv("ABCD_X6R8_T16");
   return !(v && v[0] == '0');
 }
 
@@ -2088,8 +2130,10 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
         if (K % 8 == 0 && (size_t)M * A.ld * 4 < (1ull << 31) && (size_t)N * B.ld * 4 < (1ull << 31)) {
           // short K: B slice resident, frames streamed (gemm_x6r)
           if (K <= 160)
-            return x6r8_enabled() ? gemm_x6r8_launch<5, 128, 2, 8>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
-                                  : gemm_x6r_launch<5, 128, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
+            return !x6r8_enabled() ? gemm_x6r_launch<5, 128, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
+                   : (K > 128 && K <= 144 && x6r8_t16())
+                       ? gemm_x6r8_launch<5, 128, 2, 8, 0, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
+                       : gemm_x6r8_launch<5, 128, 2, 8>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
           if (K <= 256)
             return x6r8_enabled() ? gemm_x6r8_launch<8, 64, 2, 16>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
                                   : gemm_x6r_launch<8, 64, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);

@@ -63,6 +63,44 @@ DEV void split8(const f4& x0, const f4& x1, bf8& h, bf8& m, bf8& l) {
   l = __builtin_bit_cast(bf8, L);
 }
 
+// 16-deep form for a last chunk with at most 16 valid k (the K = 144 input
+// projection's fifth chunk): v_mfma_f32_16x16x16_bf16, lane l supplies
+// A[row l&15][k = 4(l>>4) + 0..3] and B[k = 4(l>>4) + 0..3][col l&15]
+// (same accumulator layout), half the cycles of a zero-padded 32-deep slice
+typedef short s4 __attribute__((ext_vector_type(4)));
+DEV void split4(const f4& x, s4& h, s4& m, s4& l) {
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  u2 H, M, L;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const float a = x[2 * e], b = x[2 * e + 1];
+    const uint32_t hp = cvt_pk(a, b);
+    const float ra = a - lo_f(hp), rb = b - hi_f(hp);
+    const uint32_t mp = cvt_pk(ra, rb);
+    H[e] = hp;
+    M[e] = mp;
+    L[e] = cvt_pk(ra - lo_f(mp), rb - hi_f(mp));
+  }
+  h = __builtin_bit_cast(s4, H);
+  m = __builtin_bit_cast(s4, M);
+  l = __builtin_bit_cast(s4, L);
+}
+DEV f4 mfma_bf16k(const s4& a, const s4& b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0); }
+DEV f4 mma_x6_16(f4 acc, const s4& a0, const s4& a1, const s4& a2, const s4& b0, const s4& b1, const s4& b2) {
+  acc = mfma_bf16k(a2, b0, acc);
+  acc = mfma_bf16k(a1, b1, acc);
+  acc = mfma_bf16k(a0, b2, acc);
+  acc = mfma_bf16k(a1, b0, acc);
+  acc = mfma_bf16k(a0, b1, acc);
+  acc = mfma_bf16k(a0, b0, acc);
+  return acc;
+}
+// the low 8 bytes of an LDS slot as a bf16x4 fragment
+DEV s4 lo_s4(const f4& v) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(s4, f2v{v[0], v[1]});
+}
+
 // acc += a * b over one 32-deep slice, six-term split product
 DEV f4 mma_x6(f4 acc, const bf8& a0, const bf8& a1, const bf8& a2, const bf8& b0, const bf8& b1, const bf8& b2) {
   acc = mfma_bf(a2, b0, acc);

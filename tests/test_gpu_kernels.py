@@ -38,6 +38,14 @@ def test_gemm_nt_x6r_four_wave_form(M, N, K, monkeypatch):
     test_gemm_nt_vs_torch(M, N, K)
 
 
+@pytest.mark.parametrize("M,N,K", [(64044, 2048, 144), (8001, 520, 144)])
+def test_gemm_nt_x6r8_padded_tail(M, N, K, monkeypatch):
+    """ABCD_X6R8_T16=0: gemm_x6r8 with the K = 144 last chunk zero-padded to
+    32-deep instead of the default 16-deep MFMAs."""
+    monkeypatch.setenv("ABCD_X6R8_T16", "0")
+    test_gemm_nt_vs_torch(M, N, K)
+
+
 @pytest.mark.parametrize("wg", ["3", "2"])
 @pytest.mark.parametrize("nd,F,H,K", [(2, 129, 256, 65583), (1, 129, 256, 3001), (2, 130, 256, 777), (2, 33, 48, 500),
                                        (1, 20, 24, 64), (2, 129, 256, 31), (1, 143, 256, 100003)])
