@@ -29,7 +29,7 @@ SIMDS = 1024
 NAMES = (("abcd::enc_fwd_persist", "enc_fwd"), ("abcd::enc_bwd_sk", "enc_bwd"), ("abcd::enc_bwd_w8", "enc_bwd"), ("abcd::enc_bwd_persist", "enc_bwd"),
          ("abcd::dec_fwd_x6", "dec_fwd"), ("abcd::dec_fwd_persist", "dec_fwd"), ("abcd::dec_bwd_fold", "dec_bwd"),
          ("abcd::dec_bwd_sk", "dec_bwd"), ("abcd::dec_bwd_persist", "dec_bwd"), ("abcd::dec_bwd_w16", "dec_bwd"), ("gemm_wg2_kernel", "gemm_wg2"), ("gemm_wg3b_kernel", "gemm_wg3b"),
-         ("gemm_x6r_kernel", "gemm_x6r"), ("gemm_x6r8_kernel<5", "gemm_x6r8 (input projection)"), ("gemm_x6r8_kernel<8, 64, 2, 16, 1>", "gemm_x6r8 (offset head fwd)"), ("gemm_x6r8_kernel<8, 64, 2, 16, 2>", "gemm_x6r8 (offset head bwd)"), ("samp_head_fwd", "samp_head_fwd"), ("samp_head_bwd", "samp_head_bwd"),
+         ("gemm_x6r_kernel", "gemm_x6r"), ("gemm_x6r8_kernel<5", "gemm_x6r8 (input projection)"), ("gemm_x6r8_kernel<8, 64, 2, 16, 1", "gemm_x6r8 (offset head fwd)"), ("gemm_x6r8_kernel<8, 64, 2, 16, 2", "gemm_x6r8 (offset head bwd)"), ("samp_head_fwd", "samp_head_fwd"), ("samp_head_bwd", "samp_head_bwd"),
          ("gemm_tn_kernel", "gemm_tn"), ("gemm_x6s_kernel", "gemm_x6s"), ("gemm_x6t_kernel", "gemm_x6t"),
          ("gemm_tn_batch_kernel", "gemm_tn_batch"), ("colsum_batch_pass1", "colsum_batch"),
          ("slab_reduce_kernel", "slab_reduce"))

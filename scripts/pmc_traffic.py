@@ -22,7 +22,7 @@ from collections import defaultdict
 ROLES = {"enc_fwd": ("enc_fwd_persist",), "enc_bwd": ("enc_bwd_persist", "enc_bwd_sk", "enc_bwd_w8"),
          "dec_fwd": ("dec_fwd_persist", "dec_fwd_x6"), "dec_bwd": ("dec_bwd_persist", "dec_bwd_sk", "dec_bwd_fold", "dec_bwd_w16")}
 # the step's other large kernels (algorithmic bytes: DESIGN.md s3 "Other kernels")
-OTHERS = {"gemm_wg3b": ("gemm_wg3b_kernel",), "gemm_x6r": ("gemm_x6r_kernel",), "gemm_x6r8 (input projection)": ("gemm_x6r8_kernel<5",), "gemm_x6r8 (offset head fwd)": ("gemm_x6r8_kernel<8, 64, 2, 16, 1>",), "gemm_x6r8 (offset head bwd)": ("gemm_x6r8_kernel<8, 64, 2, 16, 2>",), "gemm_tn": ("gemm_tn_kernel",), "gemm_x6s": ("gemm_x6s_kernel",), "gemm_x6t": ("gemm_x6t_kernel",),
+OTHERS = {"gemm_wg3b": ("gemm_wg3b_kernel",), "gemm_x6r": ("gemm_x6r_kernel",), "gemm_x6r8 (input projection)": ("gemm_x6r8_kernel<5",), "gemm_x6r8 (offset head fwd)": ("gemm_x6r8_kernel<8, 64, 2, 16, 1",), "gemm_x6r8 (offset head bwd)": ("gemm_x6r8_kernel<8, 64, 2, 16, 2",), "gemm_tn": ("gemm_tn_kernel",), "gemm_x6s": ("gemm_x6s_kernel",), "gemm_x6t": ("gemm_x6t_kernel",),
           "gemm_tn_batch": ("gemm_tn_batch_kernel",), "colsum_batch": ("colsum_batch_pass1",),
           "slab_reduce": ("slab_reduce_kernel",)}
 KERNELS = tuple(ROLES) + tuple(OTHERS)
