@@ -404,12 +404,14 @@ def load_traffic(kernel, cfg_name):
     """HBM bytes per launch of `kernel` from the rocprofv3 PMC passes committed
     under profiles/ (scripts/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, the
     gfx950 correction of MI355X_MICROARCH.md) for this configuration, or None
-    (no PMC pass of this configuration is committed)."""
-    path = os.path.join(REPO, "profiles", "traffic.json")
+    (no PMC pass of this configuration is committed).  One file per
+    configuration: profiles/traffic_<config>.json (copied from the round's
+    profiles/rNN/ set)."""
+    path = os.path.join(REPO, "profiles", f"traffic_{cfg_name}.json")
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("config", "c2") != cfg_name:
+        if t.get("config") != cfg_name:
             return None
         e = t["kernels"][kernel]
         return int(e["hbm_bytes_per_launch"])
@@ -420,12 +422,13 @@ def load_traffic(kernel, cfg_name):
 def load_mfma(kernel, cfg_name):
     """MFMA utilisation of `kernel` from the rocprofv3 PMC pass committed under
     profiles/ (scripts/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x
-    GRBM_GUI_ACTIVE / 8), or None."""
-    path = os.path.join(REPO, "profiles", "pmc_mfma.json")
+    GRBM_GUI_ACTIVE / 8) for this configuration
+    (profiles/pmc_mfma_<config>.json), or None."""
+    path = os.path.join(REPO, "profiles", f"pmc_mfma_{cfg_name}.json")
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("config", "c2") != cfg_name:
+        if t.get("config") != cfg_name:
             return None
         return float(t["kernels"][kernel]["mfma_busy"])
     except (OSError, KeyError, ValueError):
@@ -485,8 +488,9 @@ def kernel_roofline(step, batches, cfg, run, cfg_name):
             # traffic and mfma_busy are read from rocprofv3 PMC passes committed
             # under profiles/ (PMC counters cannot run inside the timed bench)
             "provenance": {"achieved": "live: HIP events on the launch stream, this run",
-                           "traffic": "committed profile: profiles/traffic.json" if traffic is not None else None,
-                           "mfma_busy": "committed profile: profiles/pmc_mfma.json"
+                           "traffic": f"committed profile: profiles/traffic_{cfg_name}.json"
+                           if traffic is not None else None,
+                           "mfma_busy": f"committed profile: profiles/pmc_mfma_{cfg_name}.json"
                            if load_mfma(dom, cfg_name) is not None else None},
             "all_kernels": per}
 

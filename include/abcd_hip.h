@@ -216,7 +216,9 @@ int abcd_sampler_backward_split(const abcd_sampler_cfg* cfg, const abcd_sampler_
 /* the deferred codebook / W2 / W1 gradients of a preceding
  * abcd_sampler_backward_split(..., ABCD_DEFER_PARAMS) on `stream`: one
  * batched launch (dC = [d_feats; U]^T [Y; dL / sqrt(D)], dW2 = dU^T Z1,
- * dW1 = dZ1^T h); returns 0 without work when that call took another path.
+ * dW1 = dZ1^T h); returns 0 without work when that call took another path
+ * (the split call records per workspace whether it deferred; a params call
+ * without a matching deferral does nothing).
  * wgrad_stream (NULL or == stream: on `stream`): the launch goes there behind
  * an event on `stream`, in a tiling that co-resides with the encoder's
  * persistent BPTT (the training step queues it on its side stream behind the
@@ -351,6 +353,10 @@ int abcd_featurize_packed(const float* wave, const long long* seg_off, const lon
  * (learning.py:161-163, 256) over one flat fp32 parameter/gradient buffer.
  * ---------------------------------------------------------------------- */
 size_t abcd_optim_workspace_bytes(long n);
+/* The norm's last-block hand-over uses one device-wide ticket word (as do the
+ * sampler-head kernels of abcd_sampler_forward_fused / abcd_sampler_backward*):
+ * launches of these entry points on one device must not run concurrently on
+ * different streams (the training step queues them on one stream). */
 /* total 2-norm of g (device scalar) */
 int abcd_grad_norm(const float* g, long n, float* out_norm, void* ws, size_t ws_bytes, void* stream);
 /* g *= min(1, max_norm / (||g|| + 1e-6)); buf = momentum*buf + g (buf = g if
@@ -415,14 +421,17 @@ void abcd_dispatch_reset(void);
  * (dev_out holds 2 * blocks u32; the placement the persistent kernels' group
  * roles rely on).  Returns 0 / a HIP error. */
 void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask);
-/* Side-stream gate (process-wide switch, default off): the weight-gradient
+/* Side-stream gate (per calling host thread, default off): the weight-gradient
  * work abcd_decoder_backward_overlap queues on its wgrad_stream first waits,
  * on the device and bounded (tens of ms, then it proceeds), until the NEXT
- * encoder BPTT launch of this process has every workgroup resident -- for a
- * caller that queues abcd_encoder_backward* right after the decoder and
- * sampler backward, as the training step does.  Without it the side GEMMs can
- * take a CU's room before a BPTT member is placed there.  Read when that
- * call is made (the training step sets it around its decoder backward). */
+ * encoder backward of this process on that device has started: a persistent
+ * BPTT once every workgroup is resident, or a per-step encoder backward (grid
+ * past the resident capacity, other shapes) as soon as it is queued (it
+ * releases the gate itself) -- for a caller that queues
+ * abcd_encoder_backward* right after the decoder and sampler backward, as the
+ * training step does.  Without it the side GEMMs can take a CU's room before
+ * a BPTT member is placed there.  Read when that call is made, on the thread
+ * that makes it (the training step sets it around its decoder backward). */
 void abcd_side_gate_enable(int on);
 int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream);
 /* 0 if no persistent recurrent kernel has timed out waiting for its group

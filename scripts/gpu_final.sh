@@ -23,7 +23,7 @@ if [ "$PART" = "1" ]; then
   echo "part 1 done"
 else
   # PMC: HBM traffic (FETCH_SIZE / WRITE_SIZE, separate passes) and MFMA utilisation, per config
-  for c in c2 c5 c5gru; do
+  for c in c2 c4 c5 c5gru; do
     timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing > /dev/null 2> $OUT/pmc_fetch_$c.err
     timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$c -o run -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing > /dev/null 2> $OUT/pmc_write_$c.err
     python scripts/pmc_traffic.py $OUT/pmc_fetch_$c $OUT/pmc_write_$c $OUT/traffic_$c.json $c > /dev/null

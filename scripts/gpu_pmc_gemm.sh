@@ -3,7 +3,6 @@ O=gpurun_out/pmcg
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $O/p1 -o run -- python3 scripts/gemm_bench.py > $O/p1.log 2>&1
-ABCD_X6R8=0 timeout -s KILL 60 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $O/p1old -o run -- python3 scripts/gemm_bench.py > $O/p1old.log 2>&1
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/p3 -o run -- python3 scripts/gemm_bench.py > $O/p3.log 2>&1
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/p4 -o run -- python3 scripts/gemm_bench.py > $O/p4.log 2>&1
 timeout -s KILL 60 rocprofv3 -L > $O/avail.txt 2>&1 || true

@@ -3,7 +3,7 @@
 
     rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU \\
         SQ_WAVE_CYCLES --output-format csv -d gpurun_out/pmc_mfma -o run -- python3 bench.py ...
-    python scripts/pmc_mfma.py gpurun_out/pmc_mfma profiles/pmc_mfma.json [c2]
+    python scripts/pmc_mfma.py gpurun_out/pmc_mfma profiles/pmc_mfma_c2.json c2
 
 Per kernel (mean per dispatch):
   wall_cycles = GRBM_GUI_ACTIVE / 8  (rocprofv3 sums the counter over the 8 XCDs;

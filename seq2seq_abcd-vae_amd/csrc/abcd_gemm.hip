@@ -443,16 +443,12 @@ __global__ __launch_bounds__(256) void gemm_tn_batch_kernel(GemmBatchArgs b) {
                                          e, J.C, J.ldc, false);
 }
 // 32 x 32 tiles on a quiet chip: four times the workgroups at the same K
-// depth (the sampler's parameter gradients, 88 -> 352 workgroups; same-box
-// A/B at c2: step 8.51 / 8.52 -> 8.47 / 8.48 ms); ABCD_TNB=2: the 64 x 64 form
-static int tnb_tile() {
-  const char* v = getenv("ABCD_TNB");
-  return (v && v[0] == '2') ? 64 : 32;
-}
+// depth as 64 x 64 (the sampler's parameter gradients, 88 -> 352 workgroups;
+// same-box A/B at c2: step 8.51 / 8.52 -> 8.47 / 8.48 ms)
 int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
   if (n <= 0) return 0;
   if (n > GEMM_BATCH_MAX) return (int)hipErrorInvalidValue;
-  const int tb = tl_side ? 64 : tnb_tile();
+  const int tb = tl_side ? 64 : 32;
   GemmBatchArgs b{};
   int tiles = 0, k = 0;
   for (int i = 0; i < n; ++i) {
@@ -472,8 +468,7 @@ int gemm_tn_batch(hipStream_t s, const GemmJob* jobs, int n) {
   // 64-deep LDS slabs (70 KB) on a quiet chip; 16-deep ones (17 KB) beside a
   // persistent kernel (side mode), whose LDS image leaves ~40 KB per CU
   if (tl_side) gemm_tn_batch_kernel<2, 2, 16><<<tiles, 256, 0, s>>>(b);
-  else if (tb == 32) gemm_tn_batch_kernel<1, 1, 64><<<tiles, 256, 0, s>>>(b);
-  else gemm_tn_batch_kernel<2, 2, 64><<<tiles, 256, 0, s>>>(b);
+  else gemm_tn_batch_kernel<1, 1, 64><<<tiles, 256, 0, s>>>(b);
   ABCD_CHECK_LAUNCH();
   return 0;
 }
@@ -829,209 +824,32 @@ static int gemm_x6f_launch(hipStream_t s, int M, int N, int K, const float* A, l
 }
 
 // ---------------------------------------------------------------------------
-// gemm_x6r: frame-streaming split-fp32 GEMM for short K (K <= 32 NC) and
+// gemm_x6r8: frame-streaming split-fp32 GEMM for short K (K <= 32 NC) and
 // K-contiguous operands: C[M x N] = A B^T with M = packed frames (~65k) and
-// N = a few hundred to 2048 weight rows.  gemm_x6f re-stages and re-splits
-// the B tile for every 128 x 128 output tile and pays a load -> split ->
-// barrier round per 32-deep chunk -- at K = 144 a workgroup does 5 such
-// rounds and its epilogue, so the launch ran at ~80 TF/s.  Here a workgroup
-// owns one BN-column slice of B for the whole launch (split ONCE into the
-// three bf16 planes in fragment order, resident in LDS) and streams a
-// contiguous range of frames: each wave takes 16 MR rows at a time, loads
-// the A fragments straight into registers (the next block's loads in
-// flight during this block's MFMAs), splits each chunk once and issues
-// 6 MR NR MFMAs per chunk.  Epilogue: wave-private LDS transpose, whole
-// 16-B row stores.  Workgroups of one XCD (blockIdx % 8) take the slices of
-// the same frame ranges, so A rows are fetched from HBM once per XCD L2.
-// Measured (scripts/gemm_bench.py, MI355X): input projection 64044 x 2048 x
-// 144 302 us against gemm_x6f's 450 us (273 vs 458 us inside the c2 step),
-// offset head 64044 x 256 x 256 71 vs 82 us.  Where the rest goes (same
-// script, stores or MFMAs removed): 320 us -> 237 without the stores, 198
-// without the MFMAs, 136 without either -- one wave per SIMD serialises the
-// B-plane LDS reads, the splits, the epilogue transposes and the MFMAs.
-// Tried and slower: a three-slot register ring (blocks two ahead, 391 us),
-// MR = 4 (scratch), BN = 64 at two workgroups per CU (294-311 us, more A
-// re-reads), MR = 1 (306-339 us); MR = 3 (round 4: 48-row blocks, 196 AGPRs
-// as spill room): input projection 292 us either way, offset head 82 vs 71.
-// ---------------------------------------------------------------------------
-template <int NC, int BN, int MR, int OCC>
-__global__ __launch_bounds__(256, OCC) void gemm_x6r_kernel(const float* __restrict__ A, long lda,
-                                                       const float* __restrict__ B, long ldb, int K, EpiArgs e,
-                                                       int nslices, int rows_per) {
-  extern __shared__ __attribute__((aligned(16))) f4 rsm[];
-  constexpr int NR = BN / 16, SP = BN + 4;
-  const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int per = gridDim.x >> 3;  // grid = 8 * per
-  const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  const int slice = lin % nslices, part = lin / nslices;
-  const int n0 = slice * BN, M = e.M, N = e.N;
-  // B slice -> LDS planes [j][c][plane][lane]; rows >= N and k >= K read 0 (K % 8 == 0)
-  {
-    const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (size_t)n0 * ldb, (uint32_t)(std::max(0, std::min(BN, N - n0)) * ldb * 4));
-    for (int x = threadIdx.x; x < NR * NC * 64; x += 256) {
-      const int j = x / (NC * 64), c = (x / 64) % NC, ln = x & 63;
-      const int row = 16 * j + (ln & 15), kk = 32 * c + 8 * (ln >> 4);
-      const uint32_t o = kk < K ? (uint32_t)(row * ldb + kk) * 4u : 0x80000000u;
-      const f4 lo = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, o, 0, 0));
-      const f4 hi = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, kk < K ? o + 16u : o, 0, 0));
-      bf8 h, m, l;
-      split8(lo, hi, h, m, l);
-      f4* d = rsm + ((j * NC + c) * 3) * 64 + ln;
-      d[0] = __builtin_bit_cast(f4, h);
-      d[64] = __builtin_bit_cast(f4, m);
-      d[128] = __builtin_bit_cast(f4, l);
-    }
-  }
-  float* stg = reinterpret_cast<float*>(rsm + NR * NC * 3 * 64) + w * 16 * SP;
-  __syncthreads();
-  const int r0 = part * rows_per, r1 = std::min(M, r0 + rows_per);
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A, (uint32_t)((size_t)M * lda * 4));
-  // the lane's A fragments of the block at row b: rows b + 16 i + r, k = 32 c + 8 q + 0..7
-  auto aload = [&](int b, f4 (&v)[MR][NC][2]) {
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int kk = 32 * c + 8 * q;
-        const uint32_t o = kk < K ? (uint32_t)((b + 16 * i + r) * lda + kk) * 4u : 0x80000000u;
-        v[i][c][0] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, o, 0, 0));
-        v[i][c][1] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, kk < K ? o + 16u : o, 0, 0));
-      }
-  };
-  constexpr int RB = 16 * MR;
-  // epilogue columns of this lane: the same 4 for every row it stores (bias preloaded)
-  const int ec = n0 + 4 * (lane % (BN / 4));
-  f4 bq = f4zero();
-  if (e.bias) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) bq[t] = ec + t < N ? e.bias[ec + t] : 0.f;
-  }
-  f4 va[MR][NC][2];
-  int b = r0 + w * RB;
-  if (b < r1) aload(b, va);
-  for (; b < r1; b += 4 * RB) {
-    // next block's fragments: issued here, unconditionally (rows past M read
-    // 0; a last block's look-ahead into the next range is a wasted read), and
-    // pinned -- the compiler otherwise sinks them to the copy at the end of
-    // the block, exposing the whole load latency once per block
-    f4 vn[MR][NC][2];
-    const bool more = b + 4 * RB < r1;
-    aload(b + 4 * RB, vn);
-    __builtin_amdgcn_sched_barrier(0);
-    f4 acc[MR][NR];
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j) acc[i][j] = f4zero();
-    // B planes of step (c, j) read one step ahead (their LDS latency hides
-    // behind the previous step's 6 MR MFMAs)
-    auto bread = [&](int c, int j, f4 (&bb)[3]) {
-      const f4* bp = rsm + ((j * NC + c) * 3) * 64 + lane;
-      bb[0] = bp[0], bb[1] = bp[64], bb[2] = bp[128];
-    };
-    f4 bcur[3];
-    bread(0, 0, bcur);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      bf8 as[MR][3];
-#pragma unroll
-      for (int i = 0; i < MR; ++i) split8(va[i][c][0], va[i][c][1], as[i][0], as[i][1], as[i][2]);
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        f4 bnxt[3];
-        const bool nx = j + 1 < NR || c + 1 < NC;
-        if (nx) bread(j + 1 < NR ? c : c + 1, j + 1 < NR ? j + 1 : 0, bnxt);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < MR; ++i)
-          acc[i][j] = mma_x6(acc[i][j], as[i][0], as[i][1], as[i][2], __builtin_bit_cast(bf8, bcur[0]),
-                             __builtin_bit_cast(bf8, bcur[1]), __builtin_bit_cast(bf8, bcur[2]));
-        __builtin_amdgcn_sched_barrier(0);
-        if (nx) bcur[0] = bnxt[0], bcur[1] = bnxt[1], bcur[2] = bnxt[2];
-      }
-    }
-    // epilogue: 16 rows x BN per subtile row i through the wave's LDS tile
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) stg[(4 * q + g) * SP + 16 * j + r] = acc[i][j][g];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int pp = 0; pp < NR; ++pp) {  // 16 rows x BN / 4 quads = 64 NR quads per wave
-        const int lr = (lane + 64 * pp) / (BN / 4), col = ec;
-        const int row = b + 16 * i + lr;
-        f4 val = *reinterpret_cast<const f4*>(stg + lr * SP + 4 * (lane % (BN / 4)));
-        if (row < r1 && col < N) {
-          float* d = e.C + (long)row * e.ldc + col;
-          val = val * e.alpha + bq;
-          if (e.beta != 0.f) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-              if (col + t < N) val[t] += e.beta * d[t];
-          }
-          if (e.act == ACT_TANH) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) val[t] = tanhf(val[t]);
-          }
-          if (col + 4 <= N) *reinterpret_cast<f4*>(d) = val;
-          else
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-              if (col + t < N) d[t] = val[t];
-        }
-      }
-    }
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int c = 0; c < NC; ++c) va[i][c][0] = vn[i][c][0], va[i][c][1] = vn[i][c][1];
-    }
-  }
-}
-
-template <int NC, int BN, int MR, int OCC = 1>
-static int gemm_x6r_launch(hipStream_t s, int M, int N, int K, const float* A, long lda, const float* B, long ldb,
-                           EpiArgs e) {
-  const int nslices = cdiv(N, BN);
-  // OCC workgroups per CU: about 256 OCC / nslices frame ranges, their count
-  // a multiple of 8 / gcd(nslices, 8) so that the grid (every (slice, range)
-  // pair exactly once) is a multiple of 8 for the kernel's XCD grouping
-  const int step = 8 / std::gcd(nslices, 8);
-  const int nparts = std::max(step, (256 * OCC / nslices) / step * step);
-  const int grid = nslices * nparts;
-  const int rows_per = ((cdiv(M, nparts) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
-  const size_t lds = (size_t)(BN / 16) * NC * 3 * 64 * 16 + (size_t)4 * 16 * (BN + 4) * 4;
-  static bool attr = false;  // per process (the attribute is per function, not per device)
-  if (!attr) {
-    ABCD_TRY(hipFuncSetAttribute((const void*)gemm_x6r_kernel<NC, BN, MR, OCC>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr = true;
-  }
-  gemm_x6r_kernel<NC, BN, MR, OCC><<<grid, 256, lds, s>>>(A, lda, B, ldb, K, e, nslices, rows_per);
-  ABCD_CHECK_LAUNCH();
-  return 0;
-}
-
-// gemm_x6r8: gemm_x6r with EIGHT waves (two per SIMD) sharing the resident B
-// slice.  With one wave per SIMD every A-load wait, split, B-plane read and
-// epilogue store of gemm_x6r sits between its MFMAs (36 % MFMA busy at the
-// input projection); a second wave issues its MFMAs in those gaps.  The
-// register budget halves (256 per wave), so the look-ahead is a rolling one
-// in the same registers: as soon as chunk c of a block is split, the next
-// block's chunk c is loaded into the fragment registers it came from.  The
-// epilogue stages HR rows per wave (HR = 8 where 16 rows of the slice width
-// would not fit beside the B planes).  MI355X, scripts/gemm_bench.py, same
-// box: input projection 64044 x 2048 x 144 268-279 us against gemm_x6r's
-// 304-311, offset head 64044 x 256 x 256 57-60 against 70-71 (PMC: MFMA busy
-// 51 % at the ~1.7 GHz the chip holds under this load).  Measured slower: the
-// epilogue straight from the accumulators (64-B row segments, no LDS
-// transpose): 342-347 / 69-70 us.
+// N = a few hundred to 2048 weight rows (the encoder's input projection, the
+// offset head).  A workgroup owns one BN-column slice of B for the whole
+// launch (split ONCE into the three bf16 planes in fragment order, resident
+// in LDS) and streams a contiguous range of frames: each wave takes 16 MR
+// rows at a time, loads the A fragments straight into registers, splits each
+// chunk once and issues 6 MR NR MFMAs per chunk; epilogue through a
+// wave-private LDS transpose, whole 16-B row stores.  Workgroups of one XCD
+// (blockIdx % 8) take the slices of the same frame ranges, so A rows are
+// fetched from HBM once per XCD L2.  EIGHT waves (two per SIMD) share the
+// resident slice: with one wave per SIMD (round-4 gemm_x6r, removed in
+// round 6) every A-load wait, split, B-plane read and epilogue store sat
+// between its MFMAs (36 % MFMA busy); the second wave issues its MFMAs in
+// those gaps.  The register budget halves (256 per wave), so the look-ahead
+// is a rolling one in the same registers: as soon as chunk c of a block is
+// split, the next block's chunk c is loaded into the fragment registers it
+// came from.  The epilogue stages HR rows per wave (HR = 8 where 16 rows of
+// the slice width would not fit beside the B planes).  MI355X,
+// scripts/gemm_bench.py, same box: input projection 64044 x 2048 x 144
+// 268-279 us against the four-wave form's 304-311 (gemm_x6f: 450), offset
+// head 64044 x 256 x 256 57-60 against 70-71 (PMC: MFMA busy 51 % at the
+// ~1.7 GHz the chip holds under this load).  Measured slower: the epilogue
+// straight from the accumulators (64-B row segments, no LDS transpose):
+// 342-347 / 69-70 us; a three-slot register ring, MR = 1 / 3 / 4 and 64-column
+// slices at two workgroups per CU (four-wave form, rounds 2-4).
 // MODE 1 / 2: the offset head's forward / backward (abcd_internal.h,
 // gemm_offset_fwd / gemm_offset_bwd; BN = 64)
 struct OffArgs {
@@ -1058,7 +876,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x6r8_kernel(const float* __restri
   const int lin = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
   const int slice = lin % nslices, part = lin / nslices;
   const int n0 = slice * BN, M = e.M, N = e.N;
-  {  // B slice -> LDS planes [j][c][plane][lane] (as gemm_x6r)
+  {  // B slice -> LDS planes [j][c][plane][lane]; rows >= N and k >= K read 0 (K % 8 == 0)
     const __amdgpu_buffer_rsrc_t rb = make_rsrc(B + (size_t)n0 * ldb, (uint32_t)(std::max(0, std::min(BN, N - n0)) * ldb * 4));
     for (int x = threadIdx.x; x < NR * NC * 64; x += 64 * NW) {
       const int j = x / (NC * 64), c = (x / 64) % NC, ln = x & 63;
@@ -1265,7 +1083,10 @@ struct X6r8Grid {
   int nslices, grid, rows_per;
   X6r8Grid(int M, int N) {
     nslices = cdiv(N, BN);
-    const int step = 8 / std::gcd(nslices, 8);  // as gemm_x6r_launch, one workgroup per CU
+    // one workgroup per CU: about 256 / nslices frame ranges, their count a
+    // multiple of 8 / gcd(nslices, 8) so that the grid (every (slice, range)
+    // pair once) is a multiple of 8 for the XCD grouping
+    const int step = 8 / std::gcd(nslices, 8);
     const int nparts = std::max(step, (256 / nslices) / step * step);
     grid = nslices * nparts;
     rows_per = ((cdiv(M, nparts) + 16 * MR - 1) / (16 * MR)) * (16 * MR);
@@ -1287,27 +1108,11 @@ static int gemm_x6r8_launch(hipStream_t s, int M, int N, int K, const float* A, 
   ABCD_CHECK_LAUNCH();
   return 0;
 }
-// ABCD_X6R8=0: the four-wave gemm_x6r (same-box A/B; read per call, as the
-// other form switches, so one test process covers both forms)
-static bool x6r8_enabled() {
-  const char* v = getenv("ABCD_X6R8");
-  return !(v && v[0] == '0');
-}
-
-// ABCD_X6R8_T16=0: the K in (128, 144] last chunk zero-padded to 32-deep
-static bool x6r8_t16() {
-  const char* v = getenv("ABCD_X6R8_T16");
-  return !(v && v[0] == '0');
-}
-
-// the offset head's GEMMs (abcd_internal.h); ABCD_OFFSET_FUSED=0 keeps the
-// separate head kernels (same-box A/B)
-static bool offset_fused_enabled() {
-  const char* v = getenv("ABCD_OFFSET_FUSED");
-  return !(v && v[0] == '0') && x6r8_enabled();
-}
+// the offset head's GEMMs (abcd_internal.h); shapes they do not take
+// (decoder hidden size > 256, unaligned operands) run the separate head
+// kernels dec_offset_head / dec_offset_bwd beside plain GEMMs
 static bool offset_fused_ok(int M, int N, int K, long lda, const void* A, const void* B, long ldb) {
-  return offset_fused_enabled() && M > 0 && N > 0 && K > 0 && K <= 256 && K % 8 == 0 && lda % 4 == 0 &&
+  return M > 0 && N > 0 && K > 0 && K <= 256 && K % 8 == 0 && lda % 4 == 0 &&
          ldb % 4 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 &&
          (size_t)M * lda * 4 < (1ull << 31) && (size_t)N * ldb * 4 < (1ull << 31);
 }
@@ -2076,34 +1881,6 @@ static int gemm_x6s_launch(hipStream_t s, int M, int N, int K, const float* A, l
 }
 
 
-// both operands K-major with 16-B aligned rows covering roundup(M|N, 4).
-// Tile: 128 rows x 32*NR columns covering N up to 256 per tile.
-static int gemm_tn(hipStream_t s, int M, int N, int K, const Operand& A, const Operand& B, EpiArgs e,
-                   float* scratch, size_t scratch_floats) {
-  int nr = std::min(tl_side ? 4 : 8, cdiv(N, 32));
-  // one 160-wide tile for N in (128, 160] (the decoder's dW_ih, N = F = 129)
-  // instead of a second, nearly empty 128-wide one: 38 KB LDS, 142 VGPRs --
-  // still one workgroup per CU beside enc_bwd_sk (98 KB, 258 registers)
-  if (tl_side && N > 128 && N <= 160) nr = 5;
-  // the same along M (the emission MLPs' dW2, M = F = 129): one 160-row tile
-  if (tl_side && nr == 4 && M > 128 && M <= 160)
-    return gemm_tn_launch<5, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
-#define TN_CASE(n) \
-  case n: return gemm_tn_launch<4, n>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
-  switch (nr) {
-    TN_CASE(1) TN_CASE(2) TN_CASE(3) TN_CASE(4) TN_CASE(5) TN_CASE(6) TN_CASE(7)
-    default: return gemm_tn_launch<4, 8>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
-  }
-#undef TN_CASE
-}
-// ABCD_SIDE_X6=0: the side-stream frame reductions on gemm_tn (fp32 MFMA)
-static bool side_x6() {
-  static const bool on = [] {
-    const char* v = getenv("ABCD_SIDE_X6");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
 static bool tn_ok(const Operand& o, int rows) {
   return o.kmajor && o.ld % 4 == 0 && ((uintptr_t)o.p % 16) == 0 && o.ld >= ((rows + 3) & ~3);
 }
@@ -2128,15 +1905,13 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
       if (!tl_side) {
         // fragment-staged form (one split per workgroup) when both operands fit a buffer resource
         if (K % 8 == 0 && (size_t)M * A.ld * 4 < (1ull << 31) && (size_t)N * B.ld * 4 < (1ull << 31)) {
-          // short K: B slice resident, frames streamed (gemm_x6r)
+          // short K: B slice resident, frames streamed (gemm_x6r8)
+          // (K in (128, 144]: the half-empty last chunk on 16-deep MFMAs, T16;
+          // zero-padded to 32-deep it ran 269-282 against 266-267 us)
           if (K <= 160)
-            return !x6r8_enabled() ? gemm_x6r_launch<5, 128, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
-                   : (K > 128 && K <= 144 && x6r8_t16())
-                       ? gemm_x6r8_launch<5, 128, 2, 8, 0, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
-                       : gemm_x6r8_launch<5, 128, 2, 8>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
-          if (K <= 256)
-            return x6r8_enabled() ? gemm_x6r8_launch<8, 64, 2, 16>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
-                                  : gemm_x6r_launch<8, 64, 2>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
+            return (K > 128 && K <= 144) ? gemm_x6r8_launch<5, 128, 2, 8, 0, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e)
+                                         : gemm_x6r8_launch<5, 128, 2, 8>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
+          if (K <= 256) return gemm_x6r8_launch<8, 64, 2, 16>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
           return gemm_x6f_launch<4, 4>(s, M, N, K, A.p, A.ld, B.p, B.ld, e);
         }
         return gemm_x6s_launch<4, 4, true, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, nullptr, 0);
@@ -2166,15 +1941,14 @@ int gemm(hipStream_t s, int M, int N, int K, Operand A, Operand B, float* C, lon
       return gemm_x6s_launch<4, 4, false, false>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
     }
     // beside the encoder BPTT (side mode): split-fp32 on one operand stage
-    // (34 KB, 204 VGPRs: fits beside enc_bwd_w8's 120 KB / 256 registers)
-    if (side_x6()) {
-      if (N > 128 && N <= 160)
-        return gemm_x6s_launch<4, 5, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
-      if (M > 128 && M <= 160)
-        return gemm_x6s_launch<5, 4, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
-      return gemm_x6s_launch<4, 4, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
-    }
-    return gemm_tn(s, M, N, K, A, B, e, scratch, scratch_floats);
+    // (34 KB, 204 VGPRs: fits beside enc_bwd_w8's 120 KB / 256 registers);
+    // the fp32-MFMA gemm_tn tiles it replaced cost the BPTT 0.2 ms of matrix
+    // pipe
+    if (N > 128 && N <= 160)
+      return gemm_x6s_launch<4, 5, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+    if (M > 128 && M <= 160)
+      return gemm_x6s_launch<5, 4, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
+    return gemm_x6s_launch<4, 4, false, false, true>(s, M, N, K, A.p, A.ld, B.p, B.ld, e, scratch, scratch_floats);
   }
   return gemm_launch(s, M, N, K, KM{A.p, A.ld, std::min(A.nrows, M), K}, KM{B.p, B.ld, std::min(B.nrows, N), K},
                      e, scratch, scratch_floats);

@@ -2374,9 +2374,13 @@ static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
 }
 
 // the side-stream gate's bookkeeping: encoder BPTT launches per device (the
-// device counts the same launches once all their workgroups have started)
+// device counts the same launches once all their workgroups have started) and
+// whether a queued gate still waits for one.  The switch is per host thread:
+// the training step turns it on around its own decoder-backward call, so
+// another thread's decoder backward never gets a gate it did not ask for.
 static unsigned h_bptt_launches[64];
-static std::atomic<bool> g_side_gate{false};
+static bool h_gate_pending[64];
+static thread_local bool g_side_gate = false;
 static int cur_dev() {
   int dev = 0;
   return hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 ? dev : 0;
@@ -2385,18 +2389,37 @@ static int cur_dev() {
 // by the reset in front of it) and the host launch count
 static void bptt_launch(PBwdArgs& b, int ngroups) {
   b.started = b.sync + (size_t)2 * ngroups * PERSIST_SYNC_STRIDE;
-  ++h_bptt_launches[cur_dev()];
+  const int dev = cur_dev();
+  ++h_bptt_launches[dev];
+  h_gate_pending[dev] = false;
+}
+// an encoder backward that did NOT launch a persistent BPTT (the per-step
+// kernels: grid past the resident capacity, an unsupported shape, or
+// ABCD_PERSIST=0) releases a pending gate itself: one single-lane kernel on
+// the BPTT's stream bumps the epoch, so the side work behind the gate starts
+// when the encoder backward starts instead of after the gate's spin bound
+__global__ void bptt_release_kernel() {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&g_bptt_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static int bptt_release(hipStream_t s) {
+  const int dev = cur_dev();
+  if (!h_gate_pending[dev]) return 0;
+  bptt_release_kernel<<<1, 64, 0, s>>>();
+  ABCD_TRY(hipGetLastError());
+  ++h_bptt_launches[dev];
+  h_gate_pending[dev] = false;
+  return 0;
 }
 // ABCD_SIDE_GATE=0 keeps it off whatever the switch says (same-box A/B)
 bool side_gate_enabled() {
-  static const bool env_off = [] {
-    const char* v = getenv("ABCD_SIDE_GATE");
-    return v && v[0] == '0';
-  }();
-  return g_side_gate.load() && !env_off && persist_enabled();  // (no persistent BPTT: nothing to wait for)
+  const char* v = getenv("ABCD_SIDE_GATE");  // read per call (tests flip it in-process)
+  const bool env_off = v && v[0] == '0';
+  return g_side_gate && !env_off && persist_enabled();  // (no persistent BPTT: nothing to wait for)
 }
 int side_gate(hipStream_t sw) {
-  side_gate_kernel<<<1, 64, 0, sw>>>(h_bptt_launches[cur_dev()] + 1);
+  const int dev = cur_dev();
+  side_gate_kernel<<<1, 64, 0, sw>>>(h_bptt_launches[dev] + 1);
+  h_gate_pending[dev] = true;
   return (int)hipGetLastError();
 }
 
@@ -2520,8 +2543,14 @@ static int launch_bwd_w8(hipStream_t s, const PBwdArgs& a, bool* launched) {
   return 0;
 }
 
+static int persist_encoder_bwd_k(hipStream_t s, int G, const PBwdArgs& a, bool* launched);
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
   *launched = false;
+  const int rc = persist_encoder_bwd_k(s, G, a, launched);
+  if (rc || *launched) return rc;
+  return bptt_release(s);
+}
+static int persist_encoder_bwd_k(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
   if (!persist_enabled()) return 0;
   if (a.part && a.H == 256) {
     const int rc = G == 4 ? launch_bwd_w8<4>(s, a, launched) : launch_bwd_w8<3>(s, a, launched);
@@ -2718,7 +2747,7 @@ extern "C" int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream) {
 
 // diagnostics (abcd_hip.h: abcd_debug_persist_prof): stamp buffer for the
 // persistent kernels selected by mask, grid x T x 8 u64, or null to disable
-extern "C" void abcd_side_gate_enable(int on) { abcd::g_side_gate.store(on != 0); }
+extern "C" void abcd_side_gate_enable(int on) { abcd::g_side_gate = on != 0; }
 
 extern "C" void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask) {
   abcd::g_prof = dev_buf;

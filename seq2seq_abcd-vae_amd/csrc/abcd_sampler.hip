@@ -10,6 +10,7 @@
 #include "abcd_internal.h"
 
 #include <mutex>
+#include <vector>
 
 namespace abcd {
 
@@ -157,9 +158,16 @@ DEV void prior_block(const float* psl, int K, int Kv, double N, float a0, float*
   __syncthreads();
 }
 
-// standalone form (abcd_sampler_kl): alpha / elog land in the global stash
+// standalone form (abcd_sampler_kl, abcd_sampler_prior): alpha / elog land in
+// the global stash.  The training step queues it on the side stream while the
+// input projection holds every CU; at issue priority 0 its fp64 chains shared
+// the SIMDs with the GEMM's waves and ran ~210 us (11 us alone), ending just
+// before the encoder's persistent launch -- on a slower box it would hold a CU
+// one of that launch's members needs.  At priority 3 its waves win the issue
+// arbitration over the GEMM's, so it finishes early in the projection.
 __global__ void kl_prior(const float* psl, int K, int Kv, double N, float a0, float* p_out, float* alpha_out,
                          float* elog_out, float* tri_out, double* kl_small) {
+  __builtin_amdgcn_s_setprio(3);
   __shared__ double sh[16];
   prior_block(psl, K, Kv, N, a0, alpha_out, elog_out, sh, true, p_out, alpha_out, elog_out, tri_out, kl_small);
 }
@@ -1425,6 +1433,32 @@ extern "C" int abcd_sampler_forward_backward(const abcd_sampler_cfg* c, const ab
   return samp_fwd_bwd(c, p, h, B, d_logits, d_h, g, accumulate_codebook, w, s, s);
 }
 
+// Which workspaces hold a deferred parameter-gradient job: set by a split
+// call that actually deferred (fused ABCD path), consumed by
+// abcd_sampler_backward_params, which does nothing for a workspace without one
+// (the split call then took the unfused path and wrote those gradients itself;
+// the products backward_params multiplies were never filled).
+static std::mutex g_defer_mu;
+static std::vector<const void*> g_deferred;
+static void defer_mark(const void* ws, bool on) {
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  for (size_t i = 0; i < g_deferred.size(); ++i)
+    if (g_deferred[i] == ws) {
+      if (!on) g_deferred.erase(g_deferred.begin() + (long)i);
+      return;
+    }
+  if (on) g_deferred.push_back(ws);
+}
+static bool defer_take(const void* ws) {
+  std::lock_guard<std::mutex> lk(g_defer_mu);
+  for (size_t i = 0; i < g_deferred.size(); ++i)
+    if (g_deferred[i] == ws) {
+      g_deferred.erase(g_deferred.begin() + (long)i);
+      return true;
+    }
+  return false;
+}
+
 // fused: sample + kl + forward backward in one call (the training step).
 // wgrad_stream (may be NULL or == stream): where the parameter gradients go;
 // the caller joins it before reading them.
@@ -1436,8 +1470,9 @@ extern "C" int abcd_sampler_backward_split(const abcd_sampler_cfg* c, const abcd
   SampWS w;
   ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
   hipStream_t s = (hipStream_t)stream;
-  const bool defer = wgrad_stream == ABCD_DEFER_PARAMS;
-  if (defer && !samp_fused_ok(c, d_feats, d_kl)) wgrad_stream = nullptr;  // only the fused path defers
+  bool defer = wgrad_stream == ABCD_DEFER_PARAMS;
+  if (defer && !samp_fused_ok(c, d_feats, d_kl)) wgrad_stream = nullptr, defer = false;  // only the fused path defers
+  defer_mark(ws, defer);
   hipStream_t sw = wgrad_stream ? (hipStream_t)wgrad_stream : s;
   if (!defer) ABCD_TRY((hipError_t)stream_fork(s, sw, 0));  // d_feats and the forward products
   const int D = c->feature_dim, K = c->num_categories;
@@ -1475,9 +1510,7 @@ extern "C" int abcd_sampler_backward_params(const abcd_sampler_cfg* c, const abc
                                             int B, const abcd_sampler_grads* g, void* ws, size_t ws_bytes,
                                             void* stream, void* wgrad_stream) {
   ABCD_REQUIRE(samp_check(c) == 0 && p && h && g && ws && B > 0 && wgrad_stream != ABCD_DEFER_PARAMS);
-  if (c->plain || c->num_categories > 1024 ||
-      head_bwd_lds(c->mlp_hidden, c->feature_dim, c->num_categories) > HEAD_LDS_MAX)
-    return 0;  // the split call ran the unfused path, parameter gradients included
+  if (!defer_take(ws)) return 0;  // the split call ran the unfused path, parameter gradients included
   SampWS w;
   ABCD_REQUIRE(samp_ws(c, B, ws, ws_bytes, &w) == 0);
   hipStream_t s = (hipStream_t)stream;

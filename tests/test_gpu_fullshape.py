@@ -130,3 +130,51 @@ def test_full_shape_step_vs_oracle(name, B, seed):
         dr = new[k].double() - P[k].double()
         tol = GRAD_TOL * float(dr.abs().max()) + 2 * 2.0 ** -23 * float(P[k].abs().max())
         assert float((dh - dr).abs().max()) <= tol, (k, float((dh - dr).abs().max()), tol)
+
+
+def test_side_gate_released_by_per_step_encoder_backward(monkeypatch):
+    """A batch past the persistent kernels' resident capacity (B = 544: 17
+    encoder BPTT groups x 2 directions x 8 members = 272 workgroups > 256 CUs)
+    runs the per-step encoder backward.  The training step still queues the
+    side-stream gate (it waits for the NEXT encoder BPTT to be resident), so
+    the per-step encoder backward must release it itself; otherwise the
+    decoder's weight gradients wait out the gate's spin bound (~0.1 s) every
+    step.  Checked: the dispatch is the per-step one, the step with
+    the gate on is no slower than with it off (ABCD_SIDE_GATE=0) beyond noise,
+    and both give the same loss."""
+    import time
+    sys.path.insert(0, REPO)
+    import bench
+    from modules import engine, noise, _native as N
+    cfg = dict(bench.CONFIGS["c2"], B=544, tmin=12, tmax=24)
+    batch = bench.make_batch(cfg, 77, "cpu")
+    L = batch["L"]
+    g = torch.Generator().manual_seed(78)
+    feat = -torch.empty(cfg["B"], cfg["K"]).exponential_(generator=g).log()
+    eps = torch.randn(L, cfg["F"], generator=g)
+    step = bench.build(cfg, "cuda")
+    args = (batch["data"].cuda(), batch["batch_sizes"], batch["is_offset"].cuda(), batch["speakers"].cuda(), cfg["N"])
+
+    def run(gate):
+        if gate:
+            monkeypatch.delenv("ABCD_SIDE_GATE", raising=False)
+        else:
+            monkeypatch.setenv("ABCD_SIDE_GATE", "0")
+        best, loss = 1e9, None
+        for _ in range(3):
+            noise.replay(feat, eps)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sc, _ = step.forward_backward(*args)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+            loss = float(sc.cpu()[engine.LOSS])
+        return best, loss
+
+    N.lib().abcd_dispatch_reset()
+    t_on, loss_on = run(True)
+    assert "per-step" in N.dispatch()["enc_bwd"][0], N.dispatch()["enc_bwd"]
+    assert N.lib().abcd_device_status() == 0
+    t_off, loss_off = run(False)
+    assert loss_on == loss_off, (loss_on, loss_off)
+    assert t_on <= 1.5 * t_off + 0.01, (t_on, t_off)

@@ -12,8 +12,8 @@ pytestmark = pytest.mark.gpu
 def test_gemm_nt_vs_torch(M, N, K):
     """C = A B^T + bias; the shapes from (8001, 520, 144) on take the
     frame-parallel route (>= 240 128-wide tiles): K <= 256 the frame-streaming
-    split-fp32 gemm_x6r (ragged M / N, a partial last K chunk, the c2 input
-    projection, the GRU encoder's 3 x 2 x 256 = 1536 gate columns: slice
+    split-fp32 gemm_x6r8 (ragged M / N, a partial last K chunk -- K in (128,
+    144] on 16-deep MFMAs --, the c2 input projection, the GRU encoder's 3 x 2 x 256 = 1536 gate columns: slice
     counts that do not divide the grid evenly), else the fragment-staged
     gemm_x6f."""
     from modules import _native as Nn
@@ -28,22 +28,6 @@ def test_gemm_nt_vs_torch(M, N, K):
     ref = (A.double() @ B.double().t() + bias.double()).float()
     err = (C - ref).abs().max().item()
     assert err <= 1e-5 * K ** 0.5 * 4 + 1e-5, err
-
-
-@pytest.mark.parametrize("M,N,K", [(64044, 2048, 144), (9000, 300, 136), (30001, 384, 256)])
-def test_gemm_nt_x6r_four_wave_form(M, N, K, monkeypatch):
-    """ABCD_X6R8=0: the four-wave gemm_x6r that gemm_x6r8 replaced, at the
-    frame-streaming shapes of test_gemm_nt_vs_torch."""
-    monkeypatch.setenv("ABCD_X6R8", "0")
-    test_gemm_nt_vs_torch(M, N, K)
-
-
-@pytest.mark.parametrize("M,N,K", [(64044, 2048, 144), (8001, 520, 144)])
-def test_gemm_nt_x6r8_padded_tail(M, N, K, monkeypatch):
-    """ABCD_X6R8_T16=0: gemm_x6r8 with the K = 144 last chunk zero-padded to
-    32-deep instead of the default 16-deep MFMAs."""
-    monkeypatch.setenv("ABCD_X6R8_T16", "0")
-    test_gemm_nt_vs_torch(M, N, K)
 
 
 @pytest.mark.parametrize("wg", ["3", "2"])

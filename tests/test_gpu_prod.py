@@ -92,17 +92,6 @@ def test_fused_step_prod_vs_reference(name):
         assert abs(float(delta.sum()) - ref_s) <= GRAD_TOL * ref_n * delta.numel() ** 0.5 + 1e-9, k
 
 
-@pytest.mark.parametrize("env", ["ABCD_OFFSET_FUSED=0", "ABCD_X6R8=0", "ABCD_TNB=2"])
-def test_fused_step_prod_replaced_forms(env, monkeypatch):
-    """The forms round 5's defaults replaced, still selected by switch (and,
-    for the offset head, by shapes the fused GEMM modes do not take): the
-    separate offset-head kernels beside plain GEMMs, the four-wave gemm_x6r,
-    64 x 64 gemm_tn_batch tiles -- the same reference checks as the default."""
-    k, v = env.split("=")
-    monkeypatch.setenv(k, v)
-    test_fused_step_prod_vs_reference("lstm_k128")
-
-
 @pytest.mark.parametrize("name", ["lstm_k128", "gru_k1024_spk", "plain_lstm"])
 def test_module_surface_prod_vs_reference(name):
     """encoder(packed) -> sampler -> sample -> kl -> decoder on the nn.Module
@@ -189,3 +178,46 @@ def test_op_surface_timeout_does_not_poison_later_launches(monkeypatch):
         torch.cuda.synchronize()
     N.op_status.sync("launch after the timeouts")
     assert torch.equal(again, good)
+
+
+def test_fused_step_wide_decoder_separate_offset_head():
+    """The offset head's GEMM-folded forms (gemm_x6r8 modes 1 / 2) take a
+    decoder hidden size <= 256; a wider decoder (H = 288 here) runs the
+    separate head kernels (dec_offset_head / dec_offset_bwd) beside plain
+    GEMMs, and the per-step recurrent kernels.  One fused training step
+    against the oracle (model.py:287-334 offset MLP + BCE, learning.py:147-163)."""
+    from modules import engine, noise
+    from modules import model as M
+    from oracle import abcd_oracle as O
+    F, He, Hd, Hm, D, K = 33, 32, 288, 64, 32, 16
+    lengths = [11, 9, 9, 6, 3, 2]
+    g = torch.Generator().manual_seed(17)
+    seqs = [torch.randn(T, F, generator=g) for T in lengths]
+    packed = torch.nn.utils.rnn.pack_sequence(seqs)
+    is_off = torch.nn.utils.rnn.pack_sequence([torch.tensor([0.0] * (T - 1) + [1.0]) for T in lengths]).data
+    B = len(lengths)
+    gumbel = -torch.empty(B, K).exponential_(generator=g).log()
+    eps = torch.randn(packed.data.shape[0], F, generator=g)
+    torch.manual_seed(1111)
+    enc = M.RNN_Variational_Encoder(F, He)
+    samp = M.ABCDSampler(enc.hidden_size_total, Hm, K, D)
+    dec = M.RNN_Variational_Decoder(F, Hd, Hm, D)
+    for m in (enc, samp, dec):
+        m.cuda().train()
+    ocfg = O.default_cfg(F=F, H=He, Hdec=Hd, Hm=Hm, D=D, K=K)
+    P = O.init_params(ocfg, 1111)
+    named = named_params(enc, samp, dec)
+    for k, p in named.items():
+        assert torch.equal(p.detach().cpu(), P[k]), k
+    step = engine.FusedStep(enc, samp, dec)
+    noise.replay(gumbel, eps)
+    sc, _ = step.forward_backward(packed.data.cuda(), packed.batch_sizes, is_off.cuda(), torch.zeros(B).cuda(), 50)
+    torch.cuda.synchronize()
+    out, grads, _, _, _ = O.train_step(
+        P, dict(data=packed.data, batch_sizes=packed.batch_sizes, is_offset=is_off), ocfg,
+        dict(feat=gumbel, eps=eps), 50)
+    sc = sc.cpu()
+    for i, k in ((engine.EM, "em"), (engine.OFF, "off"), (engine.KL, "kl"), (engine.LOSS, "loss")):
+        assert abs(float(sc[i]) - float(out[k])) <= 1e-4 * abs(float(out[k])) + 1e-5, (k, float(sc[i]), float(out[k]))
+    for k, p in named.items():
+        assert rel_err(step.flat.grad_of(p), grads[k]) < GRAD_TOL, (k, rel_err(step.flat.grad_of(p), grads[k]))
