@@ -323,11 +323,28 @@ int abcd_decoder_forward_split(const abcd_decoder_cfg* cfg, const abcd_decoder_p
                                const float* eps, const float* xmask, uint64_t seed, uint64_t offset,
                                float* flatten_out, float* mu, float* log_var, float* offset_logits, float* losses,
                                void* ws, size_t ws_bytes, void* stream, void* loss_stream);
+/* wgrad_stream == ABCD_DEFER_PARAMS: only the data-gradient part (offset head,
+ * BPTT, initial-state / feature gradients: d_features complete in `stream`
+ * order); the weight gradients are queued by abcd_decoder_backward_params
+ * with the SAME arguments later on this host thread (the training step calls
+ * it after queuing the sampler and encoder backward). */
 int abcd_decoder_backward_dropout(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
                                   const float* features, const int64_t* speakers, const float* gt_offset,
                                   const float* xmask, const float* d_em, const float* d_off, float* d_features,
                                   const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream,
                                   void* wgrad_stream);
+/* the deferred weight gradients of the preceding
+ * abcd_decoder_backward_dropout(..., ABCD_DEFER_PARAMS) (same arguments): on
+ * wgrad_stream (NULL or == stream: on `stream`) behind an event recorded at the
+ * end of that call's data path, in the tiling that co-resides with the
+ * encoder's persistent BPTT; with the side-stream gate on, behind a wait for
+ * the encoder BPTT launched in between to be resident.  The caller joins
+ * wgrad_stream before reading the gradients. */
+int abcd_decoder_backward_params(const abcd_decoder_cfg* cfg, const abcd_decoder_params* p, const abcd_packed* x,
+                                 const float* features, const int64_t* speakers, const float* gt_offset,
+                                 const float* xmask, const float* d_em, const float* d_off, float* d_features,
+                                 const abcd_decoder_grads* g, void* ws, size_t ws_bytes, void* stream,
+                                 void* wgrad_stream);
 
 /* ------------------------------------------------------------------------
  * Featurisation + packing on the device: replaces the per-item host path
@@ -421,17 +438,16 @@ void abcd_dispatch_reset(void);
  * (dev_out holds 2 * blocks u32; the placement the persistent kernels' group
  * roles rely on).  Returns 0 / a HIP error. */
 void abcd_debug_persist_prof(unsigned long long* dev_buf, int mask);
-/* Side-stream gate (per calling host thread, default off): the weight-gradient
- * work abcd_decoder_backward_overlap queues on its wgrad_stream first waits,
- * on the device and bounded (tens of ms, then it proceeds), until the NEXT
- * encoder backward of this process on that device has started: a persistent
- * BPTT once every workgroup is resident, or a per-step encoder backward (grid
- * past the resident capacity, other shapes) as soon as it is queued (it
- * releases the gate itself) -- for a caller that queues
- * abcd_encoder_backward* right after the decoder and sampler backward, as the
- * training step does.  Without it the side GEMMs can take a CU's room before
- * a BPTT member is placed there.  Read when that call is made, on the thread
- * that makes it (the training step sets it around its decoder backward). */
+/* Side-stream gate (per calling host thread, default off): read by a deferred
+ * abcd_decoder_backward_dropout(..., ABCD_DEFER_PARAMS).  The first encoder
+ * BPTT this thread launches persistently after it becomes the gate's target,
+ * and the abcd_decoder_backward_params call that follows queues, in front of
+ * its side-stream work, a wait (on the device, bounded) until every workgroup
+ * of that launch is resident -- without it the side GEMMs can take a CU's
+ * room before a BPTT member is placed there.  No persistent BPTT in between
+ * (a per-step encoder backward): no wait.  The wait is queued after the
+ * BPTT's launch, so a side stream that shares the BPTT's hardware queue
+ * cannot hold the BPTT back. */
 void abcd_side_gate_enable(int on);
 int abcd_debug_xcc_map(unsigned* dev_out, int blocks, void* stream);
 /* 0 if no persistent recurrent kernel has timed out waiting for its group

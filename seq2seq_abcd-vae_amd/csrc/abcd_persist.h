@@ -67,6 +67,13 @@ struct PDecFwdArgs {
   const float *W1, *b1;            // 2Hm x H, 2Hm  ([mu; lv] first layers)
   const float *W2m, *W2l, *b2m, *b2l;  // Fp x Hm (padded rows), Fp
   const float* eps; uint64_t seed, offset;  // explicit noise (rows x F) or Philox stream
+  // eps_fill: eps is a workspace the launch fills itself with the Philox
+  // stream (philox_normal(seed, offset + row F + col), nfill = L F values):
+  // dec_fwd_x6's members without an emit tile draw step t + 1's rows in step
+  // t's emit phase (step 0's before the loop); the other persistent forms get
+  // it filled by abcd_fill_normal in front of their launch
+  int eps_fill;
+  long nfill;
   const float* xmask;              // input-dropout noise of the cell input (rows x F, 0 or 1/(1-p)); null: none
   float *Xin, *Hprev, *Cprev, *Gst, *Cst, *Hs, *Aact, *MU, *LV, *OUT;
 };
@@ -131,12 +138,17 @@ int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launch
 // ABCD_PERSIST=0 disables the persistent path (parity/timing comparisons).
 bool persist_enabled();
 
-// Side-stream gate (abcd_side_gate_enable): a one-wave kernel on the side
-// stream that waits, bounded, until the NEXT encoder BPTT launch has every
-// workgroup resident, so side work queued behind it cannot take that
+// Side-stream gate (abcd_side_gate_enable): a deferred decoder backward arms
+// it (side_gate_arm), the first encoder BPTT launched after that on this host
+// thread becomes its target, and abcd_decoder_backward_params queues, in front
+// of the deferred side work, a one-wave kernel that waits (bounded) until that
+// launch has every workgroup resident -- so the side GEMMs cannot take the
 // launch's CUs first (two side GEMM workgroups on a CU leave no room for a
-// BPTT member, which then starts only when one of them retires).
+// BPTT member, which then starts only when one of them retires).  Queued after
+// the launch, so it never holds back a BPTT that shares its hardware queue.
 bool side_gate_enabled();
+void side_gate_arm();
+void side_gate_disarm();
 int side_gate(hipStream_t sw);
 
 }  // namespace abcd

@@ -155,7 +155,9 @@ DEV void spin_timed_out() {
   __hip_atomic_store(&g_persist_abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // lane 0 of the workgroup polls until *cnt >= target (bounded), then the
-// barrier releases every wave
+// barrier releases every wave (two polls in flight -- a new load issued
+// before the previous one is checked -- measured slower: c2 step 8.43-8.49 ->
+// 8.51-8.54 ms, dec_fwd +50 us, same box)
 DEV void group_wait(unsigned* cnt, unsigned target, int pw = 0) {
   if (threadIdx.x == 64 * pw) {
     unsigned spins = 0;
@@ -1133,6 +1135,23 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
   }
   const float bias0 = a.bias[dec_cell_row(H, u0, 0, r)], bias1 = a.bias[dec_cell_row(H, u0, 1, r)];
   const float b1v = has1 ? a.b1[16 * mem + r] : 0.f;
+  // members without an emit tile draw the Philox noise of the group's rows of
+  // a step into the eps workspace (write-through; read by the emit members'
+  // sc1 loads a step later, after at least one hand-off that drained these
+  // stores): the same philox_normal values abcd_fill_normal writes, drawn in
+  // the emit phase these members otherwise idle through -- a side-stream fill
+  // ran beside the input projection and delayed it / the encoder's launch
+  const int nidle = M - 2 * n2t;
+  auto fill_eps = [&](int ts) {
+    const int o1 = a.off[ts], bs1 = a.off[ts + 1] - o1, rows = min(PERSIST_ROWS, bs1 - rt * PERSIST_ROWS);
+    float* ep = const_cast<float*>(a.eps);
+    for (int e = (mem - 2 * n2t) * 256 + (int)threadIdx.x; e < rows * F; e += nidle * 256) {
+      const long rr = o1 + rt * PERSIST_ROWS + e / F;
+      const int col = e % F;
+      st_sc1(ep + rr * F + col, philox_normal(a.seed, a.offset + (uint64_t)rr * F + col));
+    }
+  };
+  if (a.eps_fill && !has2 && nidle > 0) fill_eps(0);
   const int col2 = 16 * j2 + r;
   const float b2v = has2 ? (part ? a.b2l[col2] : a.b2m[col2]) : 0.f;
   const bool lo = r < 8;
@@ -1254,6 +1273,7 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
     gs.publish();
     PSTAMP(3);
     // ---------------- emit ----------------
+    if (a.eps_fill && !has2 && nidle > 0 && i + 1 < T) fill_eps(t + 1);
     // the mu waves' noise, drawn before the wait (independent of the recurrence)
     float epre[4] = {0.f, 0.f, 0.f, 0.f}, mpre[4] = {1.f, 1.f, 1.f, 1.f};
     if (has2 && part == 0 && col2 < F) {
@@ -1262,7 +1282,9 @@ __global__ __launch_bounds__(256) void dec_fwd_x6(PDecFwdArgs a) {
         const int b = erow0 + 4 * q + g;
         if (b < bs) {
           const long rr = o + b;
-          epre[g] = a.eps ? a.eps[rr * F + col2] : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col2);
+          epre[g] = a.eps_fill ? __hip_atomic_load(a.eps + rr * F + col2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : a.eps    ? a.eps[rr * F + col2]
+                               : philox_normal(a.seed, a.offset + (uint64_t)rr * F + col2);
           if (a.xmask && b < next_bs) mpre[g] = a.xmask[(long)(next_off + b) * F + col2];
         }
       }
@@ -1768,7 +1790,6 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
         const BufKC2x A{ra, ra, (uint32_t)Fp * 4u, (uint32_t)Fp * 4u, ncz, Fp};  // k >= Fp reads 0
         wave_mma_x6<2, NCZ, 4>(acc, A, zr0 + r, B1, ncz, lane, q);
       }
-      const __amdgpu_buffer_rsrc_t rzs = make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         float dz[4];
@@ -1776,8 +1797,6 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
         for (int g = 0; g < 4; ++g) dz[g] = acc[jj][g] * (1.f - zpre[jj][g] * zpre[jj][g]);
 #pragma unroll
         for (int g = 0; g < 4; ++g) ZT[(16 * w + 4 * q + g) * W16_ZTP + 16 * jj + r] = dz[g];
-        const f4 zq = tp_quad(tb, dz, lane);
-        if (zr0 < bs) st4(rzs, (uint32_t)((zr0 + trow) * 2 * Hm + 32 * mem + 16 * jj + tcol) * 4u, zq, false);
       }
     }
 #ifdef ABCD_STAMP_DIAG
@@ -1804,6 +1823,16 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
 #endif
     gs.publish();
     PSTAMP(3);
+    // the dZ stash for the weight gradients (plain 16-B stores of the LDS tile,
+    // 32 rows x 32 columns = 1 quad per thread) after the publish, so the
+    // publish's drain does not wait for them
+    {
+      const int row = threadIdx.x >> 3, qd = 4 * (threadIdx.x & 7);
+      if (rowg + row < bs)
+        st4(make_rsrc(a.dZ + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u),
+            (uint32_t)((rowg + row) * 2 * Hm + 32 * mem + qd) * 4u,
+            *reinterpret_cast<const f4*>(ZT + row * W16_ZTP + qd), false);
+    }
     // ---------------- P2: dh -> cell backward -> dG_t -> dx partials ----------------
     float pg[4][4], pc[4], pcp[4], pdho[4];
     {
@@ -2375,12 +2404,13 @@ static hipError_t zero_sync(hipStream_t s, unsigned* sync, int ngroups) {
 
 // the side-stream gate's bookkeeping: encoder BPTT launches per device (the
 // device counts the same launches once all their workgroups have started) and
-// whether a queued gate still waits for one.  The switch is per host thread:
-// the training step turns it on around its own decoder-backward call, so
-// another thread's decoder backward never gets a gate it did not ask for.
+// the gate's target.  The switch and the target are per host thread: the
+// training step turns the switch on around its own decoder backward, so
+// another thread's calls never queue a gate they did not ask for.
 static unsigned h_bptt_launches[64];
-static bool h_gate_pending[64];
 static thread_local bool g_side_gate = false;
+static thread_local bool tl_gate_armed[64];     // a deferred decoder backward waits for the next BPTT launch
+static thread_local unsigned tl_gate_target[64];  // that launch's count (0: none was launched)
 static int cur_dev() {
   int dev = 0;
   return hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 ? dev : 0;
@@ -2390,25 +2420,11 @@ static int cur_dev() {
 static void bptt_launch(PBwdArgs& b, int ngroups) {
   b.started = b.sync + (size_t)2 * ngroups * PERSIST_SYNC_STRIDE;
   const int dev = cur_dev();
-  ++h_bptt_launches[dev];
-  h_gate_pending[dev] = false;
-}
-// an encoder backward that did NOT launch a persistent BPTT (the per-step
-// kernels: grid past the resident capacity, an unsupported shape, or
-// ABCD_PERSIST=0) releases a pending gate itself: one single-lane kernel on
-// the BPTT's stream bumps the epoch, so the side work behind the gate starts
-// when the encoder backward starts instead of after the gate's spin bound
-__global__ void bptt_release_kernel() {
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(&g_bptt_epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-static int bptt_release(hipStream_t s) {
-  const int dev = cur_dev();
-  if (!h_gate_pending[dev]) return 0;
-  bptt_release_kernel<<<1, 64, 0, s>>>();
-  ABCD_TRY(hipGetLastError());
-  ++h_bptt_launches[dev];
-  h_gate_pending[dev] = false;
-  return 0;
+  const unsigned n = ++h_bptt_launches[dev];
+  if (tl_gate_armed[dev]) {
+    tl_gate_target[dev] = n;
+    tl_gate_armed[dev] = false;
+  }
 }
 // ABCD_SIDE_GATE=0 keeps it off whatever the switch says (same-box A/B)
 bool side_gate_enabled() {
@@ -2416,10 +2432,25 @@ bool side_gate_enabled() {
   const bool env_off = v && v[0] == '0';
   return g_side_gate && !env_off && persist_enabled();  // (no persistent BPTT: nothing to wait for)
 }
+void side_gate_arm() {
+  const int dev = cur_dev();
+  tl_gate_armed[dev] = side_gate_enabled();
+  tl_gate_target[dev] = 0;
+}
+void side_gate_disarm() {
+  const int dev = cur_dev();
+  tl_gate_armed[dev] = false;
+  tl_gate_target[dev] = 0;
+}
+// queued on the side stream AFTER the encoder backward: waits only if that
+// backward launched a persistent BPTT since the arming decoder backward (a
+// per-step encoder backward, or none, leaves nothing to wait for)
 int side_gate(hipStream_t sw) {
   const int dev = cur_dev();
-  side_gate_kernel<<<1, 64, 0, sw>>>(h_bptt_launches[dev] + 1);
-  h_gate_pending[dev] = true;
+  const unsigned target = tl_gate_target[dev];
+  side_gate_disarm();
+  if (!target) return 0;
+  side_gate_kernel<<<1, 64, 0, sw>>>(target);
   return (int)hipGetLastError();
 }
 
@@ -2543,14 +2574,8 @@ static int launch_bwd_w8(hipStream_t s, const PBwdArgs& a, bool* launched) {
   return 0;
 }
 
-static int persist_encoder_bwd_k(hipStream_t s, int G, const PBwdArgs& a, bool* launched);
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
   *launched = false;
-  const int rc = persist_encoder_bwd_k(s, G, a, launched);
-  if (rc || *launched) return rc;
-  return bptt_release(s);
-}
-static int persist_encoder_bwd_k(hipStream_t s, int G, const PBwdArgs& a, bool* launched) {
   if (!persist_enabled()) return 0;
   if (a.part && a.H == 256) {
     const int rc = G == 4 ? launch_bwd_w8<4>(s, a, launched) : launch_bwd_w8<3>(s, a, launched);
@@ -2572,6 +2597,12 @@ static int persist_encoder_bwd_k(hipStream_t s, int G, const PBwdArgs& a, bool* 
 }
 
 
+// eps_fill for a form that does not draw the noise itself: the whole block up
+// front (abcd_fill_normal: the same philox_normal(seed, offset + i) values)
+static int prefill_eps(hipStream_t s, const PDecFwdArgs& a) {
+  if (!a.eps_fill) return 0;
+  return abcd_fill_normal(const_cast<float*>(a.eps), a.nfill, a.seed, a.offset, s);
+}
 template <int NCC>
 static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   const int M = a.H / 8, nchx = a.feedback ? a.Fp / 16 : 0, nchh = a.H / 16, nchm = a.Hm / 16;
@@ -2582,8 +2613,10 @@ static int launch_dec_fwd(hipStream_t s, const PDecFwdArgs& a, bool* launched) {
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(dec_fwd_persist<NCC>, grid, lds, &ok));
   if (!ok) return 0;
+  ABCD_TRY((hipError_t)prefill_eps(s, a));
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
+  b.eps_fill = 0;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {
@@ -2604,8 +2637,11 @@ static int launch_dec_fwd_x6_k(hipStream_t s, const PDecFwdArgs& a, bool* launch
   bool ok = false;
   ABCD_TRY((hipError_t)fits_resident(dec_fwd_x6<NCC, NH32, NM32, GRU, HPRE>, grid, lds, &ok));
   if (!ok) return 0;
+  const bool inkernel = 2 * (a.Fp / 16) < M;  // members without an emit tile draw the noise
+  if (!inkernel) ABCD_TRY((hipError_t)prefill_eps(s, a));
   ABCD_TRY(zero_sync(s, a.sync, a.nrt));
   PDecFwdArgs b = a;
+  if (!inkernel) b.eps_fill = 0;
   b.flags = 1;  // per-member flags (the group-counter form measured slower)
   b.prof = (g_prof_mask & 4) ? g_prof : nullptr;
   {

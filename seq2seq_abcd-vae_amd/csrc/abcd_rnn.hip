@@ -1212,13 +1212,16 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
     pa.W1 = w.W1cat; pa.b1 = w.b1cat;
     pa.W2m = w.W2mp; pa.W2l = w.W2lp; pa.b2m = w.b2mp; pa.b2l = w.b2lp;
     pa.eps = eps; pa.seed = seed; pa.offset = offset; pa.xmask = xmask;
-    // Philox noise drawn up front (abcd_fill_normal: the same philox_normal(seed,
-    // offset + row * F + col) the kernel would draw), read with one load per
-    // element instead of ~1 us of VALU per step on the emit phase's path
-    // (dec_fwd 2.31 -> 2.17 ms at c2).  ABCD_DEC_EPSFILL=0: drawn in-kernel.
+    // Philox noise in a workspace block (the same philox_normal(seed, offset +
+    // row * F + col) the kernel would draw), read with one load per element
+    // instead of ~1 us of VALU per step on the emit phase's path (dec_fwd 2.31
+    // -> 2.17 ms at c2); drawn by the persistent launch's idle members (or up
+    // front for the forms without them: PDecFwdArgs::eps_fill).
+    // ABCD_DEC_EPSFILL=0: drawn by the emit waves themselves.
     if (!eps && persist_enabled() && dec_eps_fill()) {
-      ABCD_TRY((hipError_t)abcd_fill_normal(w.EPS, (long)L * F, seed, offset, s));
       pa.eps = w.EPS;
+      pa.eps_fill = 1;
+      pa.nfill = (long)L * F;
     }
     pa.Xin = w.Xin; pa.Hprev = w.Hprev; pa.Cprev = w.Cprev; pa.Gst = w.Gst; pa.Cst = w.Cst; pa.Hs = w.Hs;
     pa.Aact = w.Aact; pa.MU = w.MU; pa.LV = w.LV; pa.OUT = w.OUT;
@@ -1297,13 +1300,16 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
 
 // reusable cross-stream events per device and slot (re-recorded each call:
 // hipStreamWaitEvent captures the record that precedes it).  Slot 0: decoder
-// data-gradient path done; 1: encoder counters zeroed; 2: encoder chunk A done.
+// data-gradient path done; 1: encoder counters zeroed; 2: encoder chunk A done;
+// 3: decoder data-gradient path done, weight gradients deferred (the record of
+// abcd_decoder_backward_dropout(..., ABCD_DEFER_PARAMS), waited for by the
+// abcd_decoder_backward_params call that follows it on this host thread).
 static int fork_event(hipEvent_t* ev, int slot) {
   static std::mutex mu;
-  static hipEvent_t evs[64][3] = {};
+  static hipEvent_t evs[64][4] = {};
   int dev = 0;
   ABCD_TRY(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64 || slot < 0 || slot >= 3) return (int)hipErrorInvalidDevice;
+  if (dev < 0 || dev >= 64 || slot < 0 || slot >= 4) return (int)hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lk(mu);
   if (!evs[dev][slot]) ABCD_TRY(hipEventCreateWithFlags(&evs[dev][slot], hipEventDisableTiming));
   *ev = evs[dev][slot];
@@ -1327,11 +1333,41 @@ extern "C" int abcd_decoder_backward_overlap(const abcd_decoder_cfg* c, const ab
                                        ws, ws_bytes, stream, wgrad_stream);
 }
 
+// the decoder backward in two parts: DEC_DATA = the offset head, the BPTT and
+// the initial-state / feature gradients (everything the sampler and encoder
+// backward need), DEC_WGRAD = the weight gradients over all frames
+enum { DEC_DATA = 1, DEC_WGRAD = 2 };
+static int dec_bwd_impl(const abcd_decoder_cfg* c, const abcd_decoder_params* p, const abcd_packed* x,
+                        const float* features, const int64_t* speakers, const float* gt_offset, const float* xmask,
+                        const float* d_em, const float* d_off, float* d_features, const abcd_decoder_grads* g,
+                        void* ws, size_t ws_bytes, void* stream, void* wgrad_stream, int mode);
+
 extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
                                              const abcd_packed* x, const float* features, const int64_t* speakers,
                                              const float* gt_offset, const float* xmask, const float* d_em,
                                              const float* d_off, float* d_features, const abcd_decoder_grads* g,
                                              void* ws, size_t ws_bytes, void* stream, void* wgrad_stream) {
+  if (wgrad_stream == ABCD_DEFER_PARAMS)
+    return dec_bwd_impl(c, p, x, features, speakers, gt_offset, xmask, d_em, d_off, d_features, g, ws, ws_bytes,
+                        stream, nullptr, DEC_DATA);
+  return dec_bwd_impl(c, p, x, features, speakers, gt_offset, xmask, d_em, d_off, d_features, g, ws, ws_bytes, stream,
+                      wgrad_stream, DEC_DATA | DEC_WGRAD);
+}
+
+extern "C" int abcd_decoder_backward_params(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
+                                            const abcd_packed* x, const float* features, const int64_t* speakers,
+                                            const float* gt_offset, const float* xmask, const float* d_em,
+                                            const float* d_off, float* d_features, const abcd_decoder_grads* g,
+                                            void* ws, size_t ws_bytes, void* stream, void* wgrad_stream) {
+  ABCD_REQUIRE(wgrad_stream != ABCD_DEFER_PARAMS);
+  return dec_bwd_impl(c, p, x, features, speakers, gt_offset, xmask, d_em, d_off, d_features, g, ws, ws_bytes, stream,
+                      wgrad_stream, DEC_WGRAD);
+}
+
+static int dec_bwd_impl(const abcd_decoder_cfg* c, const abcd_decoder_params* p, const abcd_packed* x,
+                        const float* features, const int64_t* speakers, const float* gt_offset, const float* xmask,
+                        const float* d_em, const float* d_off, float* d_features, const abcd_decoder_grads* g,
+                        void* ws, size_t ws_bytes, void* stream, void* wgrad_stream, int mode) {
   ABCD_REQUIRE(dec_check(c) == 0 && p && x && x->data && features && g && ws && d_em && d_off && gt_offset);
   ABCD_REQUIRE(!xmask || c->feedback);
   ABCD_REQUIRE(validate_batch(x->batch_sizes, x->T, x->L, x->B) == 0);
@@ -1351,6 +1387,8 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
   // (the transposed weights of the backward GEMMs were packed by the forward
   // pass, in its one pack launch: the backward reads the forward's stashes
   // from the same workspace anyway)
+  const float* FS = S > 0 ? w.FS : features;
+  if (mode & DEC_DATA) {
   // ---- offset head backward (batched over all frames): dZo formed from Zo
   // inside the DHO GEMM where it applies ----
   bool fused = false;
@@ -1423,12 +1461,19 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
                             ACT_NONE, sc, scf));
   dec_hidden_init_bwd<<<launch_grid((long)B * H), 256, 0, s>>>(w.dH0, w.DC0, B, H, G == 4, w.dhid);
   ABCD_CHECK_LAUNCH();
-  const float* FS = S > 0 ? w.FS : features;
   ABCD_TRY((hipError_t)gemm(s, B, DS, Htot, opKC(w.dhid, Htot, B), opKC(w.Wf2hT, Htot, DS), w.dFS, DS, 1.f, 0.f,
                             nullptr, ACT_NONE, sc, scf));
   dec_feats_bwd<<<launch_grid((long)B * std::max(D, 1)), 256, 0, s>>>(w.dFS, D, S, B, speakers, c->num_speakers,
                                                                      d_features, S > 0 ? g->embed_speaker : nullptr);
   ABCD_CHECK_LAUNCH();
+  }
+  if (!(mode & DEC_WGRAD)) {  // deferred: mark the end of the data path for abcd_decoder_backward_params
+    hipEvent_t ev;
+    ABCD_TRY((hipError_t)fork_event(&ev, 3));
+    ABCD_TRY(hipEventRecord(ev, s));
+    side_gate_arm();  // the next encoder BPTT launch of this thread is the gate's target
+    return 0;
+  }
   // ---- weight gradients, K = L frames ----
   // With a separate wgrad stream they run there, behind the data-gradient
   // path above, beside whatever the caller queues next on `stream` (the
@@ -1436,15 +1481,18 @@ extern "C" int abcd_decoder_backward_dropout(const abcd_decoder_cfg* c, const ab
   const bool side = wgrad_stream && wgrad_stream != stream;
   if (side) {
     hipEvent_t ev;
-    ABCD_TRY((hipError_t)fork_event(&ev, 0));
-    ABCD_TRY(hipEventRecord(ev, s));
+    ABCD_TRY((hipError_t)fork_event(&ev, (mode & DEC_DATA) ? 0 : 3));
+    if (mode & DEC_DATA) ABCD_TRY(hipEventRecord(ev, s));
     s = (hipStream_t)wgrad_stream;
     ABCD_TRY(hipStreamWaitEvent(s, ev, 0));
-    // abcd_side_gate_enable: hold the side work until the encoder BPTT that
-    // follows is resident (its members would otherwise wait for CUs the
-    // side GEMMs took first: up to 150 us of start skew measured)
-    if (side_gate_enabled()) ABCD_TRY((hipError_t)side_gate(s));
+    // deferred form with abcd_side_gate_enable: the side work waits, on the
+    // device, until the encoder BPTT queued since the data part is resident
+    // (its members would otherwise wait for CUs the side GEMMs took first: up
+    // to 150 us of start skew measured).  Queued only AFTER that launch, so
+    // even a side stream sharing the BPTT's hardware queue cannot hold it back.
+    if (!(mode & DEC_DATA)) ABCD_TRY((hipError_t)side_gate(s));
   }
+  if (!(mode & DEC_DATA) && !side) side_gate_disarm();
   GemmSideScope side_tiles(side);
   if (g->f2h_w)
     ABCD_TRY((hipError_t)gemm(s, Htot, DS, B, opKM(w.dhid, Htot, Htot), opKM(FS, DS, DS), g->f2h_w, DS, 1.f, 0.f,

@@ -159,15 +159,9 @@ DEV void prior_block(const float* psl, int K, int Kv, double N, float a0, float*
 }
 
 // standalone form (abcd_sampler_kl, abcd_sampler_prior): alpha / elog land in
-// the global stash.  The training step queues it on the side stream while the
-// input projection holds every CU; at issue priority 0 its fp64 chains shared
-// the SIMDs with the GEMM's waves and ran ~210 us (11 us alone), ending just
-// before the encoder's persistent launch -- on a slower box it would hold a CU
-// one of that launch's members needs.  At priority 3 its waves win the issue
-// arbitration over the GEMM's, so it finishes early in the projection.
+// the global stash
 __global__ void kl_prior(const float* psl, int K, int Kv, double N, float a0, float* p_out, float* alpha_out,
                          float* elog_out, float* tri_out, double* kl_small) {
-  __builtin_amdgcn_s_setprio(3);
   __shared__ double sh[16];
   prior_block(psl, K, Kv, N, a0, alpha_out, elog_out, sh, true, p_out, alpha_out, elog_out, tri_out, kl_small);
 }

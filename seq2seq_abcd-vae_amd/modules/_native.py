@@ -134,6 +134,9 @@ _SIGS = {
     "abcd_decoder_backward_dropout": (c_int, [_P(DecoderCfg), _P(DecoderParams), _P(Packed), c_void_p, c_void_p,
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, _P(DecoderGrads),
                                               c_void_p, c_size_t, c_void_p, c_void_p]),
+    "abcd_decoder_backward_params": (c_int, [_P(DecoderCfg), _P(DecoderParams), _P(Packed), c_void_p, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, _P(DecoderGrads),
+                                             c_void_p, c_size_t, c_void_p, c_void_p]),
     "abcd_stft_frames": (c_int, [ctypes.c_longlong, c_int, c_int, c_int]),
     "abcd_featurize_workspace_bytes": (c_size_t, [c_int, c_int]),
     "abcd_featurize_packed": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_float,

@@ -26,6 +26,7 @@ from .model import ABCDSampler
 # the step's results are invalid; check_status raises)
 EM, OFF, KL, LOSS, NORM, PPL_CLUSTER, PPL_BATCH, PPL_SHAPE, STATUS = range(9)
 N_SCALARS = 9
+_SIDE_STREAMS = {}  # (device index, k) -> torch.cuda.Stream shared by every FusedStep (_side_stream)
 
 
 class FlatParams:
@@ -175,9 +176,7 @@ class FusedStep:
             de = self.pad.dims[0]
             enc_noise = [_pad.pad_col_blocks(n, de.dirs, de.H, de.Hp) for n in enc_noise]
         # the sampler's and the decoder's draws, in the reference's order, taken
-        # up front: the decoder's Philox block (L x F normals) is then drawn on
-        # the side stream while the encoder runs (VALU work beside a
-        # hand-off-bound kernel) instead of in front of the decoder
+        # up front (the decoder's Philox block is drawn inside its launch)
         W = ksamp._logit_width()
         if self.plain:
             mode, tau = 0, 1.0
@@ -192,17 +191,22 @@ class FusedStep:
         eps, eseed, eoff, xmask = _noise.decoder_noise(bs_keep, F, pdrop, dev)
         side = self._side_stream()
         side.wait_stream(torch.cuda.current_stream(dev))  # the previous step (parameters, eps) is queued before
-        if eps is None:  # Philox mode: eps[row, f] = philox_normal(eseed, eoff + row * F + f)
-            eps = self._workspace("eps", L * F * 4)[:L * F * 4].view(torch.float32)
-            N.check(L_.abcd_fill_normal(N.ptr(eps), L * F, eseed, eoff, N.c_void_p(side.cuda_stream)),
-                    "decoder noise")
         # the Dirichlet prior's per-category terms depend on the parameters
-        # only: one small kernel on the side stream now instead of in every
-        # sampler-head tile on the sampler's chain (abcd_sampler_prior)
+        # only: one small kernel on the side stream now, beside the input pack,
+        # instead of in every sampler-head tile on the sampler's chain
+        # (abcd_sampler_prior).  (Queued behind a noise fill it was dispatched
+        # once the input projection held every CU -- that GEMM leaves no
+        # registers for another workgroup -- and ran only as the projection
+        # retired, beside the encoder's persistent launch.)
         prior = not self.plain
         if prior:
             N.check(L_.abcd_sampler_prior(self.samp_cfg, self.samp_p, B, float(entire_data_size), N.ptr(ws_s),
                                           ws_s.numel(), N.c_void_p(side.cuda_stream)), "sampler prior")
+        # Philox mode (eps None): eps[row, f] = philox_normal(eseed, eoff + row * F + f),
+        # drawn inside the decoder's persistent launch by its members without
+        # an emit tile (a side-stream fill here ran beside the input projection:
+        # that GEMM holds every CU, so the fill was squeezed into its tail and
+        # overlapped the encoder's persistent launch)
         N.check(L_.abcd_encoder_forward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(h),
                                                 N.ptr(ws_e), ws_e.numel(), st), "encoder forward")
         logits = torch.empty(B, W, device=dev)
@@ -245,17 +249,18 @@ class FusedStep:
             return sc, self._real_logits(logits)
         inv = self._inv_b(Bn)
         d_feats = torch.empty(B, self.Dfeat, device=dev)
-        # the decoder's weight-gradient reductions run on a side stream beside
-        # the sampler + encoder backward (joined below, before clip + SGD):
-        # measured at c2 ~0.5 ms/step shorter than serial (DESIGN.md §3 Streams)
-        # (the side work waits on the device until the encoder BPTT queued below
-        # is resident on every CU: abcd_side_gate_enable, read at this call)
+        # the decoder's data-gradient path now; its weight-gradient reductions
+        # (abcd_decoder_backward_params, below) are queued on the side stream
+        # AFTER the encoder backward, to run beside it (joined before clip +
+        # SGD: measured at c2 ~0.5 ms/step shorter than serial, DESIGN.md s3
+        # Streams).  The gate armed here makes them wait, on the device, until
+        # the encoder BPTT is resident on every CU; queuing them after that
+        # launch means a side stream sharing its hardware queue cannot stall it.
+        dargs = (dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off), N.ptr(xmask), N.ptr(inv), N.ptr(inv),
+                 N.ptr(d_feats), self.dec_g, N.ptr(ws_d), ws_d.numel(), st)
         L_.abcd_side_gate_enable(1)
         try:
-            N.check(L_.abcd_decoder_backward_dropout(dcfg, self.dec_p, pk, N.ptr(feats), N.ptr(spk), N.ptr(gt_off),
-                                                     N.ptr(xmask), N.ptr(inv), N.ptr(inv), N.ptr(d_feats),
-                                                     self.dec_g, N.ptr(ws_d), ws_d.numel(), st, side_p),
-                    "decoder backward")
+            N.check(L_.abcd_decoder_backward_dropout(*dargs, N.DEFER_PARAMS), "decoder backward")
         finally:
             L_.abcd_side_gate_enable(0)
         d_h = torch.empty(B, self.E, device=dev)
@@ -268,12 +273,18 @@ class FusedStep:
                                                float(entire_data_size), N.ptr(d_feats), N.ptr(inv), N.ptr(d_h),
                                                self.samp_g, N.ptr(ws_s), ws_s.numel(), st, N.DEFER_PARAMS),
                 "sampler backward")
+        # (the encoder's own side work -- a GRU layer 0's backward-direction
+        # weight gradients, forked after its BPTT -- on a second side stream,
+        # so that the decoder's queued behind it below are not held back)
+        side2 = self._side_stream(1)
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
-                                                 self.enc_g, N.ptr(ws_e), ws_e.numel(), st, side_p),
-                "encoder backward")
+                                                 self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
+                                                 N.c_void_p(side2.cuda_stream)), "encoder backward")
+        N.check(L_.abcd_decoder_backward_params(*dargs, side_p), "decoder weight gradients")
         N.check(L_.abcd_sampler_backward_params(self.samp_cfg, self.samp_p, N.ptr(h), B, self.samp_g, N.ptr(ws_s),
                                                 ws_s.numel(), st, None), "sampler parameter gradients")
         torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.current_stream(dev).wait_stream(side2)
         if self.pad is not None:  # the real positions of the twin's gradients
             torch.index_select(self.kflat.grad, 0, self.pad_index, out=self.flat.grad)
         return sc, self._real_logits(logits)
@@ -304,10 +315,15 @@ class FusedStep:
             return self._padded_feats[:, :self.pad.dims[1].D]
         raise AttributeError(name)
 
-    def _side_stream(self):
-        s = getattr(self, "_side", None)
+    def _side_stream(self, k=0):
+        """Side stream k (0: the step's side work, 1: the encoder backward's),
+        one per device for the whole process: FusedSteps built one after the
+        other reuse them instead of drawing new streams from torch's pool."""
+        d = torch.device(self.device)
+        key = (d.index if d.index is not None else torch.cuda.current_device(), k)
+        s = _SIDE_STREAMS.get(key)
         if s is None:
-            s = self._side = torch.cuda.Stream(self.device)
+            s = _SIDE_STREAMS[key] = torch.cuda.Stream(self.device)
         return s
 
     def optimizer_step(self, lr, momentum=0.0, clip=1.0):
