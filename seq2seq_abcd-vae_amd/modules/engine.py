@@ -204,9 +204,10 @@ class FusedStep:
                                           ws_s.numel(), N.c_void_p(side.cuda_stream)), "sampler prior")
         # Philox mode (eps None): eps[row, f] = philox_normal(eseed, eoff + row * F + f),
         # drawn inside the decoder's persistent launch by its members without
-        # an emit tile (a side-stream fill here ran beside the input projection:
-        # that GEMM holds every CU, so the fill was squeezed into its tail and
-        # overlapped the encoder's persistent launch)
+        # an emit tile.  A side-stream fill here ran beside the input
+        # projection (that GEMM holds every CU, so the fill was squeezed into
+        # its tail, beside the encoder's persistent launch): same-box A/B at
+        # c2, step 8.46 / 8.48 -> 8.39 / 8.43 ms, dec_fwd 2.24-2.25 -> 2.20 ms
         N.check(L_.abcd_encoder_forward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(h),
                                                 N.ptr(ws_e), ws_e.numel(), st), "encoder forward")
         logits = torch.empty(B, W, device=dev)
