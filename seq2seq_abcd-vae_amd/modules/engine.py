@@ -276,16 +276,20 @@ class FusedStep:
                 "sampler backward")
         # (the encoder's own side work -- a GRU layer 0's backward-direction
         # weight gradients, forked after its BPTT -- on a second side stream,
-        # so that the decoder's queued behind it below are not held back)
-        side2 = self._side_stream(1)
+        # so that the decoder's queued behind it below are not held back; the
+        # LSTM's one-launch gemm_wg3b needs none, and an unused stream's join
+        # would still cost a ~6 us barrier on the main stream)
+        side2 = self._side_stream(1) if self.enc_cfg.rnn_type != N.LSTM else None
         N.check(L_.abcd_encoder_backward_dropout(self.enc_cfg, self.enc_p, pk, N.ptr_array(enc_noise), N.ptr(d_h),
                                                  self.enc_g, N.ptr(ws_e), ws_e.numel(), st,
-                                                 N.c_void_p(side2.cuda_stream)), "encoder backward")
+                                                 N.c_void_p(side2.cuda_stream) if side2 is not None else None),
+                "encoder backward")
         N.check(L_.abcd_decoder_backward_params(*dargs, side_p), "decoder weight gradients")
         N.check(L_.abcd_sampler_backward_params(self.samp_cfg, self.samp_p, N.ptr(h), B, self.samp_g, N.ptr(ws_s),
                                                 ws_s.numel(), st, None), "sampler parameter gradients")
         torch.cuda.current_stream(dev).wait_stream(side)
-        torch.cuda.current_stream(dev).wait_stream(side2)
+        if side2 is not None:
+            torch.cuda.current_stream(dev).wait_stream(side2)
         if self.pad is not None:  # the real positions of the twin's gradients
             torch.index_select(self.kflat.grad, 0, self.pad_index, out=self.flat.grad)
         return sc, self._real_logits(logits)
