@@ -20,6 +20,7 @@ if [ "$PART" = "1" ]; then
   done
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_c2.json 2> $OUT/prof_c2.err
   python scripts/step_timeline.py $(find $OUT/prof_c2 -name "run_kernel_trace.csv" | head -1) > $OUT/step_timeline_c2.txt
+  python scripts/queue_gaps.py $(find $OUT/prof_c2 -name "run_kernel_trace.csv" | head -1) > $OUT/queue_gaps_c2.txt
   echo "part 1 done"
 else
   # PMC: HBM traffic (FETCH_SIZE / WRITE_SIZE, separate passes) and MFMA utilisation, per config
