@@ -1567,7 +1567,7 @@ DEV void sum_partials(__amdgpu_buffer_rsrc_t rs, uint32_t base, f4& acc, int rot
 //   P0  (18 units = 2 row blocks x 9 column tiles, one wave each): sum the 16
 //       dx partials of the tile -> dMU, dLV (+ the emission NLL terms)
 //   P1  wave (rb, jj): the member's dZ column tile 2 mem + jj of row block rb
-//       (fp32 MFMA, K = Fp); then every wave: its 8 dh partial tiles
+//       (x6, K = Fp); then every wave: its 8 dh partial tiles
 //       = dG_{t+1}[:, own 64] W_hh[own 64, its 64 units]   (x6, before the wait)
 //       + dZ_t[:, own 32]   W1cat[own 32, its 64 units]   (x6)
 //  P2  waves (rb, half) sum 8 of the 16 dh partials of the member's 16
@@ -1582,9 +1582,11 @@ constexpr int W16_ROWS = 32;    // rows per group
 constexpr int W16_M = 16;       // members per group (16 units each)
 constexpr int W16_DTP = 68;     // pitch (floats) of the group's 32 x 64 dG tile in LDS
 constexpr int W16_ZTP = 36;     // pitch of the 32 x 32 dZ tile
-// The P1 dZ product runs on waves 0 / 1 only (row block w, both of the
-// member's dZ column tiles, x6 over K = Fp in ceil(Fp / 32) chunks), so each
-// row block's dMU / dLV rows are loaded once per member.
+// The P1 dZ product (x6 over K = Fp in ceil(Fp / 32) chunks) runs on all four
+// waves, one (row block, dZ column tile) each: a row block's dMU / dLV rows
+// are loaded by two waves (the second mostly from L2), for half the MFMAs per
+// wave on the critical path.  Same-box A/B (round 6) against waves 0 / 1 each
+// running both tiles of one row block: dec_bwd 2.29 vs 2.32 ms (3 pairs).
 // GRU: the member's gate columns are dec_fwd_x6's [r | z | n_x | n_h]
 // (dG = [dr, dz, dn, dn r] pre-activation gradients), the split-K images take
 // the n_x column from W_ih only and n_h from W_hh only, the carry is dh z, and
@@ -1769,35 +1771,32 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
     PSTAMP(6);
 #endif
     // ---------------- P1: dZ tile -> this member's dh partials ----------------
-    float zpre[2][4];  // the activations of both tiles of row block w (waves 0 / 1)
+    // the dZ product on all four waves: wave w -> row block w & 1, the
+    // member's dZ column tile w >> 1 (the two waves of a row block load the
+    // same dMU / dLV rows; the second one's mostly from this XCD's L2)
+    const int zrb = w & 1, zjj = w >> 1;
+    float zpre[4];  // the activations of this wave's tile
     {
-      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, w >= 2 ? 0u : (uint32_t)bs * 2 * Hm * 4u);
-      const int zr0 = rowg + 16 * w;
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.Aact + (size_t)o * 2 * Hm, (uint32_t)bs * 2 * Hm * 4u);
+      const int zr0 = rowg + 16 * zrb;
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          zpre[jj][g] = bld(rz, ((uint32_t)(zr0 + 4 * q + g) * 2 * Hm + 32 * mem + 16 * jj + r) * 4u);
+      for (int g = 0; g < 4; ++g)
+        zpre[g] = bld(rz, ((uint32_t)(zr0 + 4 * q + g) * 2 * Hm + 32 * mem + 16 * zjj + r) * 4u);
     }
     gs.wait(3u * i + 1);
-    pin(zpre[0]), pin(zpre[1]);
+    pin(zpre);
     PSTAMP(2);
-    if (w < 2) {
-      const int zr0 = rowg + 16 * w;
-      f4 acc[2] = {f4zero(), f4zero()};
+    {
+      const int zr0 = rowg + 16 * zrb;
+      f4 acc[1] = {f4zero()};
       if (zr0 < bs) {
         const __amdgpu_buffer_rsrc_t ra = make_rsrc((ismu ? a.dMU : a.dLV) + (size_t)o * Fp, (uint32_t)bs * Fp * 4u);
         const BufKC2x A{ra, ra, (uint32_t)Fp * 4u, (uint32_t)Fp * 4u, ncz, Fp};  // k >= Fp reads 0
-        wave_mma_x6<2, NCZ, 4>(acc, A, zr0 + r, B1, ncz, lane, q);
+        wave_mma_x6<1, NCZ, 4>(acc, A, zr0 + r, B1 + zjj * ncz * 3 * 64, ncz, lane, q);
       }
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        float dz[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) dz[g] = acc[jj][g] * (1.f - zpre[jj][g] * zpre[jj][g]);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) ZT[(16 * w + 4 * q + g) * W16_ZTP + 16 * jj + r] = dz[g];
-      }
+      for (int g = 0; g < 4; ++g)
+        ZT[(16 * zrb + 4 * q + g) * W16_ZTP + 16 * zjj + r] = acc[0][g] * (1.f - zpre[g] * zpre[g]);
     }
 #ifdef ABCD_STAMP_DIAG
     PSTAMP(6);  // diagnostics build: dZ tile done (before the barrier)
