@@ -100,6 +100,11 @@ struct PDecBwdArgs {
   float *dG, *dMU, *dLV, *dZ, *DHR, *DC0;
   float* dGH;                      // GRU: the recurrent-side gate gradients (dG holds the input side)
   float* part;  // split-K partials (dec_bwd_w16): 2 parity slots x 32-row groups x (Fp+H)/16 subtiles x 2 row blocks x 16 producers x 256
+  // dhid (dec_bwd_w16; null: not formed): the gradient of feature2hidden's
+  // output, [dh_{-1} | dc_{-1}] interleaved per unit (LSTM, B x 2H) or
+  // dh_{-1} + the carry (GRU, B x H), with dh_{-1} = dG_0 W_hh summed over the
+  // members by one more split-K hand-off after the time loop
+  float* dhid;
 };
 inline size_t dec_part_floats(int B, int H, int Fp) {
   return 2 * (size_t)cdiv(B, 64) * (size_t)((Fp + H) / 16) * 4 * (size_t)(H / 8) * 256;
@@ -134,6 +139,8 @@ int persist_encoder_fwd(hipStream_t s, int G, const PFwdArgs& a, bool* launched)
 int persist_encoder_bwd(hipStream_t s, int G, const PBwdArgs& a, bool* launched);
 int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launched);
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched);
+// true if the last persist_decoder_bwd of this thread wrote a.dhid
+bool dec_bwd_dhid_done();
 
 // ABCD_PERSIST=0 disables the persistent path (parity/timing comparisons).
 bool persist_enabled();

@@ -1952,6 +1952,54 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
       }
     }
   }
+  // ---------------- dh_{-1} = dG_0 W_hh -> dhid (feature2hidden's output gradient) ----------------
+  // one more split-K round after the loop: every member's partial of dG_0[:,
+  // own 64] W_hh[own 64, all units] (DT still holds dG_0) into the next
+  // parity slot (its last readers, step T - 1's P0, are all past), a hand-off,
+  // and the member's 16 units summed over the 16 producers: the three launches
+  // after the kernel (dH0 GEMM, its slab reduction, the dhid assembly) go away
+  if (a.dhid) {
+    const __amdgpu_buffer_rsrc_t pw = (T & 1) ? pr1 : pr0;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      if (rowg + 16 * rb >= a.B) continue;  // uniform
+      f4 h0[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float* ar = DT + (16 * rb + r) * W16_DTP + 32 * c + 8 * q;
+        bf8 a0, a1, a2;
+        split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h0[j] = mma_x6(h0[j], a0, a1, a2, Bh[j][c][0], Bh[j][c][1], Bh[j][c][2]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, h0[j]), pw,
+                                               hblk(4 * w + j, rb) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+    }
+    gs.publish();
+    gs.wait(3u * T + 1);
+    f4 dhr = f4zero();
+    if (crow0 < a.B)
+      sum_partials<M / 2>(pw, hblk(mem, crb) + (uint32_t)(8 * (w >> 1)) * 1024u + (uint32_t)lane * 16u, dhr,
+                          mem % (M / 2));
+    if (!cellw) DHX[crb * 64 + lane] = dhr;
+    __syncthreads();
+    if (cellw) {
+      dhr += DHX[crb * 64 + lane];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = crow0 + 4 * q + g;
+        if (b >= a.B) continue;
+        if constexpr (GRU) {
+          a.dhid[(long)b * H + unit] = dhr[g] + carry[g];  // carry = dh_0 z at t = 0
+        } else {
+          a.dhid[(long)b * 2 * H + 2 * unit] = dhr[g];
+          a.dhid[(long)b * 2 * H + 2 * unit + 1] = carry[g];  // carry = dc_0 f at t = 0
+        }
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2688,6 +2736,9 @@ int persist_decoder_fwd(hipStream_t s, int G, const PDecFwdArgs& a, bool* launch
 }
 
 
+// whether the last persistent decoder BPTT of this thread wrote PDecBwdArgs::dhid
+thread_local bool tl_dec_bwd_dhid = false;
+bool dec_bwd_dhid_done() { return tl_dec_bwd_dhid; }
 // dec_bwd_w16 (32-row groups of 16 members: half the split-K exchange of the
 // 64-row dec_bwd_fold it replaced): same-box A/B at c2, dec_bwd 3.08 / 3.06 ->
 // 2.55 / 2.55 ms per launch, step 9.99 / 9.99 -> 9.49 / 9.47 ms
@@ -2712,6 +2763,7 @@ static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launche
     dec_bwd_w16<NXS, GRU><<<grid, 256, lds, s>>>(b);
   }
   note_dispatch(TK_DEC_BWD, "dec_bwd_w16<%d,%s> grid %d", NXS, GRU ? "GRU" : "LSTM", grid);
+  tl_dec_bwd_dhid = b.dhid != nullptr;
   ABCD_CHECK_LAUNCH();
   *launched = true;
   return 0;
@@ -2719,6 +2771,7 @@ static int launch_dec_bwd_w16(hipStream_t s, const PDecBwdArgs& a, bool* launche
 
 int persist_decoder_bwd(hipStream_t s, int G, const PDecBwdArgs& a, bool* launched) {
   *launched = false;
+  tl_dec_bwd_dhid = false;
   if (!persist_enabled() || a.H % 8) return 0;
   // the split-K form: H = Hm = 256, Fp / 16 <= 16 (the GRU has no other persistent form)
   if (a.part && x6_enabled(a.H) && a.H == 256 && a.Hm == a.H && a.Fp / 16 <= a.H / 8 &&

@@ -1402,7 +1402,7 @@ static int dec_bwd_impl(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
                               ACT_NONE, sc, scf));
   }
   // ---- BPTT: one persistent launch, or three launches per step ----
-  bool done = false;
+  bool done = false, dhid_done = false;
   {
     PDecBwdArgs pa{};
     pa.H = H; pa.Hm = Hm; pa.F = F; pa.Fp = Fp; pa.T = T; pa.nrt = cdiv(B, PERSIST_ROWS); pa.B = B;
@@ -1414,8 +1414,10 @@ static int dec_bwd_impl(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
     pa.dG = w.dGX; pa.dMU = w.dMU; pa.dLV = w.dLV; pa.dZ = w.dZ; pa.DHR = w.DC; pa.DC0 = w.DC0;
     pa.Hprev = w.Hprev; pa.dGH = w.dGH;
     pa.part = w.skp;
+    pa.dhid = w.dhid;  // dec_bwd_w16 forms it in-kernel (dec_bwd_dhid_done)
     if (persist_enabled()) ABCD_TRY((hipError_t)stage_offsets(s, off, w.off));
     ABCD_TRY((hipError_t)persist_decoder_bwd(s, G, pa, &done));
+    dhid_done = done && dec_bwd_dhid_done();
     ABCD_TRY((hipError_t)flush_offsets());
   }
   const int TN = bwd_tn(H);
@@ -1457,10 +1459,12 @@ static int dec_bwd_impl(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
     else ABCD_TRY((hipError_t)launch_bwd_step<3>(s, a, bd.tiles, H));
   }
   // ---- initial state gradient -> feature2hidden -> features / speaker embedding ----
-  ABCD_TRY((hipError_t)gemm(s, B, H, GH, opKC(w.dGH, GH, B), opKC(w.WhhT, GH, H), w.dH0, H, 1.f, 0.f, nullptr,
-                            ACT_NONE, sc, scf));
-  dec_hidden_init_bwd<<<launch_grid((long)B * H), 256, 0, s>>>(w.dH0, w.DC0, B, H, G == 4, w.dhid);
-  ABCD_CHECK_LAUNCH();
+  if (!dhid_done) {
+    ABCD_TRY((hipError_t)gemm(s, B, H, GH, opKC(w.dGH, GH, B), opKC(w.WhhT, GH, H), w.dH0, H, 1.f, 0.f, nullptr,
+                              ACT_NONE, sc, scf));
+    dec_hidden_init_bwd<<<launch_grid((long)B * H), 256, 0, s>>>(w.dH0, w.DC0, B, H, G == 4, w.dhid);
+    ABCD_CHECK_LAUNCH();
+  }
   ABCD_TRY((hipError_t)gemm(s, B, DS, Htot, opKC(w.dhid, Htot, B), opKC(w.Wf2hT, Htot, DS), w.dFS, DS, 1.f, 0.f,
                             nullptr, ACT_NONE, sc, scf));
   dec_feats_bwd<<<launch_grid((long)B * std::max(D, 1)), 256, 0, s>>>(w.dFS, D, S, B, speakers, c->num_speakers,
