@@ -1465,11 +1465,17 @@ static int dec_bwd_impl(const abcd_decoder_cfg* c, const abcd_decoder_params* p,
     dec_hidden_init_bwd<<<launch_grid((long)B * H), 256, 0, s>>>(w.dH0, w.DC0, B, H, G == 4, w.dhid);
     ABCD_CHECK_LAUNCH();
   }
-  ABCD_TRY((hipError_t)gemm(s, B, DS, Htot, opKC(w.dhid, Htot, B), opKC(w.Wf2hT, Htot, DS), w.dFS, DS, 1.f, 0.f,
-                            nullptr, ACT_NONE, sc, scf));
-  dec_feats_bwd<<<launch_grid((long)B * std::max(D, 1)), 256, 0, s>>>(w.dFS, D, S, B, speakers, c->num_speakers,
-                                                                     d_features, S > 0 ? g->embed_speaker : nullptr);
-  ABCD_CHECK_LAUNCH();
+  if (S == 0) {  // no speaker columns: the GEMM writes d_features itself (the split kernel was a copy)
+    if (d_features)
+      ABCD_TRY((hipError_t)gemm(s, B, D, Htot, opKC(w.dhid, Htot, B), opKC(w.Wf2hT, Htot, DS), d_features, D, 1.f,
+                                0.f, nullptr, ACT_NONE, sc, scf));
+  } else {
+    ABCD_TRY((hipError_t)gemm(s, B, DS, Htot, opKC(w.dhid, Htot, B), opKC(w.Wf2hT, Htot, DS), w.dFS, DS, 1.f, 0.f,
+                              nullptr, ACT_NONE, sc, scf));
+    dec_feats_bwd<<<launch_grid((long)B * std::max(D, 1)), 256, 0, s>>>(w.dFS, D, S, B, speakers, c->num_speakers,
+                                                                       d_features, g->embed_speaker);
+    ABCD_CHECK_LAUNCH();
+  }
   }
   if (!(mode & DEC_WGRAD)) {  // deferred: mark the end of the data path for abcd_decoder_backward_params
     hipEvent_t ev;
