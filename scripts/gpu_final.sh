@@ -33,6 +33,7 @@ else
     echo "pmc $c done"
   done
   timeout -k 10 240 python -u scripts/persist_stamps.py > $OUT/persist_phase_stamps.log 2>&1
+  timeout -k 10 240 python -u scripts/persist_stamps.py c5 > $OUT/persist_phase_stamps_c5.log 2>&1
   timeout -k 10 300 python -u scripts/contention_probe.py > $OUT/contention_probe.log 2>&1
   echo "part 2 done"
 fi

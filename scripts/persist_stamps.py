@@ -6,7 +6,7 @@ kernel at a time (abcd_debug_persist_prof), and prints, per kernel, the median
 over workgroups of each phase's cycles averaged over the time steps, plus
 the kernel's event-timed duration (to convert cycles to microseconds).
 
-    python scripts/persist_stamps.py
+    python scripts/persist_stamps.py [config]      (default c2; e.g. c5)
 """
 import ctypes
 import os
@@ -31,7 +31,7 @@ def main():
     lib = N.lib()
     lib.abcd_debug_persist_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.abcd_debug_persist_prof.restype = None
-    cfg = bench.CONFIGS["c2"]
+    cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
     dev = torch.device("cuda", 0)
     noise.set_mode("philox")
     noise.manual_seed(1234)
