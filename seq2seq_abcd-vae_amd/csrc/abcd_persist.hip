@@ -1676,10 +1676,16 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
   auto hblk = [&](int s, int rb) {
     return (uint32_t)(((size_t)ng * NXS * 2 * M + (((size_t)grp * NHS + s) * 2 + rb) * M)) * 1024u;
   };
-  // P0 unit of this wave: k = 16 w + mem < 2 nFt -> (row block k / nFt, column tile k % nFt)
-  const int pk = M * w + mem;
+  // P0 unit of this wave: k = 16 w + mem < 2 nFt.  The 2 (nFt - 1) full
+  // column tiles come first (k -> row block k / (nFt - 1), tile k % (nFt - 1)),
+  // the last tile of each row block last: at F = 129 that tile holds ONE real
+  // column, so its lanes with col >= F gather nothing (out-of-range offsets) and
+  // the two members that carry a second unit (k = 16, 17 on wave 1) carry a
+  // 1-KiB gather instead of a 16-KiB one
+  const int pk = M * w + mem, nfull = nFt - 1;
   const bool p0 = pk < 2 * nFt;
-  const int prb = p0 ? pk / nFt : 0, jx = p0 ? pk % nFt : 0;
+  const int prb = !p0 ? 0 : pk < 2 * nfull ? pk / nfull : pk - 2 * nfull;
+  const int jx = !p0 ? 0 : pk < 2 * nfull ? pk % nfull : nfull;
   const int prow0 = rowg + 16 * prb;
   // P1 dZ unit of this wave: row block w >> 1, column tile 2 mem + (w & 1)
   // P2: dh half-sum of row block w & 1 over producers 8 (w >> 1) .. + 7; waves 0 / 1 run the cell
@@ -1726,7 +1732,8 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
     PSTAMP(0);
     if (p0) {
       f4 dx = f4zero();
-      if (NXS > 0 && i > 0 && prow0 < succ_valid) sum_partials<M>(prd, xblk(jx, prb) + (uint32_t)lane * 16u, dx, mem % M);
+      if (NXS > 0 && i > 0 && prow0 < succ_valid)  // (lanes of padding columns: out-of-range offsets, no traffic)
+        sum_partials<M>(prd, col0 < F ? xblk(jx, prb) + (uint32_t)lane * 16u : 0x80000000u, dx, mem % M);
       float dmu[4], dlv[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1753,18 +1760,36 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
     f4 hx[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) hx[j][0] = hx[j][1] = f4zero();
-    if (dgv) {
+    // blocks k = (row block k >> 1, chunk k & 1) of rows with a successor
+    // (rows without one have no dG_{t+1}); block k + 1's split runs between
+    // block k's 24 MFMAs (as wave_mma_x6p)
+    {
+      const int nblk = !dgv ? 0 : rowg + 16 < succ_valid ? 4 : rowg < succ_valid ? 2 : 0;  // uniform
+      auto dt_split = [&](int k, bf8 (&v)[3]) {
+        const float* ar = DT + (16 * (k >> 1) + r) * W16_DTP + 32 * (k & 1) + 8 * q;
+        split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), v[0], v[1], v[2]);
+      };
+      bf8 av[3];
+      if (nblk) dt_split(0, av);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        if (rowg + 16 * rb >= succ_valid) continue;  // uniform: rows without a successor have no dG_{t+1}
+      for (int k = 0; k < 4; ++k) {
+        if (k >= nblk) break;
+        bf8 nv[3];
+        if (k + 1 < 4) dt_split(k + 1, nv);  // (block 2 of a one-row-block step: unused)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const float* ar = DT + (16 * rb + r) * W16_DTP + 32 * c + 8 * q;
-          bf8 a0, a1, a2;
-          split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), a0, a1, a2);
+        for (int j = 0; j < 4; ++j)
+          hx[j][k >> 1] = mma_x6(hx[j][k >> 1], av[0], av[1], av[2], Bh[j][k & 1][0], Bh[j][k & 1][1], Bh[j][k & 1][2]);
+        if (k + 1 < 4) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) hx[j][rb] = mma_x6(hx[j][rb], a0, a1, a2, Bh[j][c][0], Bh[j][c][1], Bh[j][c][2]);
+          for (int m = 0; m < 24; ++m) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
         }
+        __builtin_amdgcn_sched_barrier(0);
+        if (k + 1 < 4) av[0] = nv[0], av[1] = nv[1], av[2] = nv[2];
       }
     }
 #ifndef ABCD_STAMP_DIAG
@@ -1802,19 +1827,39 @@ __global__ __launch_bounds__(256) void dec_bwd_w16(PDecBwdArgs a) {
     PSTAMP(6);  // diagnostics build: dZ tile done (before the barrier)
 #endif
     __syncthreads();  // the member's 32 x 32 dZ tile is in LDS
+    {  // row block 1's split between row block 0's 24 MFMAs
+      const int nrb = rowg + 16 < bs ? 2 : rowg < bs ? 1 : 0;  // uniform
+      auto zt_split = [&](int rb, bf8 (&v)[3]) {
+        const float* ar = ZT + (16 * rb + r) * W16_ZTP + 8 * q;
+        split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), v[0], v[1], v[2]);
+      };
+      bf8 zv[3];
+      if (nrb) zt_split(0, zv);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      if (rowg + 16 * rb >= bs) continue;  // uniform
-      const float* ar = ZT + (16 * rb + r) * W16_ZTP + 8 * q;
-      bf8 z0, z1, z2;
-      split8(*reinterpret_cast<const f4*>(ar), *reinterpret_cast<const f4*>(ar + 4), z0, z1, z2);
+      for (int rb = 0; rb < 2; ++rb) {
+        if (rb >= nrb) break;
+        bf8 nv[3];
+        if (rb == 0) zt_split(1, nv);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f4* bp = W1X + ((4 * w + j) * 3) * 64 + lane;
-        const f4 v = mma_x6(hx[j][rb], z0, z1, z2, __builtin_bit_cast(bf8, bp[0]), __builtin_bit_cast(bf8, bp[64]),
-                            __builtin_bit_cast(bf8, bp[128]));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
-                                               hblk(4 * w + j, rb) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0, 16);
+        for (int j = 0; j < 4; ++j) {
+          const f4* bp = W1X + ((4 * w + j) * 3) * 64 + lane;
+          const f4 v = mma_x6(hx[j][rb], zv[0], zv[1], zv[2], __builtin_bit_cast(bf8, bp[0]),
+                              __builtin_bit_cast(bf8, bp[64]), __builtin_bit_cast(bf8, bp[128]));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), pw,
+                                                 hblk(4 * w + j, rb) + (uint32_t)mem * 1024u + (uint32_t)lane * 16u, 0,
+                                                 16);
+        }
+        if (rb == 0) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+          for (int m = 0; m < 24; ++m) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (rb == 0) zv[0] = nv[0], zv[1] = nv[1], zv[2] = nv[2];
       }
     }
 #ifdef ABCD_STAMP_DIAG

@@ -164,67 +164,22 @@ DEV void stage_x6(f4* dst, const float* W, long ldw, int kvalid, int nsub, int n
 // trip count made the compiler rotate the ring with moves that waited for
 // every load).  A supplies frag8(row, c, q, lo, hi) (k = 32c + 8q + 0..7 as
 // two float4).  PD chunks of raw fp32 stay in flight; each is split in
-// registers right before its chunk's 6 x NR MFMAs (the persistent kernels
+// registers during the previous chunk's 6 x NR MFMAs (the persistent kernels
 // use PD = 4: same-box A/B at c2 against PD = 8, enc_fwd 1.35 -> 1.23 ms,
 // dec_fwd 2.51 -> 2.36 ms, dec_bwd 4.22 -> 4.17 ms; PD = 2 no better).
-// Bl: the chunk-major x6
-// image with `nch` chunks per subtile (nch >= NCH; a segment of a wider image
-// starts at Bl + c0 * 3 * 64).
+// wave_mma_x6p: one image segment per output tile, chunk c of tile j at
+// Bp[j] + c * 3 * 64 (tiles from different LDS images sharing one A operand);
+// wave_mma_x6 (below): the chunk-major image Bl with `nch` chunks per subtile
+// (nch >= NCH; a segment of a wider image starts at Bl + c0 * 3 * 64).
+// NR >= 4 (the encoder forward's four gate tiles): software-pipelined by one
+// chunk (round 6) -- chunk c + 1's split (~36 dependent VALU) and its
+// B-fragment LDS reads are interleaved with chunk c's 6 NR MFMAs instead of
+// sitting between two MFMA runs, where the matrix pipe idled ~150 cycles per
+// chunk (enc_fwd: 8 x 150 of its ~3070 MFMA cycles per step).  Same products
+// in the same order: bit-identical results.
 template <int NR, int NCH, int PD, class OA>
-DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q, int rot = 0) {
-  constexpr int P = PD < NCH ? PD : NCH;
-  // chunk order rotated by `rot` (wave-uniform, < NCH): consumers of one
-  // hand-off tile start on different lines instead of all on chunk 0.  The
-  // decoder kernels pass the member index (same-box A/B at c2 against the
-  // constant-0 form: dec_fwd_x6 2.63 -> 2.50 ms, dec_bwd_sk 4.37 -> 4.19 ms);
-  // enc_fwd_persist keeps rot = 0 (1.34 vs 1.37 ms rotated)
-  auto cc = [&](int c) { const int x = c + rot; return x >= NCH ? x - NCH : x; };
-  f4 ra[P], rb[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) A.frag8(arow, cc(p), q, ra[p], rb[p]);
-  // B fragments double-buffered: chunk c + 1's LDS reads are issued before
-  // chunk c's MFMAs so their latency hides behind them
-  f4 bw[NR][3];
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bl[((j * nch + cc(0)) * 3 + pl) * 64 + lane];
-  // pin the whole ring's loads here (the scheduler would sink each next to
-  // its use) and keep each chunk's split + refill ahead of its MFMAs
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int p = c % P;
-    f4 bn[NR][3];
-    if (c + 1 < NCH) {
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bl[((j * nch + cc(c + 1)) * 3 + pl) * 64 + lane];
-    }
-    bf8 a0, a1, a2;
-    split8(ra[p], rb[p], a0, a1, a2);
-    if (c + P < NCH) A.frag8(arow, cc(c + P), q, ra[p], rb[p]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-      acc[j] = mma_x6(acc[j], a0, a1, a2, __builtin_bit_cast(bf8, bw[j][0]), __builtin_bit_cast(bf8, bw[j][1]),
-                      __builtin_bit_cast(bf8, bw[j][2]));
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < NCH) {
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bw[j][pl] = bn[j][pl];
-    }
-  }
-}
-
-// wave_mma_x6 with one image segment per output tile: chunk c of tile j at
-// Bp[j] + c * 3 * 64 (tiles from different LDS images sharing one A operand)
-template <int NR, int NCH, int PD, class OA>
-DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp)[NR], int lane, int q,
-                      int rot = 0) {
+DEV void wave_mma_x6p_pipe(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp)[NR], int lane, int q,
+                           int rot) {
   constexpr int P = PD < NCH ? PD : NCH;
   auto cc = [&](int c) { const int x = c + rot; return x >= NCH ? x - NCH : x; };
   f4 ra[P], rb[P];
@@ -235,6 +190,68 @@ DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp
   for (int j = 0; j < NR; ++j)
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bp[j][(cc(0) * 3 + pl) * 64 + lane];
+  __builtin_amdgcn_sched_barrier(0);
+  bf8 a0, a1, a2;
+  split8(ra[0], rb[0], a0, a1, a2);
+  if (P < NCH) A.frag8(arow, cc(P), q, ra[0], rb[0]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    f4 bn[NR][3];
+    bf8 n0, n1, n2;
+    if (c + 1 < NCH) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bn[j][pl] = Bp[j][(cc(c + 1) * 3 + pl) * 64 + lane];
+      const int p1 = (c + 1) % P;
+      split8(ra[p1], rb[p1], n0, n1, n2);
+      if (c + 1 + P < NCH) A.frag8(arow, cc(c + 1 + P), q, ra[p1], rb[p1]);
+    }
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      acc[j] = mma_x6(acc[j], a0, a1, a2, __builtin_bit_cast(bf8, bw[j][0]), __builtin_bit_cast(bf8, bw[j][1]),
+                      __builtin_bit_cast(bf8, bw[j][2]));
+    if (c + 1 < NCH) {
+      // the next chunk's B reads first, then MFMAs with the split's VALU between them
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * NR, 0);
+#pragma unroll
+      for (int k = 0; k < 6 * NR; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, (40 + 6 * NR - 1) / (6 * NR), 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < NCH) {
+      a0 = n0, a1 = n1, a2 = n2;
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bw[j][pl] = bn[j][pl];
+    }
+  }
+}
+
+// the same with each chunk split right before its own MFMAs (NR < 4: with
+// 6 or 12 MFMAs per chunk the split's dependent VALU chain outlasts them, and
+// the interleaved form measured no faster in the decoder kernels)
+template <int NR, int NCH, int PD, class OA>
+DEV void wave_mma_x6p_serial(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp)[NR], int lane, int q,
+                             int rot) {
+  constexpr int P = PD < NCH ? PD : NCH;
+  auto cc = [&](int c) { const int x = c + rot; return x >= NCH ? x - NCH : x; };
+  f4 ra[P], rb[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) A.frag8(arow, cc(p), q, ra[p], rb[p]);
+  // B fragments double-buffered: chunk c + 1's LDS reads are issued before
+  // chunk c's MFMAs so their latency hides behind them
+  f4 bw[NR][3];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) bw[j][pl] = Bp[j][(cc(0) * 3 + pl) * 64 + lane];
+  // pin the whole ring's loads here (the scheduler would sink each next to
+  // its use) and keep each chunk's split + refill ahead of its MFMAs
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -262,6 +279,21 @@ DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp
         for (int pl = 0; pl < 3; ++pl) bw[j][pl] = bn[j][pl];
     }
   }
+}
+
+template <int NR, int NCH, int PD, class OA>
+DEV void wave_mma_x6p(f4 (&acc)[NR], const OA& A, int arow, const f4* const (&Bp)[NR], int lane, int q,
+                      int rot = 0) {
+  if constexpr (NR >= 4) wave_mma_x6p_pipe<NR, NCH, PD>(acc, A, arow, Bp, lane, q, rot);
+  else wave_mma_x6p_serial<NR, NCH, PD>(acc, A, arow, Bp, lane, q, rot);
+}
+
+template <int NR, int NCH, int PD, class OA>
+DEV void wave_mma_x6(f4 (&acc)[NR], const OA& A, int arow, const f4* Bl, int nch, int lane, int q, int rot = 0) {
+  const f4* Bp[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) Bp[j] = Bl + (size_t)j * nch * 3 * 64;
+  wave_mma_x6p<NR, NCH, PD>(acc, A, arow, Bp, lane, q, rot);
 }
 
 }  // namespace abcd
