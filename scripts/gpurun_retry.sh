@@ -1,5 +1,5 @@
 #!/bin/bash
-# Local helper: run a gpurun call, re-submitting it (up to 12 tries, 200 s apart: longer than the service back-off)
+# Local helper: run a gpurun call, re-submitting it (up to 12 tries, 60 s apart)
 # only when the service reports an infrastructure transient or no free box --
 # i.e. when NOTHING ran on a GPU.  Any other outcome (pass, fail, fault,
 # timeout) is returned as is and never retried.
@@ -10,7 +10,7 @@ for try in 1 2 3 4 5 6 7 8 9 10 11 12; do
   rc=$?
   if grep -q "status=transient\|has no free box" "$LOG" || [ $rc -eq 3 ]; then
     echo "try $try: transient / no box, retrying" >&2
-    sleep 200
+    sleep 60
     continue
   fi
   exit $rc

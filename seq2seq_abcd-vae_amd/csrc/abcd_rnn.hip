@@ -839,6 +839,92 @@ __global__ void dec_init(const float* Hinit, int B, int H, int lstm, float* Hpre
   }
   for (int i = blockIdx.x * 256 + threadIdx.x; i < B * Fp; i += gridDim.x * 256) Xin[i] = 0.f;
 }
+// feature2hidden (model.py:100,262-263) computed straight into the initial
+// state: dec_init's scatter with the B x Htot product formed in place (fp32
+// FMAs, k ascending, + bias), one launch instead of a split-K GEMM + dec_init
+// on the sampler -> decoder chain.  A workgroup owns a 32 x 32 output tile:
+// its FS rows (32 x DS) and WT columns (WT = f2h_w^T, DS x Htot, the
+// backward's packed transpose) are loaded with every 16-B load in flight at
+// once (NV per thread and operand, DS <= 32 NV), staged in LDS, and each
+// thread forms a 2 x 2 block over all of K.  (One column per thread straight
+// from HBM / L2 ran 121 us at c2: a chain of dependent load latencies.)
+template <int NV>
+__global__ __launch_bounds__(256) void dec_init_f2h(const float* FS, int DS, const float* WT, const float* bias,
+                                                    int B, int H, int lstm, float* Hprev, float* Cprev, float* Xin,
+                                                    int Fp) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int P = DS + 4;  // FS row pitch: 16-B rows, consecutive rows 4 banks apart
+  float* fs = sm;        // 32 x P
+  float* wt = sm + 32 * P;  // DS x 32
+  const int tid = threadIdx.x, Htot = lstm ? 2 * H : H, q = DS / 4;
+  const int j0 = blockIdx.x * 32, b0 = blockIdx.y * 32;
+  f4 a[NV], w[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int e = tid + 256 * v, r = e / q, c = e % q;
+    a[v] = e < 32 * q && b0 + r < B ? *reinterpret_cast<const f4*>(FS + (long)(b0 + r) * DS + 4 * c) : f4zero();
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int e = tid + 256 * v, k = e >> 3, c = e & 7;
+    w[v] = k < DS && j0 + 4 * c < Htot ? *reinterpret_cast<const f4*>(WT + (long)k * Htot + j0 + 4 * c) : f4zero();
+  }
+  if (blockIdx.x == 0)  // Xin rows [b0, b0 + 32) = 0
+    for (int i = tid; i < 32 * Fp; i += 256)
+      if (b0 + i / Fp < B) Xin[(long)b0 * Fp + i] = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int e = tid + 256 * v;
+    if (e < 32 * q) *reinterpret_cast<f4*>(fs + (e / q) * P + 4 * (e % q)) = a[v];
+    if ((e >> 3) < DS) *reinterpret_cast<f4*>(wt + (e >> 3) * 32 + 4 * (e & 7)) = w[v];
+  }
+  __syncthreads();
+  const int r0 = (tid >> 4) * 2, c0 = (tid & 15) * 2;
+  float acc00 = 0.f, acc01 = 0.f, acc10 = 0.f, acc11 = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < DS; ++k) {
+    const float x0 = fs[r0 * P + k], x1 = fs[(r0 + 1) * P + k];
+    const float2 y = *reinterpret_cast<const float2*>(wt + k * 32 + c0);
+    acc00 = fmaf(x0, y.x, acc00);
+    acc01 = fmaf(x0, y.y, acc01);
+    acc10 = fmaf(x1, y.x, acc10);
+    acc11 = fmaf(x1, y.y, acc11);
+  }
+  const float acc[2][2] = {{acc00, acc01}, {acc10, acc11}};
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int j = j0 + c0 + jj;
+    if (j >= Htot) continue;
+    const float bj = bias ? bias[j] : 0.f;
+    const int u = lstm ? j >> 1 : j;
+    float* dst = lstm && (j & 1) ? Cprev : Hprev;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (b0 + r0 + i < B) dst[(long)(b0 + r0 + i) * H + u] = acc[i][jj] + bj;
+  }
+}
+static int dec_init_f2h_launch(hipStream_t s, const float* FS, int DS, const float* WT, const float* bias, int B,
+                               int H, int lstm, float* Hprev, float* Cprev, float* Xin, int Fp) {
+  const int Htot = lstm ? 2 * H : H;
+  if (DS % 4 || Htot % 4 || DS > 512 || (((uintptr_t)FS | (uintptr_t)WT) & 15)) return -1;
+  const size_t lds = ((size_t)32 * (DS + 4) + (size_t)DS * 32) * 4;
+  const dim3 grid(cdiv(Htot, 32), cdiv(B, 32));
+#define ABCD_DEC_INIT(NV)                                                                                 \
+  {                                                                                                       \
+    static bool attr = false;                                                                             \
+    if (!attr) {                                                                                          \
+      ABCD_TRY(hipFuncSetAttribute((const void*)dec_init_f2h<NV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                   160 * 1024));                                                          \
+      attr = true;                                                                                        \
+    }                                                                                                     \
+    dec_init_f2h<NV><<<grid, 256, lds, s>>>(FS, DS, WT, bias, B, H, lstm, Hprev, Cprev, Xin, Fp);         \
+  }
+  if (DS <= 128) ABCD_DEC_INIT(4)
+  else if (DS <= 256) ABCD_DEC_INIT(8)
+  else ABCD_DEC_INIT(16)
+#undef ABCD_DEC_INIT
+  return (int)hipGetLastError();
+}
 // offset head (model.py:121-122,191,195): logit = Zo . w2 + b2 ; BCE-with-logits (sum)
 __global__ void dec_offset_head(const float* Zo, int L, int Hm, const float* w2, const float* b2, const float* tgt,
                                 float* logit, float* dlog_raw, float* bce) {
@@ -1035,6 +1121,11 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
 }
 
 static int launch_grid(long n) { return (int)std::max<long>(1, std::min<long>(4096, cdiv(n, 256))); }
+// ABCD_DEC_INIT_F2H=0: feature2hidden as a GEMM + dec_init (same-box A/B)
+static bool dec_init_fused() {
+  const char* v = getenv("ABCD_DEC_INIT_F2H");
+  return !(v && v[0] == '0');
+}
 static bool dec_eps_fill() {
   const char* v = getenv("ABCD_DEC_EPSFILL");
   return !(v && v[0] == '0');
@@ -1197,9 +1288,16 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
     ABCD_CHECK_LAUNCH();
     FS = w.FS;
   }
-  ABCD_TRY((hipError_t)gemm(s, B, Htot, DS, opKC(FS, DS, B), opKC(p->f2h_w, DS, Htot), w.Hinit, Htot, 1.f, 0.f,
-                            p->f2h_b, ACT_NONE, nullptr, 0));
-  dec_init<<<launch_grid((long)B * std::max(H, Fp)), 256, 0, s>>>(w.Hinit, B, H, G == 4, w.Hprev, w.Cprev, w.Xin, Fp);
+  int rc = -1;
+  if (dec_init_fused())
+    rc = dec_init_f2h_launch(s, FS, DS, w.Wf2hT, p->f2h_b, B, H, G == 4, w.Hprev, w.Cprev, w.Xin, Fp);
+  if (rc > 0) return rc;
+  if (rc < 0) {
+    ABCD_TRY((hipError_t)gemm(s, B, Htot, DS, opKC(FS, DS, B), opKC(p->f2h_w, DS, Htot), w.Hinit, Htot, 1.f, 0.f,
+                              p->f2h_b, ACT_NONE, nullptr, 0));
+    dec_init<<<launch_grid((long)B * std::max(H, Fp)), 256, 0, s>>>(w.Hinit, B, H, G == 4, w.Hprev, w.Cprev, w.Xin,
+                                                                   Fp);
+  }
   ABCD_CHECK_LAUNCH();
   // ---- time loop: one persistent launch, or one launch per phase and step ----
   bool done = false;

@@ -205,3 +205,21 @@ def test_decoder_input_dropout_persist_vs_stepwise(rnn):
         assert abs(sc_p[k] - sc_s[k]) <= 1e-5 * abs(sc_s[k]) + 1e-6, (k, sc_p[k].item(), sc_s[k].item())
     assert _rel(g_p, g_s) < 1e-4
     assert sc_p[0] != sc_0[0] and _rel(g_p, g_0) > 1e-3
+
+
+@pytest.mark.parametrize("cfg_name", ["c2", "c5gru", "odd"])
+def test_fused_decoder_init_vs_gemm(cfg_name):
+    """feature2hidden formed straight into the decoder's initial state
+    (dec_init_f2h, the default) against the split-K GEMM + dec_init scatter
+    (ABCD_DEC_INIT_F2H=0), model.py:100,262-263: the whole training step at
+    c2 (DS = 256, LSTM h / c interleave), c5gru (DS = 512 with the speaker
+    embedding, GRU) and the odd shapes (DS = 32, a ragged 32-column tile)."""
+    import bench
+    cfg = ODD if cfg_name == "odd" else bench.CONFIGS[cfg_name]
+    step = bench.build(cfg, "cuda")
+    batch = bench.make_batch(cfg, 0, "cuda")
+    sc_f, g_f = _with_env("ABCD_DEC_INIT_F2H", "1", lambda: _fused_run(step, batch, True))
+    sc_g, g_g = _with_env("ABCD_DEC_INIT_F2H", "0", lambda: _fused_run(step, batch, True))
+    for k in range(4):
+        assert abs(sc_f[k] - sc_g[k]) <= 1e-5 * abs(sc_g[k]) + 1e-6, (k, sc_f[k].item(), sc_g[k].item())
+    assert _rel(g_f, g_g) < 1e-4
