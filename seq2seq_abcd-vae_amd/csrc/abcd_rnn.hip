@@ -1360,16 +1360,6 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
     dec_emit_fwd<<<cdiv(b_t, 16) * (Fp / 16), 256, 0, s>>>(e);
     ABCD_CHECK_LAUNCH();
   }
-  // ---- loss reductions: only the loss scalars read them, so with a loss
-  // stream sl they run there beside the offset head (w.part is theirs alone)
-  if (losses && x->data) {
-    ABCD_TRY((hipError_t)stream_fork(s, sl, 4));  // MU, LV
-    const int nbk = 1024;
-    dec_emission_nll<<<nbk, 1024, 0, sl>>>(w.MU, w.LV, Fp, x->data, F, L, w.part);  // 16 waves / block
-    ABCD_CHECK_LAUNCH();
-    sum_partials<<<1, 256, 0, sl>>>(w.part, nbk, losses);
-    ABCD_CHECK_LAUNCH();
-  }
   // ---- offset head over all frames (off the recurrent critical path): the
   // logit's dot product folded into the Zo GEMM's epilogue where it applies ----
   bool fused = false;
@@ -1385,10 +1375,21 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
                                                w.dlog_raw, w.bce);
   }
   ABCD_CHECK_LAUNCH();
-  if (losses && gt_offset) {
-    ABCD_TRY((hipError_t)stream_fork(s, sl, 5));  // bce
-    ABCD_TRY((hipError_t)reduce_sum(sl, w.bce, L, w.part + 1024, losses + 1, nullptr));
+  // ---- loss reductions: only the loss scalars read them, so with a loss
+  // stream sl they run there beside the offset head's backward GEMM, behind
+  // ONE fork after the logit pass (MU, LV, bce; w.part is theirs alone).  A
+  // second fork after dec_fwd for the emission NLL alone cost its 6-7 us
+  // event packet on the main queue.
+  const bool em_loss = losses && x->data, off_loss = losses && gt_offset;
+  if (em_loss || off_loss) ABCD_TRY((hipError_t)stream_fork(s, sl, 4));
+  if (em_loss) {
+    const int nbk = 1024;
+    dec_emission_nll<<<nbk, 1024, 0, sl>>>(w.MU, w.LV, Fp, x->data, F, L, w.part);  // 16 waves / block
+    ABCD_CHECK_LAUNCH();
+    sum_partials<<<1, 256, 0, sl>>>(w.part, nbk, losses);
+    ABCD_CHECK_LAUNCH();
   }
+  if (off_loss) ABCD_TRY((hipError_t)reduce_sum(sl, w.bce, L, w.part + 1024, losses + 1, nullptr));
   if (flatten_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.OUT, Fp, flatten_out, F, L); ABCD_CHECK_LAUNCH(); }
   if (mu_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.MU, Fp, mu_out, F, L); ABCD_CHECK_LAUNCH(); }
   if (lv_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.LV, Fp, lv_out, F, L); ABCD_CHECK_LAUNCH(); }
