@@ -962,28 +962,35 @@ __global__ void dec_offset_logit(const float* part, int nsl, int L, const float*
   }
 }
 // emission NLL partial sums: 0.5*(log 2pi + lv + (y-mu)^2 e^{-lv}) over L x F
-__global__ void dec_emission_nll(const float* MU, const float* LV, int Fp, const float* Y, int F, long L,
-                                 double* part) {
-  __shared__ double sh[16];
+constexpr int NLL_ROWS = 16;
+__global__ __launch_bounds__(256) void dec_emission_nll(const float* MU, const float* LV, int Fp, const float* Y,
+                                                        int F, long L, double* part) {
+  // a workgroup owns NLL_ROWS consecutive rows (one wave per NLL_ROWS / 4 of
+  // them: coalesced row reads, every load of a wave in flight together) and
+  // writes one fp64 partial.  Short workgroups: the pass runs on the loss
+  // stream beside the offset head's backward GEMM, and the decoder BPTT
+  // launched behind that GEMM needs one workgroup slot per CU -- it finds them
+  // within one short workgroup's time (1024 grid-striding 16-wave workgroups
+  // held them to the pass's end: dec_bwd start skew 1.4 us median at c2, 17 us
+  // at c5)
+  __shared__ double sh[4];
   double acc = 0.0;
-  // one wave per row (grid-stride over rows): coalesced row reads, no
-  // per-element 64-bit index division
-  const int nwv = gridDim.x * (blockDim.x >> 6);
-  for (long r = blockIdx.x * (long)(blockDim.x >> 6) + (threadIdx.x >> 6); r < L; r += nwv)
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long r0 = (long)blockIdx.x * NLL_ROWS + w * (NLL_ROWS / 4);
+#pragma unroll
+  for (int i = 0; i < NLL_ROWS / 4; ++i) {
+    const long r = r0 + i;
+    if (r < L)
 #pragma unroll 3
-    for (int j = threadIdx.x & 63; j < F; j += 64) {
-      const float mu = MU[r * Fp + j], lv = LV[r * Fp + j], d = Y[r * F + j] - mu;
-      acc += 0.5f * (1.8378770664093453f + lv + d * d * __expf(-lv));
-    }
+      for (int j = lane; j < F; j += 64) {
+        const float mu = MU[r * Fp + j], lv = LV[r * Fp + j], d = Y[r * F + j] - mu;
+        acc += 0.5f * (1.8378770664093453f + lv + d * d * __expf(-lv));
+      }
+  }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) sh[w] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += sh[k];
-    part[blockIdx.x] = t;
-  }
+  if (threadIdx.x == 0) part[blockIdx.x] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
 }
 __global__ void sum_partials(const double* part, int np, float* out) {
   __shared__ double sh[4];
@@ -1102,7 +1109,7 @@ static DecWS carve_decoder(Arena& A, const abcd_decoder_cfg* c, int T, int L, in
   w.EPS = A.f((size_t)L * F);
   w.Zo = A.f((size_t)L * Hm); w.offlog = A.f(L); w.dlog_raw = A.f(L); w.bce = A.f(L);
   w.offpart = A.f((size_t)L * offset_head_slices(Hm));
-  w.part = A.d(2048);
+  w.part = A.d(1024 + (size_t)std::max(1, cdiv(L, NLL_ROWS)));  // [0, 1024): bce reduction; then the NLL partials
   w.dGX = A.f((size_t)L * GH);
   w.dGH = G == 4 ? w.dGX : A.f((size_t)L * GH);
   w.DC = A.f((size_t)L * H); w.DC0 = A.f((size_t)B * H); w.dH0 = A.f((size_t)B * H);
@@ -1383,13 +1390,13 @@ static int dec_forward_impl(const abcd_decoder_cfg* c, const abcd_decoder_params
   const bool em_loss = losses && x->data, off_loss = losses && gt_offset;
   if (em_loss || off_loss) ABCD_TRY((hipError_t)stream_fork(s, sl, 4));
   if (em_loss) {
-    const int nbk = 1024;
-    dec_emission_nll<<<nbk, 1024, 0, sl>>>(w.MU, w.LV, Fp, x->data, F, L, w.part);  // 16 waves / block
+    const int nbk = std::max(1, cdiv(L, NLL_ROWS));
+    dec_emission_nll<<<nbk, 256, 0, sl>>>(w.MU, w.LV, Fp, x->data, F, L, w.part + 1024);
     ABCD_CHECK_LAUNCH();
-    sum_partials<<<1, 256, 0, sl>>>(w.part, nbk, losses);
+    sum_partials<<<1, 256, 0, sl>>>(w.part + 1024, nbk, losses);
     ABCD_CHECK_LAUNCH();
   }
-  if (off_loss) ABCD_TRY((hipError_t)reduce_sum(sl, w.bce, L, w.part + 1024, losses + 1, nullptr));
+  if (off_loss) ABCD_TRY((hipError_t)reduce_sum(sl, w.bce, L, w.part, losses + 1, nullptr));
   if (flatten_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.OUT, Fp, flatten_out, F, L); ABCD_CHECK_LAUNCH(); }
   if (mu_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.MU, Fp, mu_out, F, L); ABCD_CHECK_LAUNCH(); }
   if (lv_out) { unpad_rows<<<launch_grid((long)L * F), 256, 0, s>>>(w.LV, Fp, lv_out, F, L); ABCD_CHECK_LAUNCH(); }
